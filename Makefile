@@ -1,0 +1,44 @@
+# Build recipe (no cmake in the product path).  `make -j8` builds:
+#   real-time-ray-tracing_amd/lib/librtx.so   the product: HIP kernels for gfx950 + host runtime + C-ABI
+#   oracle/_build/liboracle.so                the CPU restatement (test infrastructure only)
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+PKG      := real-time-ray-tracing_amd
+CSRC     := $(PKG)/csrc
+LIBDIR   := $(PKG)/lib
+OBJDIR   := $(PKG)/lib/obj
+# -ffp-contract=off on host AND device: every expression rounds once per operation, as the
+# CPU oracle does (DESIGN.md §4 numerics policy).
+HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude -I$(CSRC)
+CXXFLAGS := -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude -I$(CSRC)
+
+HIP_SRCS := $(wildcard $(CSRC)/*.hip)
+CPP_SRCS := $(wildcard $(CSRC)/*.cpp)
+HDRS     := $(wildcard $(CSRC)/*.h) include/rtx_amd.h
+HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.hip.o,$(HIP_SRCS))
+CPP_OBJS := $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.cpp.o,$(CPP_SRCS))
+
+ORC_SRCS := $(wildcard oracle/*.cpp)
+ORC_HDRS := $(wildcard oracle/*.h) $(CSRC)/rtmath.h $(CSRC)/scene_gen.h
+
+all: $(LIBDIR)/librtx.so oracle/_build/liboracle.so
+
+$(OBJDIR)/%.hip.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(filter-out --offload-arch=gfx950,$(HIPFLAGS)) -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -x c++ -c $< -o $@
+
+$(LIBDIR)/librtx.so: $(HIP_OBJS) $(CPP_OBJS)
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^ -ldl
+
+oracle/_build/liboracle.so: $(ORC_SRCS) $(ORC_HDRS) $(CSRC)/scene_gen.cpp
+	@mkdir -p oracle/_build
+	$(CXX) $(CXXFLAGS) -shared -o $@ $(ORC_SRCS) $(CSRC)/scene_gen.cpp -lpthread
+
+clean:
+	rm -rf $(LIBDIR) oracle/_build
+
+.PHONY: all clean

@@ -1,0 +1,199 @@
+/* rtx_amd.h — C-ABI of the MI355X-native real-time path tracer (librtx.so).
+ *
+ * Drop-in boundary for the reference's renderer API, class RayTracer
+ * (/root/reference/src/kernel.cuh:431-470) and its config surface LoadConfig
+ * (configLoader.cpp:5-27).  Plain C: opaque handle, plain pointers and sizes, status codes
+ * instead of the reference's exit() on errors (cudaError.cuh:6-13).  Not thread-safe per
+ * handle (same as the reference).  All output buffers are caller-owned host memory.
+ *
+ * Every entry point below names the reference interface it replaces.
+ */
+#ifndef RTX_AMD_H
+#define RTX_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK 0
+#define RT_ERR_ARG (-1)         /* invalid argument / size */
+#define RT_ERR_HIP (-2)         /* HIP runtime error (rt_last_error has the text) */
+#define RT_ERR_IO (-3)          /* config / data file problem */
+#define RT_ERR_STATE (-4)       /* call out of order (e.g. draw before init) */
+#define RT_ERR_NO_DEVICE (-5)   /* no gfx950 device visible */
+
+typedef struct rt_context rt_context;
+
+/* ---------------------------------------------------------------- lifecycle */
+
+/* RayTracer::RayTracer(screenWidth, screenHeight), kernel.cuh:435-441, plus LoadConfig
+ * (configLoader.cpp:5-27).  config_toml may be NULL (defaults) or a path to a TOML file with
+ * the reference's [resolution] / [file] / [optimziation] tables; extensions: [scene]
+ * chunkDim (VoxelsGenerator::kChunkDim, terrain.h:42), [render] spp, [render] device. */
+int rt_create(int screen_width, int screen_height, const char* config_toml, rt_context** out);
+
+/* RayTracer::init, init.cu:53-410: builds the procedural default scene (or loads
+ * [file] inputMeshFileName when it is a meshProcessor .bin), allocates every device
+ * resource, uploads blue-noise/sky tables, runs the frame-1 smooth normals. */
+int rt_init(rt_context* ctx);
+
+/* RayTracer::draw, kernel.cu:259-398: one synchronous frame.  rgba8_out (screen W*H*4)
+ * and hdr_out (render W*H*4 floats, pre-tone-map HDR) may each be NULL. */
+int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out);
+
+/* RayTracer::cleanup + ~RayTracer, init.cu:601-663, kernel.cuh:443-446 */
+void rt_destroy(rt_context* ctx);
+
+/* last error text for this handle (NULL handle: last rt_create failure) */
+const char* rt_last_error(const rt_context* ctx);
+
+/* ---------------------------------------------------------------- parameter surface */
+
+/* SkyParams, settingParams.h:26-47 */
+typedef struct rt_sky_params {
+    int32_t needRegenerate;
+    float timeOfDay, sunAxisAngle, skyScalar, sunScalar, sunAngle;
+} rt_sky_params;
+
+/* SampleParams, settingParams.h:49-66 */
+typedef struct rt_sample_params {
+    int32_t sampleSurfaceVsLightUseMisWeight, sampleSkyVsSunUseFluxWeight;
+    float sampleSurfaceVsLight, sampleSkyVsSun;
+} rt_sample_params;
+
+/* RenderPassSettings, settingParams.h:68-104 */
+typedef struct rt_render_pass_settings {
+    int32_t enableTemporalDenoising, enableLocalSpatialFilter, enableNoiseLevelVisualize, enableWideSpatialFilter,
+        enableTemporalDenoising2, enablePostProcess, enableDownScalePasses, enableHistogram, enableAutoExposure,
+        enableBloomEffect, enableLensFlare, enableToneMapping, enableSharpening;
+} rt_render_pass_settings;
+
+/* PostProcessParams, settingParams.h:106-124 (toneMappingType: 0 Uncharted, 1 ACES1,
+ * 2 ACES2, 3 Reinhard) */
+typedef struct rt_post_process_params {
+    int32_t toneMappingType;
+    float exposure, gain, maxWhite, gamma;
+} rt_post_process_params;
+
+/* DenoisingParams, settingParams.h:126-157 */
+typedef struct rt_denoising_params {
+    float local_denoise_sigma_normal, local_denoise_sigma_depth, local_denoise_sigma_material;
+    float large_denoise_sigma_normal, large_denoise_sigma_depth, large_denoise_sigma_material;
+    float temporal_denoise_sigma_normal, temporal_denoise_sigma_depth, temporal_denoise_sigma_material;
+    float noise_threshold_local, noise_threshold_large;
+} rt_denoising_params;
+
+/* public members skyParams .. sampleParams, kernel.cuh:465-470 */
+typedef struct rt_params {
+    rt_sky_params sky;
+    rt_sample_params sample;
+    rt_render_pass_settings pass;
+    rt_post_process_params post;
+    rt_denoising_params denoise;
+} rt_params;
+
+int rt_get_params(const rt_context* ctx, rt_params* out);
+int rt_set_params(rt_context* ctx, const rt_params* in);
+
+/* Camera fields the app sets (init.cu:412-439, kernel.cuh:78-121); fovX in radians */
+typedef struct rt_camera {
+    float pos[3];
+    float yaw, pitch;
+    float focal, aperture;
+    float fovX;
+} rt_camera;
+
+int rt_get_camera(const rt_context* ctx, rt_camera* out); /* RayTracer::GetCamera */
+int rt_set_camera(rt_context* ctx, const rt_camera* in);
+
+/* Determinism hooks the reference lacks: the frame counter is a function static
+ * (kernel.cu:64) and AutoExposure reads wall-clock deltaTime (postprocessing.cu:46-51). */
+int rt_set_frame_index(rt_context* ctx, int frame_num); /* next rt_draw renders this frameNum */
+int rt_set_delta_time(rt_context* ctx, float ms);       /* <= 0: wall clock */
+
+/* ---------------------------------------------------------------- queries */
+
+typedef struct rt_info {
+    uint32_t triCount;          /* real triangles */
+    uint32_t triCountPadded;    /* RayTracer::GetTriangleCount (kernel.cuh:462) */
+    uint32_t batchCount;        /* BLAS batches of 1024 */
+    uint32_t vertexCount;
+    int32_t renderWidth, renderHeight, screenWidth, screenHeight;
+    int32_t frameNum;           /* frame index of the last rt_draw (0 before the first) */
+    int32_t deviceId;
+    uint32_t spp;               /* samples (reference PathTrace evaluations) per frame */
+} rt_info;
+
+int rt_get_info(const rt_context* ctx, rt_info* out);
+
+/* GetBuffer2D, kernel.cuh:459: copies a render buffer to host memory.  Names follow the
+ * Buffer2DName enum (kernel.cuh:286-315); half buffers come back as uint16 bit patterns. */
+enum rt_buffer_name {
+    RT_BUF_RENDER_COLOR = 0,   /* half4 (rgb + ushort material mask), render res */
+    RT_BUF_ACCUMULATION = 1,   /* half4 */
+    RT_BUF_HISTORY_COLOR = 2,  /* half4 */
+    RT_BUF_SCALED_COLOR = 3,   /* half4, screen res */
+    RT_BUF_NORMAL = 10,        /* half4 */
+    RT_BUF_DEPTH = 11,         /* half */
+    RT_BUF_HISTORY_DEPTH = 12, /* half */
+    RT_BUF_MOTION = 13,        /* half2 */
+    RT_BUF_NOISE_LEVEL = 14,   /* half, 8x8-tile grid */
+    RT_BUF_NOISE_LEVEL16 = 15, /* half, 16x16-tile grid */
+    RT_BUF_SKY = 16,           /* float4 512x256 */
+    RT_BUF_SUN = 17,           /* float4 32x32 */
+    RT_BUF_ALBEDO = 18         /* half4 */
+};
+int rt_get_buffer(const rt_context* ctx, int name, void* dst, size_t bytes);
+
+/* ---------------------------------------------------------------- hot-path stages */
+
+/* BuildBvhLevel1 + BuildBvhLevel2 (bvh.cu:7-97): one per-frame two-level LBVH rebuild,
+ * enqueued on the context stream (asynchronous). */
+int rt_build_bvh(rt_context* ctx);
+
+/* BASELINE config 2: GenerateRay + RaySceneIntersect for every render pixel with the
+ * blue-noise sample of frame_num (pathtrace.cuh:116-130), enqueued asynchronously.
+ * with_detail != 0 also stores normals / shading normals / traversal counters. */
+int rt_trace_primary(rt_context* ctx, int frame_num, int with_detail);
+
+/* wait for all work on the context stream */
+int rt_sync(rt_context* ctx);
+
+/* HIP-event timing on the context stream: runs `iters` back-to-back launches of a stage
+ * (0 = BVH build, 1 = primary rays, 2 = path trace, 3 = full frame) and returns the total
+ * milliseconds between the first launch and the end of the last. */
+int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms);
+
+/* Copies device arrays to host (debug dumps of bvh.cu:15-96, traversal outputs). */
+enum rt_array_name {
+    RT_ARR_VERTICES = 0,         /* float[nv][3] */
+    RT_ARR_INDICES = 1,          /* uint32[triCountPadded][3] */
+    RT_ARR_NORMALS = 2,          /* float[nv][3] (smooth normals) */
+    RT_ARR_TRI_POS = 3,          /* float4[triCountPadded][3] */
+    RT_ARR_AABBS = 4,            /* float[triCountPadded][6] min xyz max xyz */
+    RT_ARR_MORTON = 5,           /* uint32[B*1024] sorted codes (morton2.csv) */
+    RT_ARR_REORDER = 6,          /* uint32[B*1024] (reorderIdx.csv) */
+    RT_ARR_NODES = 7,            /* 64-B nodes [triCountPadded]: lmin lmax rmin rmax (12 f32), idxL idxR leafL leafR */
+    RT_ARR_TLAS_AABBS = 8,       /* float[B][6] */
+    RT_ARR_TLAS_MORTON = 9,      /* uint32[1024] sorted */
+    RT_ARR_TLAS_REORDER = 10,    /* uint32[1024] */
+    RT_ARR_TLAS_NODES = 11,      /* 64-B nodes [B] */
+    RT_ARR_TLAS_SCENE_AABB = 12, /* float[6] */
+    RT_ARR_BATCH_SCENE_AABBS = 13, /* float[B][6] */
+    RT_ARR_HITS = 14,            /* float4[W*H]: t, objectIdx (int bits), u, v */
+    RT_ARR_HIT_NORMALS = 15,     /* float4[W*H]: geometric normal, hit flag */
+    RT_ARR_HIT_FAKE_NORMALS = 16,/* float4[W*H]: shading normal, ray offset */
+    RT_ARR_HIT_STATS = 17,       /* uint32[W*H][4]: node visits, tri tests, dropped pushes, iterations */
+    RT_ARR_TRI_NRM = 18          /* float4[triCountPadded][3] */
+};
+int rt_download(const rt_context* ctx, int what, void* dst, size_t bytes);
+size_t rt_array_bytes(const rt_context* ctx, int what);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTX_AMD_H */

@@ -1,0 +1,141 @@
+// ORACLE — CPU restatement of the reference's hot path.  TEST INFRASTRUCTURE ONLY.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this code,
+// and only as the checker / CPU baseline.  The product (librtx.so) never links it.
+//
+// Parity pinning: the reference is CUDA (sm_75) with no nvcc in this image and no CPU
+// build of its own; it cannot be compiled here without writing a cuda_runtime.h stand-in,
+// which this pipeline forbids, so oracle/_ref is unbuildable.  The
+// restatement is pinned by the known-answer values SURVEY.md §0/§8c recorded from the
+// reference's own per-thread code (triangle/traversal probes, Morton codes, scene counts,
+// tree depths, the TLAS reduction quirk box) — tests/test_oracle_pins.py — and is
+// otherwise "parity unpinned" against NVIDIA binaries (libdevice transcendentals and
+// nvcc's default FMA contraction are not reproducible without nvcc).
+//
+// Numerics policy (shared with the HIP kernels): every expression is evaluated in source
+// order with one rounding per operation (-ffp-contract=off); explicit fmaf only where the
+// reference calls fma (linearMath.h:41-98); transcendentals from rtmath.h.
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../real-time-ray-tracing_amd/csrc/rtmath.h"
+
+namespace orc {
+
+static const float kFltMax = 3.402823466e+38f;
+static const float kRayMax = 10e10f;                    // kernel.cuh:69
+static const float kMachineEps = 1.1920928955078125e-07f;  // precision.cuh:18-23
+
+struct F2 { float x, y; };
+struct F3 {
+    float x, y, z;
+    float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+    float& operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+};
+
+static inline F3 f3(float x, float y, float z) { F3 r = {x, y, z}; return r; }
+static inline F3 f3(float a) { F3 r = {a, a, a}; return r; }
+static inline F3 operator+(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline F3 operator-(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline F3 operator*(F3 a, F3 b) { return f3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline F3 operator/(F3 a, F3 b) { return f3(a.x / b.x, a.y / b.y, a.z / b.z); }
+static inline F3 operator+(F3 a, float b) { return f3(a.x + b, a.y + b, a.z + b); }
+static inline F3 operator-(F3 a, float b) { return f3(a.x - b, a.y - b, a.z - b); }
+static inline F3 operator*(F3 a, float b) { return f3(a.x * b, a.y * b, a.z * b); }
+static inline F3 operator/(F3 a, float b) { return f3(a.x / b, a.y / b, a.z / b); }
+static inline F3 operator*(float b, F3 a) { return f3(a.x * b, a.y * b, a.z * b); }
+static inline F3 operator-(F3 a) { return f3(-a.x, -a.y, -a.z); }
+
+// linearMath.h:27-31 — ternary min/max (operand order matters for NaN and signed zero)
+static inline float fmx(float a, float b) { return a > b ? a : b; }
+static inline float fmn(float a, float b) { return a < b ? a : b; }
+static inline F3 max3(F3 a, F3 b) { return f3(fmx(a.x, b.x), fmx(a.y, b.y), fmx(a.z, b.z)); }
+static inline F3 min3(F3 a, F3 b) { return f3(fmn(a.x, b.x), fmn(a.y, b.y), fmn(a.z, b.z)); }
+// max1f/min1f (linearMath.h:247-248)
+static inline float max1f(float a, float b) { return (a < b) ? b : a; }
+static inline float min1f(float a, float b) { return (a > b) ? b : a; }
+static inline F3 abs3(F3 a) { return f3(fabsf(a.x), fabsf(a.y), fabsf(a.z)); }
+
+// error-free transforms (linearMath.h:41-91)
+static inline float dop(float a, float b, float c, float d) {
+    float cd = c * d;
+    float err = fmaf(-c, d, cd);
+    float dp = fmaf(a, b, -cd);
+    return dp + err;
+}
+struct CF { float v, err; };
+static inline CF two_prod(float a, float b) { float ab = a * b; CF r = {ab, fmaf(a, b, -ab)}; return r; }
+static inline CF two_sum(float a, float b) {
+    float s = a + b, delta = s - a;
+    CF r = {s, (a - (s - delta)) + (b - delta)};
+    return r;
+}
+// InnerProduct(a,b,c,d,e,f) cast to float
+static inline float inner3(float a, float b, float c, float d, float e, float f) {
+    CF ef = two_prod(e, f);
+    CF cd = two_prod(c, d);
+    CF s2 = two_sum(cd.v, ef.v);
+    CF tp = {s2.v, cd.err + (ef.err + s2.err)};
+    CF ab = two_prod(a, b);
+    CF s1 = two_sum(ab.v, tp.v);
+    CF r = {s1.v, ab.err + (tp.err + s1.err)};
+    return r.v + r.err;
+}
+static inline float dot(F3 a, F3 b) { return inner3(a.x, b.x, a.y, b.y, a.z, b.z); }
+static inline F3 cross(F3 a, F3 b) {
+    return f3(dop(a.y, b.z, a.z, b.y), dop(a.z, b.x, a.x, b.z), dop(a.x, b.y, a.y, b.x));
+}
+static inline float length2(F3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+static inline F3 normalize(F3 v) {
+    float n = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
+    return f3(v.x / n, v.y / n, v.z / n);
+}
+static inline float safe_divide(float a, float b) {
+    const float eps = 1e-20f;
+    return a / ((fabsf(b) > eps) ? b : copysignf(eps, b));
+}
+
+// CUDA cvt.rzi.u32.f32 semantics: NaN/negative -> 0, >= 2^32 -> UINT_MAX
+static inline uint32_t sat_u32(float x) {
+    if (!(x > 0.0f)) return 0u;
+    if (x >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)x;
+}
+
+struct AABB { F3 min, max; };
+static inline AABB aabb_empty() { AABB r = {f3(kFltMax), f3(-kFltMax)}; return r; }
+static inline float aabb_at(const AABB& b, int i) { return i < 3 ? b.min[i] : b.max[i - 3]; }
+
+// canonical BVH node (64 B): left box, right box, children, leaf flags
+struct Node {
+    float lmin[3], lmax[3], rmin[3], rmax[3];
+    uint32_t idxLeft, idxRight, isLeftLeaf, isRightLeaf;
+};
+static inline AABB node_left(const Node& n) {
+    AABB b = {f3(n.lmin[0], n.lmin[1], n.lmin[2]), f3(n.lmax[0], n.lmax[1], n.lmax[2])};
+    return b;
+}
+static inline AABB node_right(const Node& n) {
+    AABB b = {f3(n.rmin[0], n.rmin[1], n.rmin[2]), f3(n.rmax[0], n.rmax[1], n.rmax[2])};
+    return b;
+}
+// AABBCompact::GetMerged (geometry.h:107-110): max(box1, box2), min(box1, box2)
+static inline AABB node_merged(const Node& n) {
+    AABB b;
+    for (int k = 0; k < 3; ++k) {
+        b.max[k] = fmx(n.lmax[k], n.rmax[k]);
+        b.min[k] = fmn(n.lmin[k], n.rmin[k]);
+    }
+    return b;
+}
+static inline void node_set_boxes(Node& n, const AABB& l, const AABB& r) {
+    for (int k = 0; k < 3; ++k) {
+        n.lmin[k] = l.min[k]; n.lmax[k] = l.max[k];
+        n.rmin[k] = r.min[k]; n.rmax[k] = r.max[k];
+    }
+}
+
+}  // namespace orc

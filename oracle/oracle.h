@@ -1,0 +1,90 @@
+// ORACLE C API — test infrastructure only (see ocommon.h header comment).
+// Loaded by tests/ and bench.py's cpu_baseline through ctypes (oracle/_build/liboracle.so).
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct OrcBvhIO {
+    // inputs
+    const float* vertices;   // [nverts][3]
+    const float* normals;    // [nverts][3] or NULL
+    const uint32_t* indices; // [triCountPadded][3]
+    uint32_t triCount;
+    uint32_t triCountPadded;
+    // outputs (caller allocated; B = ceil(triCount / 1024))
+    float* triangles;        // [triCountPadded][18]  v1 v2 v3 n1 n2 n3
+    float* aabbs;            // [triCountPadded][6]   min xyz, max xyz
+    uint32_t* mortonUnsorted;  // [B*1024]
+    uint32_t* mortonSorted;    // [B*1024]
+    uint32_t* reorderIdx;      // [B*1024]
+    void* nodes;               // [triCountPadded] canonical 64-B nodes
+    float* batchSceneAabbs;    // [B][6]
+    float* tlasAabbs;          // [B][6]
+    float* tlasSceneAabb;      // [6] the (quirky) reduction box used for TLAS Morton codes
+    uint32_t* tlasMortonUnsorted;  // [1024]
+    uint32_t* tlasMortonSorted;    // [1024]
+    uint32_t* tlasReorderIdx;      // [1024]
+    void* tlasNodes;               // [B]
+} OrcBvhIO;
+
+// returns B (>0) or a negative error
+int orc_build_bvh(const OrcBvhIO* io);
+uint32_t orc_morton3(uint32_t x, uint32_t y, uint32_t z);
+
+// GenerateSmoothNormals x2 (kernel.cu:228-257, 313-327) accumulated in triangle order into
+// a zeroed buffer. normals: [nverts][3] output.
+void orc_smooth_normals(const float* vertices, uint32_t nverts, const uint32_t* indices, uint32_t triCountPadded,
+                        float* normals);
+
+typedef struct OrcScene {
+    const float* triangles;  // [triCountPadded][18] as written by orc_build_bvh
+    const void* nodes;       // BLAS canonical nodes [triCountPadded]
+    const void* tlasNodes;   // [B]
+    uint32_t triCountPadded;
+    uint32_t batchCount;
+} OrcScene;
+
+typedef struct OrcHit {
+    float t;
+    int32_t objectIdx;
+    float u, v;
+    float normal[3];      // geometric normal, flipped to face the ray (traverse.cuh:193-199)
+    float fakeNormal[3];  // interpolated shading normal, flipped likewise
+    float pos[3];         // re-projected hit point (geometry.cuh:252-262)
+    float offset;         // errT + errP
+    uint32_t hit;
+    uint32_t nodeVisits;  // internal-node box-pair tests
+    uint32_t triTests;    // ray/triangle tests
+    uint32_t droppedPushes;  // pushes lost to the 16-entry stack (traverse.h:34-36)
+    uint32_t iterations;     // loop iterations used (cap 1024, traverse.h:132)
+} OrcHit;
+
+// RaySceneIntersect core (traverse.cuh:64-225 without the material bookkeeping) for n rays.
+// rays: [n][6] orig xyz, dir xyz.  threads: host threads to use (0 = all).
+void orc_intersect(const OrcScene* scene, const float* rays, uint32_t n, OrcHit* hits, int threads);
+
+typedef struct OrcCamera {
+    float pos[3];
+    float yaw, pitch;
+    float focal, aperture;
+    float fovX;          // radians
+    float resolution[2]; // render width, height
+} OrcCamera;
+
+// Camera::update + GenerateRay with blue-noise sample frameNum*4+0 (pathtrace.cuh:40-59,
+// raygen.cuh:7-38).  rays: [W*H][6]; also writes the per-pixel ray-cone spread if non-NULL.
+void orc_primary_rays(const OrcCamera* cam, uint32_t W, uint32_t H, int frameNum, const uint8_t* bluenoise,
+                      float* rays, float* coneSpread);
+
+// Blue-noise sampler (blueNoiseRandGen.h:113-146): value for pixel, sample index, dimension.
+float orc_bluenoise(const uint8_t* tables, int px, int py, int sampleIdx, int dim);
+
+// deterministic math probes (rtmath.h), for tests
+float orc_rtmath(int fn, float x, float y);
+
+#ifdef __cplusplus
+}
+#endif

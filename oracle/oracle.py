@@ -1,0 +1,168 @@
+"""ORACLE — ctypes wrapper of oracle/_build/liboracle.so (CPU restatement of the reference).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, always as the checker / CPU baseline, never as the measured product.
+See oracle/ocommon.h for what it restates and how it is pinned.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+DATA_DIR = os.path.join(os.path.dirname(HERE), "real-time-ray-tracing_amd", "data")
+
+NODE_DTYPE = np.dtype([("lmin", "<f4", 3), ("lmax", "<f4", 3), ("rmin", "<f4", 3), ("rmax", "<f4", 3),
+                       ("idxLeft", "<u4"), ("idxRight", "<u4"), ("isLeftLeaf", "<u4"), ("isRightLeaf", "<u4")])
+
+
+class BvhIO(C.Structure):
+    _fields_ = [("vertices", C.c_void_p), ("normals", C.c_void_p), ("indices", C.c_void_p),
+                ("triCount", C.c_uint32), ("triCountPadded", C.c_uint32),
+                ("triangles", C.c_void_p), ("aabbs", C.c_void_p), ("mortonUnsorted", C.c_void_p),
+                ("mortonSorted", C.c_void_p), ("reorderIdx", C.c_void_p), ("nodes", C.c_void_p),
+                ("batchSceneAabbs", C.c_void_p), ("tlasAabbs", C.c_void_p), ("tlasSceneAabb", C.c_void_p),
+                ("tlasMortonUnsorted", C.c_void_p), ("tlasMortonSorted", C.c_void_p),
+                ("tlasReorderIdx", C.c_void_p), ("tlasNodes", C.c_void_p)]
+
+
+class Scene(C.Structure):
+    _fields_ = [("triangles", C.c_void_p), ("nodes", C.c_void_p), ("tlasNodes", C.c_void_p),
+                ("triCountPadded", C.c_uint32), ("batchCount", C.c_uint32)]
+
+
+HIT_DTYPE = np.dtype([("t", "<f4"), ("objectIdx", "<i4"), ("u", "<f4"), ("v", "<f4"), ("normal", "<f4", 3),
+                      ("fakeNormal", "<f4", 3), ("pos", "<f4", 3), ("offset", "<f4"), ("hit", "<u4"),
+                      ("nodeVisits", "<u4"), ("triTests", "<u4"), ("droppedPushes", "<u4"),
+                      ("iterations", "<u4")])
+
+
+class CameraIn(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("yaw", C.c_float), ("pitch", C.c_float), ("focal", C.c_float),
+                ("aperture", C.c_float), ("fovX", C.c_float), ("resolution", C.c_float * 2)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("oracle not built: %s (run make)" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        L.orc_build_bvh.argtypes = [C.POINTER(BvhIO)]
+        L.orc_build_bvh.restype = C.c_int
+        L.orc_morton3.argtypes = [C.c_uint32] * 3
+        L.orc_morton3.restype = C.c_uint32
+        L.orc_smooth_normals.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
+        L.orc_smooth_normals.restype = None
+        L.orc_intersect.argtypes = [C.POINTER(Scene), C.c_void_p, C.c_uint32, C.c_void_p, C.c_int]
+        L.orc_intersect.restype = None
+        L.orc_primary_rays.argtypes = [C.POINTER(CameraIn), C.c_uint32, C.c_uint32, C.c_int, C.c_void_p,
+                                       C.c_void_p, C.c_void_p]
+        L.orc_primary_rays.restype = None
+        L.orc_bluenoise.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.orc_bluenoise.restype = C.c_float
+        L.orc_rtmath.argtypes = [C.c_int, C.c_float, C.c_float]
+        L.orc_rtmath.restype = C.c_float
+        L.orc_scene_generate.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                         C.POINTER(C.c_uint32)]
+        L.orc_scene_generate.restype = C.c_int
+        L.orc_scene_copy.argtypes = [C.c_void_p, C.c_void_p]
+        L.orc_scene_copy.restype = None
+        _lib = L
+    return _lib
+
+
+def scene(chunk_dim: int = 1):
+    """Procedural default scene (input generator): (vertices [nv,3] f32, indices [NP,3] u32, triCount)."""
+    L = lib()
+    n, npad, nv = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    rc = L.orc_scene_generate(os.path.join(DATA_DIR, "roundcubes_l2.bin").encode(), chunk_dim, C.byref(n),
+                              C.byref(npad), C.byref(nv))
+    if rc != 0:
+        raise RuntimeError("scene generation failed (%d)" % rc)
+    v = np.empty((nv.value, 3), np.float32)
+    i = np.empty((npad.value, 3), np.uint32)
+    L.orc_scene_copy(v.ctypes.data, i.ctypes.data)
+    return v, i, n.value
+
+
+def smooth_normals(vertices: np.ndarray, indices: np.ndarray) -> np.ndarray:
+    out = np.empty_like(vertices)
+    lib().orc_smooth_normals(vertices.ctypes.data, vertices.shape[0], indices.ctypes.data, indices.shape[0],
+                             out.ctypes.data)
+    return out
+
+
+def build_bvh(vertices, indices, tri_count, normals=None) -> dict:
+    NP = indices.shape[0]
+    B = (tri_count + 1023) // 1024
+    out = dict(
+        triangles=np.zeros((NP, 18), np.float32), aabbs=np.zeros((NP, 6), np.float32),
+        morton_unsorted=np.zeros(B * 1024, np.uint32), morton=np.zeros(B * 1024, np.uint32),
+        reorder=np.zeros(B * 1024, np.uint32), nodes=np.zeros(NP, NODE_DTYPE),
+        batch_scene_aabbs=np.zeros((B, 6), np.float32), tlas_aabbs=np.zeros((B, 6), np.float32),
+        tlas_scene_aabb=np.zeros(6, np.float32), tlas_morton_unsorted=np.zeros(1024, np.uint32),
+        tlas_morton=np.zeros(1024, np.uint32), tlas_reorder=np.zeros(1024, np.uint32),
+        tlas_nodes=np.zeros(B, NODE_DTYPE))
+    io = BvhIO(vertices.ctypes.data, normals.ctypes.data if normals is not None else None, indices.ctypes.data,
+               tri_count, NP, out["triangles"].ctypes.data, out["aabbs"].ctypes.data,
+               out["morton_unsorted"].ctypes.data, out["morton"].ctypes.data, out["reorder"].ctypes.data,
+               out["nodes"].ctypes.data, out["batch_scene_aabbs"].ctypes.data, out["tlas_aabbs"].ctypes.data,
+               out["tlas_scene_aabb"].ctypes.data, out["tlas_morton_unsorted"].ctypes.data,
+               out["tlas_morton"].ctypes.data, out["tlas_reorder"].ctypes.data, out["tlas_nodes"].ctypes.data)
+    rc = lib().orc_build_bvh(C.byref(io))
+    if rc < 0:
+        raise RuntimeError("orc_build_bvh failed (%d)" % rc)
+    out["batch_count"] = rc
+    out["tri_count"] = tri_count
+    return out
+
+
+def intersect(bvh: dict, rays: np.ndarray, threads: int = 0) -> np.ndarray:
+    rays = np.ascontiguousarray(rays, dtype=np.float32)
+    n = rays.shape[0]
+    hits = np.zeros(n, HIT_DTYPE)
+    sc = Scene(bvh["triangles"].ctypes.data, bvh["nodes"].ctypes.data, bvh["tlas_nodes"].ctypes.data,
+               bvh["triangles"].shape[0], bvh["batch_count"])
+    lib().orc_intersect(C.byref(sc), rays.ctypes.data, n, hits.ctypes.data, threads)
+    return hits
+
+
+def default_camera(width: int, height: int) -> CameraIn:
+    # CameraSetup, init.cu:412-439
+    c = CameraIn()
+    c.pos[:] = (-2.0, 2.0, -2.0)
+    c.yaw = 0.0
+    c.pitch = 0.0
+    c.focal = 5.0
+    c.aperture = 0.001
+    c.fovX = np.float32(90.0) * np.float32(0.01745329251)
+    c.resolution[:] = (float(width), float(height))
+    return c
+
+
+def bluenoise_tables() -> np.ndarray:
+    return np.fromfile(os.path.join(DATA_DIR, "bluenoise_4spp.bin"), dtype=np.uint8)
+
+
+def primary_rays(width: int, height: int, frame_num: int = 1, cam: CameraIn | None = None):
+    cam = cam or default_camera(width, height)
+    bn = bluenoise_tables()
+    rays = np.zeros((width * height, 6), np.float32)
+    cone = np.zeros(width * height, np.float32)
+    lib().orc_primary_rays(C.byref(cam), width, height, frame_num, bn.ctypes.data, rays.ctypes.data,
+                           cone.ctypes.data)
+    return rays, cone
+
+
+RTMATH = dict(sin=0, cos=1, tan=2, atan=3, atan2=4, acos=5, asin=6, exp=7, exp2=8, log=9, log2=10, pow=11)
+
+
+def rtmath(fn: str, x: float, y: float = 0.0) -> float:
+    return lib().orc_rtmath(RTMATH[fn], x, y)

@@ -1,0 +1,556 @@
+// context.cpp — RayTracer lifecycle, scene setup and hot-path stage dispatch behind the C-ABI.
+//
+//   rt_create  <- RayTracer::RayTracer + LoadConfig   (kernel.cuh:435-441, configLoader.cpp:5-27)
+//   rt_init    <- RayTracer::init                    (init.cu:53-410)
+//   rt_destroy <- RayTracer::cleanup                 (init.cu:601-663)
+//   rt_build_bvh / rt_trace_primary <- BuildBvhLevel1/2 (bvh.cu:7-97) / PathTrace's first hit
+#include "context.h"
+
+#include <dlfcn.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <fstream>
+#include <sstream>
+
+#include "rtmath.h"
+#include "toml_lite.h"
+
+namespace {
+
+thread_local std::string g_createError;
+
+#define HIP_TRY(ctx, expr)                                                            \
+    do {                                                                              \
+        hipError_t e__ = (expr);                                                      \
+        if (e__ != hipSuccess) {                                                      \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e__);          \
+            return RT_ERR_HIP;                                                        \
+        }                                                                             \
+    } while (0)
+
+template <typename T>
+int dalloc(rt_context* ctx, T** p, size_t bytes) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, bytes < 16 ? 16 : bytes);
+    if (e != hipSuccess) {
+        ctx->err = std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e);
+        return RT_ERR_HIP;
+    }
+    ctx->allocations.push_back(q);
+    *p = (T*)q;
+    return RT_OK;
+}
+
+void default_params(rt_params& p) {
+    // settingParams.h defaults
+    p.sky.needRegenerate = 1;
+    p.sky.timeOfDay = 0.25f;
+    p.sky.sunAxisAngle = 45.0f;
+    p.sky.skyScalar = 0.01f;
+    p.sky.sunScalar = 0.01f;
+    p.sky.sunAngle = 0.6f;
+    p.sample.sampleSurfaceVsLightUseMisWeight = 1;
+    p.sample.sampleSkyVsSunUseFluxWeight = 1;
+    p.sample.sampleSurfaceVsLight = 0.5f;
+    p.sample.sampleSkyVsSun = 0.5f;
+    p.pass.enableTemporalDenoising = 1;
+    p.pass.enableLocalSpatialFilter = 1;
+    p.pass.enableNoiseLevelVisualize = 0;
+    p.pass.enableWideSpatialFilter = 1;
+    p.pass.enableTemporalDenoising2 = 1;
+    p.pass.enablePostProcess = 1;
+    p.pass.enableDownScalePasses = 1;
+    p.pass.enableHistogram = 1;
+    p.pass.enableAutoExposure = 1;
+    p.pass.enableBloomEffect = 0;
+    p.pass.enableLensFlare = 0;
+    p.pass.enableToneMapping = 1;
+    p.pass.enableSharpening = 1;
+    p.post.toneMappingType = 3;
+    p.post.exposure = 1.0f;
+    p.post.gain = 40.0f;
+    p.post.maxWhite = 7.0f;
+    p.post.gamma = 2.2f;
+    p.denoise.local_denoise_sigma_normal = 100.0f;
+    p.denoise.local_denoise_sigma_depth = 0.1f;
+    p.denoise.local_denoise_sigma_material = 100.0f;
+    p.denoise.large_denoise_sigma_normal = 100.0f;
+    p.denoise.large_denoise_sigma_depth = 0.01f;
+    p.denoise.large_denoise_sigma_material = 100.0f;
+    p.denoise.temporal_denoise_sigma_normal = 100.0f;
+    p.denoise.temporal_denoise_sigma_depth = 0.1f;
+    p.denoise.temporal_denoise_sigma_material = 100.0f;
+    p.denoise.noise_threshold_local = 0.001f;
+    p.denoise.noise_threshold_large = 0.001f;
+}
+
+bool read_file(const std::string& path, std::string& out) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    std::stringstream ss;
+    ss << f.rdbuf();
+    out = ss.str();
+    return true;
+}
+
+// meshProcessor .bin (u32 count + Triangle[count], 128 B each: init.cu:28-50,
+// tool/meshProcessor.cpp:204-209) -> unshared vertex/index buffers
+bool load_triangle_bin(const std::string& path, rtscene::SceneMesh& m, std::string& err) {
+    std::string blob;
+    if (!read_file(path, blob) || blob.size() < 4) { err = "cannot read mesh file " + path; return false; }
+    uint32_t n = 0;
+    memcpy(&n, blob.data(), 4);
+    if (n < 2 || blob.size() < 4 + (size_t)n * 128) { err = "malformed mesh file " + path; return false; }
+    m.vertices.resize((size_t)n * 9);
+    m.indices.resize((size_t)n * 3);
+    for (uint32_t t = 0; t < n; ++t) {
+        const char* rec = blob.data() + 4 + (size_t)t * 128;
+        for (int k = 0; k < 3; ++k) {
+            memcpy(&m.vertices[((size_t)t * 3 + k) * 3], rec + 16 * k, 12);  // v1 w1 v2 w2 v3 w3
+            m.indices[(size_t)t * 3 + k] = t * 3 + k;
+        }
+    }
+    m.triCount = n;
+    m.triCountPadded = (n + 3u) & ~3u;
+    m.indices.resize((size_t)m.triCountPadded * 3, 0u);
+    m.cornerCount = n * 3;
+    return true;
+}
+
+}  // namespace
+
+std::string rt_data_dir() {
+    Dl_info info;
+    if (dladdr((void*)&rt_data_dir, &info) && info.dli_fname) {
+        std::string so = info.dli_fname;
+        size_t s = so.rfind('/');
+        std::string dir = s == std::string::npos ? std::string(".") : so.substr(0, s);
+        return dir + "/../data";
+    }
+    return "real-time-ray-tracing_amd/data";
+}
+
+// Camera::update (kernel.cuh:103-121), evaluated with the deterministic rtmath functions
+void rt_camera_update(const rt_camera& in, int renderW, int renderH, HostCamera& c) {
+    memcpy(c.pos, in.pos, sizeof(c.pos));
+    c.yaw = in.yaw;
+    c.pitch = in.pitch;
+    c.focal = in.focal;
+    c.aperture = in.aperture;
+    c.res[0] = (float)renderW;
+    c.res[1] = (float)renderH;
+    c.fov[0] = in.fovX;
+    const float sy = rt_sinf(c.yaw), cy = rt_cosf(c.yaw), sp = rt_sinf(c.pitch), cp = rt_cosf(c.pitch);
+    float dir[3] = {sy * cp, sp, cy * cp};
+    c.invRes[0] = 1.0f / c.res[0];
+    c.invRes[1] = 1.0f / c.res[1];
+    c.fov[1] = c.fov[0] / c.res[0] * c.res[1];
+    c.tanHalfFov[0] = rt_tanf(c.fov[0] / 2);
+    c.tanHalfFov[1] = rt_tanf(c.fov[1] / 2);
+    auto dopf = [](float a, float b, float cc, float d) {
+        float cd = cc * d;
+        float e = fmaf(-cc, d, cd);
+        float dp = fmaf(a, b, -cd);
+        return dp + e;
+    };
+    auto crossf = [&](const float* a, const float* b, float* r) {
+        r[0] = dopf(a[1], b[2], a[2], b[1]);
+        r[1] = dopf(a[2], b[0], a[0], b[2]);
+        r[2] = dopf(a[0], b[1], a[1], b[0]);
+    };
+    auto normf = [](float* v) {
+        float n = sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        v[0] = v[0] / n; v[1] = v[1] / n; v[2] = v[2] / n;
+    };
+    float up0[3] = {0.0f, 1.0f, 0.0f}, left[3], up[3];
+    crossf(up0, dir, left);
+    normf(left);
+    crossf(dir, left, up);
+    normf(up);
+    for (int k = 0; k < 3; ++k) {
+        c.dir[k] = dir[k];
+        c.left[k] = left[k];
+        c.up[k] = up[k];
+        c.adjustedFront[k] = dir[k] * c.focal;
+        c.adjustedLeft[k] = left[k] * c.tanHalfFov[0] * c.focal;
+        c.adjustedUp[k] = up[k] * c.tanHalfFov[1] * c.focal;
+        c.apertureLeft[k] = left[k] * c.aperture;
+        c.apertureUp[k] = up[k] * c.aperture;
+    }
+}
+
+TraceCamera rt_trace_camera(const HostCamera& c) {
+    TraceCamera t;
+    memcpy(t.pos, c.pos, 12);
+    memcpy(t.adjustedFront, c.adjustedFront, 12);
+    memcpy(t.adjustedLeft, c.adjustedLeft, 12);
+    memcpy(t.adjustedUp, c.adjustedUp, 12);
+    memcpy(t.apertureLeft, c.apertureLeft, 12);
+    memcpy(t.apertureUp, c.apertureUp, 12);
+    memcpy(t.invRes, c.invRes, 8);
+    return t;
+}
+
+extern "C" {
+
+const char* rt_last_error(const rt_context* ctx) { return ctx ? ctx->err.c_str() : g_createError.c_str(); }
+
+int rt_create(int screen_width, int screen_height, const char* config_toml, rt_context** out) {
+    if (!out) return RT_ERR_ARG;
+    *out = nullptr;
+    rt_context* ctx = new rt_context();
+    default_params(ctx->params);
+    // CameraSetup defaults (init.cu:412-439)
+    ctx->camera.pos[0] = -2.0f; ctx->camera.pos[1] = 2.0f; ctx->camera.pos[2] = -2.0f;
+    ctx->camera.yaw = 0.0f; ctx->camera.pitch = 0.0f;
+    ctx->camera.focal = 5.0f; ctx->camera.aperture = 0.001f;
+    ctx->camera.fovX = 90.0f * 0.01745329251f;
+    rttoml::Doc doc;
+    if (config_toml && config_toml[0]) {
+        std::string text, err;
+        if (!read_file(config_toml, text)) { g_createError = std::string("cannot read config ") + config_toml; delete ctx; return RT_ERR_IO; }
+        if (!rttoml::parse(text, doc, err)) { g_createError = "config parse error: " + err; delete ctx; return RT_ERR_IO; }
+    }
+    // LoadConfig (configLoader.cpp:15-26); the screen size passed in wins, as in main.cu:260
+    int w = rttoml::find_or_int(doc, "resolution", "width", 1920);
+    int h = rttoml::find_or_int(doc, "resolution", "height", 1080);
+    ctx->screenW = screen_width > 0 ? screen_width : w;
+    ctx->screenH = screen_height > 0 ? screen_height : h;
+    ctx->inputMeshFileName = rttoml::find_or_string(doc, "file", "inputMeshFileName", "");
+    ctx->inputTextureFileNames = rttoml::find_or_strings(doc, "file", "inputTextureFileNames");
+    ctx->inputCameraFileName = rttoml::find_or_string(doc, "file", "inputCameraFileName", "");
+    ctx->cameraSaveFileName = rttoml::find_or_string(doc, "file", "cameraSaveFileName", "");
+    ctx->loadCameraAtInit = rttoml::find_or_bool(doc, "file", "loadCameraAtInit", false);
+    ctx->useDynamicResolution = rttoml::find_or_bool(doc, "optimziation", "useDynamicResolution", true);
+    ctx->targetFps = rttoml::find_or_float(doc, "optimziation", "targetFps", 60.0f);
+    ctx->maxWidth = rttoml::find_or_int(doc, "optimziation", "maxWidth", 3840);
+    ctx->maxHeight = rttoml::find_or_int(doc, "optimziation", "maxHeight", 2160);
+    ctx->minWidth = rttoml::find_or_int(doc, "optimziation", "minWidth", 640);
+    ctx->minHeight = rttoml::find_or_int(doc, "optimziation", "minHeight", 480);
+    ctx->chunkDim = rttoml::find_or_int(doc, "scene", "chunkDim", 1);
+    ctx->meshFile = rttoml::find_or_string(doc, "scene", "meshFile", "");
+    ctx->spp = rttoml::find_or_int(doc, "render", "spp", 1);
+    ctx->device = rttoml::find_or_int(doc, "render", "device", -1);
+    ctx->stripY0 = rttoml::find_or_int(doc, "render", "stripY0", 0);
+    ctx->stripRows = rttoml::find_or_int(doc, "render", "stripRows", -1);
+    if (ctx->screenW <= 0 || ctx->screenH <= 0 || ctx->screenW > 16384 || ctx->screenH > 16384 || ctx->spp < 1 ||
+        ctx->spp > 64 || ctx->chunkDim < 1 || ctx->chunkDim > 8) {
+        g_createError = "invalid resolution / spp / chunkDim";
+        delete ctx;
+        return RT_ERR_ARG;
+    }
+    // init.cu:58-67: dynamic resolution renders at the max size
+    if (ctx->useDynamicResolution) { ctx->renderW = ctx->maxWidth; ctx->renderH = ctx->maxHeight; }
+    else { ctx->renderW = ctx->screenW; ctx->renderH = ctx->screenH; }
+    if (ctx->stripRows < 0) ctx->stripRows = ctx->renderH - ctx->stripY0;
+    if (ctx->stripY0 < 0 || ctx->stripRows < 1 || ctx->stripY0 + ctx->stripRows > ctx->renderH) {
+        g_createError = "invalid strip rows";
+        delete ctx;
+        return RT_ERR_ARG;
+    }
+    *out = ctx;
+    return RT_OK;
+}
+
+int rt_init(rt_context* ctx) {
+    if (!ctx) return RT_ERR_ARG;
+    if (ctx->inited) { ctx->err = "rt_init called twice"; return RT_ERR_STATE; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { ctx->err = "no HIP device visible"; return RT_ERR_NO_DEVICE; }
+    if (ctx->device >= 0) HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int dev = 0;
+    HIP_TRY(ctx, hipGetDevice(&dev));
+    ctx->device = dev;
+    hipDeviceProp_t prop;
+    HIP_TRY(ctx, hipGetDeviceProperties(&prop, dev));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        ctx->err = std::string("librtx is built for gfx950, device is ") + prop.gcnArchName;
+        return RT_ERR_NO_DEVICE;
+    }
+
+    // ---- scene (init.cu:78-130)
+    std::string err;
+    const std::string dataDir = rt_data_dir();
+    if (!ctx->meshFile.empty()) {
+        if (!load_triangle_bin(ctx->meshFile, ctx->mesh, err)) { ctx->err = err; return RT_ERR_IO; }
+    } else {
+        std::vector<std::vector<float>> tiles;
+        if (!rtscene::load_tiles(dataDir + "/roundcubes_l2.bin", tiles, err) ||
+            !rtscene::generate(ctx->chunkDim, tiles, ctx->mesh, err)) {
+            ctx->err = err;
+            return RT_ERR_IO;
+        }
+    }
+    const uint32_t N = ctx->mesh.triCount, NP = ctx->mesh.triCountPadded;
+    if (N < 2 || N > 1024u * 1024u) { ctx->err = "triangle count out of range"; return RT_ERR_ARG; }
+    ctx->B = (N + 1023) / 1024;
+    if (ctx->B >= 1024) { ctx->err = "batch count must stay below 1024 (init.cu:126)"; return RT_ERR_ARG; }
+    ctx->nv = (uint32_t)(ctx->mesh.vertices.size() / 3);
+
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    HIP_TRY(ctx, hipEventCreate(&ctx->ev0));
+    HIP_TRY(ctx, hipEventCreate(&ctx->ev1));
+
+    int rc;
+#define ALLOC(p, bytes) if ((rc = dalloc(ctx, &(p), (bytes))) != RT_OK) return rc
+    ALLOC(ctx->dVerts, (size_t)ctx->nv * 12);
+    ALLOC(ctx->dNormals, (size_t)ctx->nv * 12);
+    ALLOC(ctx->dIdx, (size_t)NP * 12);
+    ALLOC(ctx->dTriPos, (size_t)NP * 48);
+    ALLOC(ctx->dTriNrm, (size_t)NP * 48);
+    ALLOC(ctx->dAabbs, (size_t)NP * 24);
+    ALLOC(ctx->dBatchScene, (size_t)ctx->B * 24);
+    ALLOC(ctx->dMorton, (size_t)ctx->B * 4096);
+    ALLOC(ctx->dReorder, (size_t)ctx->B * 4096);
+    ALLOC(ctx->dNodes, (size_t)ctx->B * 1024 * 64);
+    ALLOC(ctx->dTlasAabbs, (size_t)ctx->B * 24);
+    ALLOC(ctx->dTlasScene, 24);
+    ALLOC(ctx->dTlasMorton, 4096);
+    ALLOC(ctx->dTlasReorder, 4096);
+    ALLOC(ctx->dTlasNodes, (size_t)ctx->B * 64);
+    ALLOC(ctx->dCounter, 64);
+    ALLOC(ctx->dBlueNoise, 327680);
+    const size_t P = (size_t)ctx->renderW * ctx->renderH;
+    ALLOC(ctx->dHits, P * 16);
+    ALLOC(ctx->dHitNrm, P * 16);
+    ALLOC(ctx->dHitFake, P * 16);
+    ALLOC(ctx->dHitStats, P * 16);
+
+    HIP_TRY(ctx, hipMemcpy(ctx->dVerts, ctx->mesh.vertices.data(), (size_t)ctx->nv * 12, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(ctx->dIdx, ctx->mesh.indices.data(), (size_t)NP * 12, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemset(ctx->dCounter, 0, 64));
+    HIP_TRY(ctx, hipMemset(ctx->dNodes, 0, (size_t)ctx->B * 1024 * 64));
+    HIP_TRY(ctx, hipMemset(ctx->dTlasNodes, 0, (size_t)ctx->B * 64));
+
+    std::string bn;
+    if (!read_file(dataDir + "/bluenoise_4spp.bin", bn) || bn.size() != 327680) {
+        ctx->err = "cannot read " + dataDir + "/bluenoise_4spp.bin";
+        return RT_ERR_IO;
+    }
+    HIP_TRY(ctx, hipMemcpy(ctx->dBlueNoise, bn.data(), bn.size(), hipMemcpyHostToDevice));
+
+    // ---- frame-1 smooth normals (kernel.cu:313-327): vertex -> corner CSR in triangle order
+    {
+        std::vector<uint32_t> off(ctx->nv + 1, 0), corners((size_t)NP * 3);
+        for (size_t c = 0; c < (size_t)NP * 3; ++c) off[ctx->mesh.indices[c] + 1]++;
+        for (uint32_t v = 0; v < ctx->nv; ++v) off[v + 1] += off[v];
+        std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+        for (size_t c = 0; c < (size_t)NP * 3; ++c) corners[fill[ctx->mesh.indices[c]]++] = (uint32_t)c;
+        ALLOC(ctx->dAdjOff, off.size() * 4);
+        ALLOC(ctx->dAdjCorner, corners.size() * 4);
+        HIP_TRY(ctx, hipMemcpy(ctx->dAdjOff, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(ctx, hipMemcpy(ctx->dAdjCorner, corners.data(), corners.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(ctx, rtk_launch_smooth_normals(ctx->dVerts, ctx->dAdjOff, ctx->dAdjCorner, ctx->dIdx, ctx->nv,
+                                               ctx->dNormals, ctx->stream));
+    }
+#undef ALLOC
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->inited = true;
+    return RT_OK;
+}
+
+void rt_destroy(rt_context* ctx) {
+    if (!ctx) return;
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (void* p : ctx->allocations) (void)hipFree(p);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int rt_get_params(const rt_context* ctx, rt_params* out) {
+    if (!ctx || !out) return RT_ERR_ARG;
+    *out = ctx->params;
+    return RT_OK;
+}
+
+int rt_set_params(rt_context* ctx, const rt_params* in) {
+    if (!ctx || !in) return RT_ERR_ARG;
+    ctx->params = *in;
+    return RT_OK;
+}
+
+int rt_get_camera(const rt_context* ctx, rt_camera* out) {
+    if (!ctx || !out) return RT_ERR_ARG;
+    *out = ctx->camera;
+    return RT_OK;
+}
+
+int rt_set_camera(rt_context* ctx, const rt_camera* in) {
+    if (!ctx || !in) return RT_ERR_ARG;
+    ctx->camera = *in;
+    return RT_OK;
+}
+
+int rt_set_frame_index(rt_context* ctx, int frame_num) {
+    if (!ctx || frame_num < 1) return RT_ERR_ARG;
+    ctx->nextFrame = frame_num;
+    return RT_OK;
+}
+
+int rt_set_delta_time(rt_context* ctx, float ms) {
+    if (!ctx) return RT_ERR_ARG;
+    ctx->deltaMs = ms;
+    return RT_OK;
+}
+
+int rt_get_info(const rt_context* ctx, rt_info* out) {
+    if (!ctx || !out) return RT_ERR_ARG;
+    out->triCount = ctx->mesh.triCount;
+    out->triCountPadded = ctx->mesh.triCountPadded;
+    out->batchCount = ctx->B;
+    out->vertexCount = ctx->nv;
+    out->renderWidth = ctx->renderW;
+    out->renderHeight = ctx->renderH;
+    out->screenWidth = ctx->screenW;
+    out->screenHeight = ctx->screenH;
+    out->frameNum = ctx->lastFrame;
+    out->deviceId = ctx->device;
+    out->spp = (uint32_t)ctx->spp;
+    return RT_OK;
+}
+
+int rt_build_bvh(rt_context* ctx) {
+    if (!ctx) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_build_bvh before rt_init"; return RT_ERR_STATE; }
+    BvhBuildParams p;
+    p.vertices = ctx->dVerts;
+    p.normals = ctx->dNormals;
+    p.indices = ctx->dIdx;
+    p.triCount = ctx->mesh.triCount;
+    p.triCountPadded = ctx->mesh.triCountPadded;
+    p.batchCount = ctx->B;
+    p.triPos = ctx->dTriPos;
+    p.triNrm = ctx->dTriNrm;
+    p.aabbs = ctx->dAabbs;
+    p.batchSceneAabbs = ctx->dBatchScene;
+    p.morton = ctx->dMorton;
+    p.reorder = ctx->dReorder;
+    p.nodes = ctx->dNodes;
+    p.tlasAabbs = ctx->dTlasAabbs;
+    p.tlasSceneAabb = ctx->dTlasScene;
+    p.tlasMorton = ctx->dTlasMorton;
+    p.tlasReorder = ctx->dTlasReorder;
+    p.tlasNodes = ctx->dTlasNodes;
+    p.counter = ctx->dCounter;
+    HIP_TRY(ctx, rtk_launch_build_bvh(&p, ctx->stream));
+    return RT_OK;
+}
+
+int rt_trace_primary(rt_context* ctx, int frame_num, int with_detail) {
+    if (!ctx) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_trace_primary before rt_init"; return RT_ERR_STATE; }
+    HostCamera hc;
+    rt_camera_update(ctx->camera, ctx->renderW, ctx->renderH, hc);
+    TracePrimaryParams p;
+    p.cam = rt_trace_camera(hc);
+    p.width = (uint32_t)ctx->renderW;
+    p.height = (uint32_t)ctx->renderH;
+    p.y0 = (uint32_t)ctx->stripY0;
+    p.rows = (uint32_t)ctx->stripRows;
+    p.frameNum = frame_num;
+    p.bluenoise = ctx->dBlueNoise;
+    p.triPos = ctx->dTriPos;
+    p.triNrm = ctx->dTriNrm;
+    p.nodes = ctx->dNodes;
+    p.tlasNodes = ctx->dTlasNodes;
+    p.hitOut = ctx->dHits;
+    p.normalOut = with_detail ? ctx->dHitNrm : nullptr;
+    p.fakeNormalOut = with_detail ? ctx->dHitFake : nullptr;
+    p.statsOut = with_detail ? ctx->dHitStats : nullptr;
+    HIP_TRY(ctx, rtk_launch_trace_primary(&p, ctx->stream));
+    return RT_OK;
+}
+
+int rt_sync(rt_context* ctx) {
+    if (!ctx) return RT_ERR_ARG;
+    if (!ctx->stream) return RT_OK;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+int rt_draw_frame_internal(rt_context* ctx);  // frame.cpp
+
+int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms) {
+    if (!ctx || !total_ms || iters < 1) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_time_stage before rt_init"; return RT_ERR_STATE; }
+    HIP_TRY(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    for (int i = 0; i < iters; ++i) {
+        int rc = RT_OK;
+        if (stage == 0) rc = rt_build_bvh(ctx);
+        else if (stage == 1) rc = rt_trace_primary(ctx, 1 + i, 0);
+        else { ctx->err = "unknown stage"; return RT_ERR_ARG; }
+        if (rc != RT_OK) return rc;
+    }
+    HIP_TRY(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    HIP_TRY(ctx, hipEventSynchronize(ctx->ev1));
+    HIP_TRY(ctx, hipEventElapsedTime(total_ms, ctx->ev0, ctx->ev1));
+    return RT_OK;
+}
+
+size_t rt_array_bytes(const rt_context* ctx, int what) {
+    if (!ctx) return 0;
+    const size_t NP = ctx->mesh.triCountPadded, B = ctx->B, P = (size_t)ctx->renderW * ctx->renderH;
+    switch (what) {
+        case RT_ARR_VERTICES: return (size_t)ctx->nv * 12;
+        case RT_ARR_INDICES: return NP * 12;
+        case RT_ARR_NORMALS: return (size_t)ctx->nv * 12;
+        case RT_ARR_TRI_POS: return NP * 48;
+        case RT_ARR_TRI_NRM: return NP * 48;
+        case RT_ARR_AABBS: return NP * 24;
+        case RT_ARR_MORTON: return B * 4096;
+        case RT_ARR_REORDER: return B * 4096;
+        case RT_ARR_NODES: return B * 1024 * 64;
+        case RT_ARR_TLAS_AABBS: return B * 24;
+        case RT_ARR_TLAS_MORTON: return 4096;
+        case RT_ARR_TLAS_REORDER: return 4096;
+        case RT_ARR_TLAS_NODES: return B * 64;
+        case RT_ARR_TLAS_SCENE_AABB: return 24;
+        case RT_ARR_BATCH_SCENE_AABBS: return B * 24;
+        case RT_ARR_HITS: return P * 16;
+        case RT_ARR_HIT_NORMALS: return P * 16;
+        case RT_ARR_HIT_FAKE_NORMALS: return P * 16;
+        case RT_ARR_HIT_STATS: return P * 16;
+        default: return 0;
+    }
+}
+
+int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
+    rt_context* ctx = const_cast<rt_context*>(cctx);
+    if (!ctx || !dst) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_download before rt_init"; return RT_ERR_STATE; }
+    const void* src = nullptr;
+    switch (what) {
+        case RT_ARR_VERTICES: src = ctx->dVerts; break;
+        case RT_ARR_INDICES: src = ctx->dIdx; break;
+        case RT_ARR_NORMALS: src = ctx->dNormals; break;
+        case RT_ARR_TRI_POS: src = ctx->dTriPos; break;
+        case RT_ARR_TRI_NRM: src = ctx->dTriNrm; break;
+        case RT_ARR_AABBS: src = ctx->dAabbs; break;
+        case RT_ARR_MORTON: src = ctx->dMorton; break;
+        case RT_ARR_REORDER: src = ctx->dReorder; break;
+        case RT_ARR_NODES: src = ctx->dNodes; break;
+        case RT_ARR_TLAS_AABBS: src = ctx->dTlasAabbs; break;
+        case RT_ARR_TLAS_MORTON: src = ctx->dTlasMorton; break;
+        case RT_ARR_TLAS_REORDER: src = ctx->dTlasReorder; break;
+        case RT_ARR_TLAS_NODES: src = ctx->dTlasNodes; break;
+        case RT_ARR_TLAS_SCENE_AABB: src = ctx->dTlasScene; break;
+        case RT_ARR_BATCH_SCENE_AABBS: src = ctx->dBatchScene; break;
+        case RT_ARR_HITS: src = ctx->dHits; break;
+        case RT_ARR_HIT_NORMALS: src = ctx->dHitNrm; break;
+        case RT_ARR_HIT_FAKE_NORMALS: src = ctx->dHitFake; break;
+        case RT_ARR_HIT_STATS: src = ctx->dHitStats; break;
+        default: ctx->err = "unknown array"; return RT_ERR_ARG;
+    }
+    const size_t need = rt_array_bytes(ctx, what);
+    if (bytes < need) { ctx->err = "destination too small"; return RT_ERR_ARG; }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipMemcpy(dst, src, need, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+}  // extern "C"

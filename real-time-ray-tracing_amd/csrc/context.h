@@ -1,0 +1,83 @@
+// context.h — host-side renderer state behind the C-ABI (the RayTracer of kernel.cuh:431-621).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rtx_amd.h"
+#include "bvh_kernels.h"
+#include "frame_kernels.h"
+#include "scene_gen.h"
+
+struct HostCamera {  // Camera::update outputs (kernel.cuh:103-121)
+    float pos[3], dir[3], left[3], up[3];
+    float yaw, pitch, focal, aperture;
+    float res[2], invRes[2], fov[2], tanHalfFov[2];
+    float adjustedLeft[3], adjustedUp[3], adjustedFront[3], apertureLeft[3], apertureUp[3];
+};
+
+struct rt_context {
+    // ---- settings (GlobalSettings, globalSettings.h:5-22) + extensions
+    int screenW = 1920, screenH = 1080;
+    int renderW = 1920, renderH = 1080;
+    bool useDynamicResolution = true;
+    float targetFps = 60.0f;
+    int maxWidth = 3840, maxHeight = 2160, minWidth = 640, minHeight = 480;
+    std::string inputMeshFileName, inputCameraFileName, cameraSaveFileName;
+    std::vector<std::string> inputTextureFileNames;
+    bool loadCameraAtInit = false;
+    int chunkDim = 1;
+    std::string meshFile;  // [scene] meshFile: meshProcessor .bin instead of the procedural scene
+    int spp = 1;
+    int stripY0 = 0, stripRows = -1;  // [render] stripY0/stripRows: screen-strip split
+    int device = -1;
+
+    std::string err;
+    bool inited = false;
+    rt_params params{};
+    rt_camera camera{};
+    int nextFrame = 1;     // frameNum of the next draw (kernel.cu:64 starts at 1)
+    int lastFrame = 0;
+    float deltaMs = 16.667f;
+
+    // ---- scene
+    rtscene::SceneMesh mesh;
+    uint32_t B = 0, nv = 0;
+
+    // ---- device
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float* dVerts = nullptr;
+    float* dNormals = nullptr;
+    uint32_t* dIdx = nullptr;
+    uint32_t* dAdjOff = nullptr;
+    uint32_t* dAdjCorner = nullptr;
+    float4* dTriPos = nullptr;
+    float4* dTriNrm = nullptr;
+    float* dAabbs = nullptr;
+    float* dBatchScene = nullptr;
+    uint32_t* dMorton = nullptr;
+    uint32_t* dReorder = nullptr;
+    void* dNodes = nullptr;
+    float* dTlasAabbs = nullptr;
+    float* dTlasScene = nullptr;
+    uint32_t* dTlasMorton = nullptr;
+    uint32_t* dTlasReorder = nullptr;
+    void* dTlasNodes = nullptr;
+    uint32_t* dCounter = nullptr;
+    uint8_t* dBlueNoise = nullptr;
+    float4* dHits = nullptr;
+    float4* dHitNrm = nullptr;
+    float4* dHitFake = nullptr;
+    uint32_t* dHitStats = nullptr;
+    FrameResources fr{};  // path-trace / denoise / post buffers (frame_kernels.h)
+
+    std::vector<void*> allocations;
+};
+
+// helpers shared by the C-ABI translation units
+std::string rt_data_dir();
+void rt_camera_update(const rt_camera& in, int renderW, int renderH, HostCamera& c);
+TraceCamera rt_trace_camera(const HostCamera& c);

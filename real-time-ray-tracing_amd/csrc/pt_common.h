@@ -1,0 +1,68 @@
+// pt_common.h — per-pixel sampling helpers shared by the primary-ray and path-trace kernels.
+//
+//   blue-noise sampler   blueNoiseRandGen.h:113-146 (Heitz 2019, OPTIMIZED_BLUE_NOISE_SPP 4)
+//   ConcentricSampleDisk bsdf.cuh:9-34
+//   GenerateRay          raygen.cuh:7-38
+//   GetRayConeWidth      raygen.cuh:45-63
+#pragma once
+#include "bvh_kernels.h"
+#include "rt_device.h"
+
+namespace rtd {
+
+constexpr float kPiOver4 = 0.7853981633974483096156608458198757210492f;   // linearMath.h:11-20
+constexpr float kPiOver2 = 1.5707963267948966192313216916397514420985f;
+constexpr float kPi = 3.1415926535897932384626422832795028841971f;
+constexpr float kTwoPi = 6.2831853071795864769252867665590057683943f;
+
+// tables: sobol[256*256] | scrambling[128*128*8] | ranking[128*128*8]
+RT_DEV float bluenoise(const uint8_t* tables, int px, int py, int sampleIdx, int dim) {
+    const uint8_t* sobol = tables;
+    const uint8_t* scr = tables + 256 * 256;
+    const uint8_t* rnk = scr + 128 * 128 * 8;
+    px &= 127;
+    py &= 127;
+    sampleIdx &= 255;
+    const int cell = (px + py * 128) * 8;
+    const int ranked = sampleIdx ^ (int)rnk[dim + cell];
+    int value = sobol[dim + ranked * 256];
+    value = value ^ (int)scr[(dim % 8) + cell];
+    return ((float)value + 0.5f) / 256.0f;
+}
+
+RT_DEV F2 concentric_disk(F2 u) {
+    const F2 o = {2.0f * u.x - 1.0f, 2.0f * u.y - 1.0f};
+    if (fabsf(o.x) < 1e-10f && fabsf(o.y) < 1e-10f) return F2{0.0f, 0.0f};
+    float theta, r;
+    if (fabsf(o.x) > fabsf(o.y)) {
+        r = o.x;
+        theta = kPiOver4 * (o.y / o.x);
+    } else {
+        r = o.y;
+        theta = kPiOver2 - kPiOver4 * (o.x / o.y);
+    }
+    float sn, cs;
+    rt_sincosf(theta, &sn, &cs);
+    return F2{cs * r, sn * r};
+}
+
+RT_DEV F3 load3(const float* a) { return f3(a[0], a[1], a[2]); }
+
+RT_DEV void generate_ray(const TraceCamera& c, int ix, int iy, F2 pix, F2 ap, F3& orig, F3& dir, F3& centerDir,
+                         F2& sampleUv) {
+    F2 uv = {((float)ix + pix.x) * c.invRes[0], ((float)iy + pix.y) * c.invRes[1]};
+    F2 uvc = {((float)ix + 0.5f) * c.invRes[0], ((float)iy + 0.5f) * c.invRes[1]};
+    sampleUv = uv;
+    uv = F2{uv.x * -2.0f + 1.0f, uv.y * -2.0f + 1.0f};
+    uvc = F2{uvc.x * -2.0f + 1.0f, uvc.y * -2.0f + 1.0f};
+    const F3 front = load3(c.adjustedFront), left = load3(c.adjustedLeft), up = load3(c.adjustedUp);
+    const F3 p = front + left * uv.x + up * uv.y;
+    const F3 pc = front + left * uvc.x + up * uvc.y;
+    const F2 d = concentric_disk(ap);
+    const F3 pa = d.x * load3(c.apertureLeft) + d.y * load3(c.apertureUp);
+    orig = load3(c.pos) + pa;
+    dir = normalize(p - pa);
+    centerDir = normalize(pc);
+}
+
+}  // namespace rtd

@@ -1,0 +1,309 @@
+// rtmath.h — deterministic transcendental functions, bit-identical on gfx950 and x86-64.
+//
+// The reference calls CUDA libdevice sinf/cosf/expf/powf/acosf/... on the device and
+// MSVC's libm on the host (e.g. bsdf.cuh:33, sky.cuh:167-191, kernel.cuh:105-109).
+// Neither is available here, and ROCm's ocml and glibc disagree in the last ulp, which
+// would flip Monte-Carlo decisions between the GPU kernels and the CPU oracle.  Every
+// transcendental on the hot path therefore goes through this header: each function is
+// evaluated in IEEE double with plain +,-,*,/ (no contraction: every translation unit that
+// includes this header is built with -ffp-contract=off) and rounded once to float.  The
+// results are faithfully rounded (correctly rounded in all but rare ties) and identical
+// on the GPU and on the host, so kernel-vs-oracle parity can be tested bit-exact.
+//
+// sqrtf and float division stay native: both are correctly rounded on both sides
+// (hipcc's default -fhip-fp32-correctly-rounded-divide-sqrt, SSE2 on the host).
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define RT_HD __host__ __device__ __forceinline__
+#else
+#define RT_HD static inline
+#endif
+
+namespace rtm {
+
+RT_HD double bits_to_double(uint64_t u) { union { uint64_t u; double d; } c; c.u = u; return c.d; }
+RT_HD uint64_t double_to_bits(double d) { union { uint64_t u; double d; } c; c.d = d; return c.u; }
+RT_HD float bits_to_float(uint32_t u) { union { uint32_t u; float f; } c; c.u = u; return c.f; }
+RT_HD uint32_t float_to_bits(float f) { union { uint32_t u; float f; } c; c.f = f; return c.u; }
+
+RT_HD bool d_isnan(double x) { return x != x; }
+RT_HD double d_inf() { return bits_to_double(0x7FF0000000000000ull); }
+RT_HD double d_nan() { return bits_to_double(0x7FF8000000000000ull); }
+RT_HD double d_abs(double x) { return bits_to_double(double_to_bits(x) & 0x7FFFFFFFFFFFFFFFull); }
+
+// round-half-away for the reduction index; exact for |x| < 2^52
+RT_HD double d_round(double x) {
+    double a = d_abs(x);
+    if (a >= 4503599627370496.0) return x;
+    double r = (double)(int64_t)(a + 0.5);
+    return x < 0 ? -r : r;
+}
+
+// ---------------------------------------------------------------- exp2 / log2
+RT_HD double exp2d(double x) {
+    if (d_isnan(x)) return x;
+    if (x >= 1024.0) return d_inf();
+    if (x <= -1075.0) return 0.0;
+    double n = d_round(x);
+    double f = x - n;                       // [-0.5, 0.5]
+    double y = f * 0.69314718055994530942;  // |y| <= 0.3466
+    // e^y, Taylor to y^13: truncation < 2e-17
+    double p = 1.0 / 6227020800.0;          // 1/13!
+    p = p * y + 1.0 / 479001600.0;
+    p = p * y + 1.0 / 39916800.0;
+    p = p * y + 1.0 / 3628800.0;
+    p = p * y + 1.0 / 362880.0;
+    p = p * y + 1.0 / 40320.0;
+    p = p * y + 1.0 / 5040.0;
+    p = p * y + 1.0 / 720.0;
+    p = p * y + 1.0 / 120.0;
+    p = p * y + 1.0 / 24.0;
+    p = p * y + 1.0 / 6.0;
+    p = p * y + 0.5;
+    p = p * y + 1.0;
+    p = p * y + 1.0;
+    int ni = (int)n;
+    if (ni > 1023) { p *= 2.0; ni -= 1; }
+    if (ni >= -1022) return p * bits_to_double((uint64_t)(ni + 1023) << 52);
+    // subnormal range: scale in two steps
+    p *= bits_to_double((uint64_t)(ni + 600 + 1023) << 52);
+    return p * bits_to_double((uint64_t)(-600 + 1023) << 52);
+}
+
+// natural log of x in (0, inf), exact exponent split + atanh series
+RT_HD double logd_pos(double x) {
+    uint64_t b = double_to_bits(x);
+    int e = (int)((b >> 52) & 0x7FF);
+    if (e == 0) {  // subnormal double (cannot come from a float input, kept for safety)
+        x *= 18014398509481984.0;  // 2^54
+        b = double_to_bits(x);
+        e = (int)((b >> 52) & 0x7FF) - 54;
+    }
+    e -= 1023;
+    double m = bits_to_double((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);  // [1,2)
+    if (m > 1.41421356237309504880) { m *= 0.5; e += 1; }
+    double s = (m - 1.0) / (m + 1.0);       // |s| <= 0.1716
+    double s2 = s * s;
+    double p = 1.0 / 23.0;
+    p = p * s2 + 1.0 / 21.0;
+    p = p * s2 + 1.0 / 19.0;
+    p = p * s2 + 1.0 / 17.0;
+    p = p * s2 + 1.0 / 15.0;
+    p = p * s2 + 1.0 / 13.0;
+    p = p * s2 + 1.0 / 11.0;
+    p = p * s2 + 1.0 / 9.0;
+    p = p * s2 + 1.0 / 7.0;
+    p = p * s2 + 1.0 / 5.0;
+    p = p * s2 + 1.0 / 3.0;
+    p = p * s2 + 1.0;
+    double lnm = 2.0 * s * p;
+    return (double)e * 0.69314718055994530942 + lnm;
+}
+
+RT_HD double logd(double x) {
+    if (d_isnan(x)) return x;
+    if (x < 0.0) return d_nan();
+    if (x == 0.0) return -d_inf();
+    if (x == d_inf()) return x;
+    return logd_pos(x);
+}
+
+RT_HD double log2d(double x) {
+    if (d_isnan(x)) return x;
+    if (x < 0.0) return d_nan();
+    if (x == 0.0) return -d_inf();
+    if (x == d_inf()) return x;
+    // split exponent exactly so log2 of powers of two is exact
+    uint64_t b = double_to_bits(x);
+    int e = (int)((b >> 52) & 0x7FF) - 1023;
+    double m = bits_to_double((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    if (m > 1.41421356237309504880) { m *= 0.5; e += 1; }
+    return (double)e + logd_pos(m) * 1.44269504088896340736;
+}
+
+RT_HD double expd(double x) {
+    if (d_isnan(x)) return x;
+    return exp2d(x * 1.44269504088896340736);
+}
+
+// ---------------------------------------------------------------- trig
+RT_HD void sincosd(double x, double& s, double& c) {
+    if (d_isnan(x) || d_abs(x) == d_inf()) { s = d_nan(); c = d_nan(); return; }
+    double k = d_round(x * 0.63661977236758134308);  // 2/pi
+    // Cody-Waite, fdlibm constants (pio2_1 has 33 bits: k*pio2_1 exact for |k| < 2^20)
+    double r = x - k * 1.57079632673412561417e+00;
+    r = r - k * 6.07710050650619224932e-11;
+    double r2 = r * r;
+    double sp = -1.0 / 1307674368000.0;     // -1/15!
+    sp = sp * r2 + 1.0 / 6227020800.0;
+    sp = sp * r2 - 1.0 / 39916800.0;
+    sp = sp * r2 + 1.0 / 362880.0;
+    sp = sp * r2 - 1.0 / 5040.0;
+    sp = sp * r2 + 1.0 / 120.0;
+    sp = sp * r2 - 1.0 / 6.0;
+    double sr = r + r * r2 * sp;
+    double cp = 1.0 / 20922789888000.0;     // 1/16!
+    cp = cp * r2 - 1.0 / 87178291200.0;
+    cp = cp * r2 + 1.0 / 479001600.0;
+    cp = cp * r2 - 1.0 / 3628800.0;
+    cp = cp * r2 + 1.0 / 40320.0;
+    cp = cp * r2 - 1.0 / 720.0;
+    cp = cp * r2 + 1.0 / 24.0;
+    cp = cp * r2 - 0.5;
+    double cr = 1.0 + r2 * cp;
+    int q = (int)((int64_t)k & 3);
+    if (q == 0) { s = sr; c = cr; }
+    else if (q == 1) { s = cr; c = -sr; }
+    else if (q == 2) { s = -sr; c = -cr; }
+    else { s = -cr; c = sr; }
+}
+
+// atan on [0, inf)
+RT_HD double atan_pos(double x) {
+    bool inv = x > 1.0;
+    if (inv) x = 1.0 / x;
+    // atan(x) = pi/6 + atan((sqrt3 x - 1)/(x + sqrt3)) for x > tan(pi/12)
+    bool shift = x > 0.26794919243112270647;
+    if (shift) x = (x * 1.73205080756887729353 - 1.0) / (x + 1.73205080756887729353);
+    double x2 = x * x;                       // <= 0.0718
+    double p = 1.0 / 29.0;
+    p = -p * x2 + 1.0 / 27.0;
+    p = -p * x2 + 1.0 / 25.0;
+    p = -p * x2 + 1.0 / 23.0;
+    p = -p * x2 + 1.0 / 21.0;
+    p = -p * x2 + 1.0 / 19.0;
+    p = -p * x2 + 1.0 / 17.0;
+    p = -p * x2 + 1.0 / 15.0;
+    p = -p * x2 + 1.0 / 13.0;
+    p = -p * x2 + 1.0 / 11.0;
+    p = -p * x2 + 1.0 / 9.0;
+    p = -p * x2 + 1.0 / 7.0;
+    p = -p * x2 + 1.0 / 5.0;
+    p = -p * x2 + 1.0 / 3.0;
+    p = -p * x2 + 1.0;
+    double a = x * p;
+    if (shift) a = 0.52359877559829887308 + a;
+    if (inv) a = 1.57079632679489661923 - a;
+    return a;
+}
+
+RT_HD double atand(double x) {
+    if (d_isnan(x)) return x;
+    if (x == d_inf()) return 1.57079632679489661923;
+    if (x == -d_inf()) return -1.57079632679489661923;
+    return x < 0 ? -atan_pos(-x) : atan_pos(x);
+}
+
+RT_HD double atan2d(double y, double x) {
+    if (d_isnan(x) || d_isnan(y)) return d_nan();
+    const double pi = 3.14159265358979323846;
+    bool yneg = (double_to_bits(y) >> 63) != 0;
+    bool xneg = (double_to_bits(x) >> 63) != 0;
+    double ay = d_abs(y), ax = d_abs(x);
+    double r;
+    if (ay == 0.0) r = xneg ? pi : 0.0;
+    else if (ax == 0.0) r = pi * 0.5;
+    else if (ax == d_inf() && ay == d_inf()) r = xneg ? pi * 0.75 : pi * 0.25;
+    else if (ax == d_inf()) r = xneg ? pi : 0.0;
+    else if (ay == d_inf()) r = pi * 0.5;
+    else {
+        double a = atan_pos(ay / ax);
+        r = xneg ? pi - a : a;
+    }
+    return yneg ? -r : r;
+}
+
+}  // namespace rtm
+
+// ------------------------------------------------------------------ float API
+RT_HD float rt_expf(float x) { return (float)rtm::expd((double)x); }
+RT_HD float rt_exp2f(float x) { return (float)rtm::exp2d((double)x); }
+RT_HD float rt_logf(float x) { return (float)rtm::logd((double)x); }
+RT_HD float rt_log2f(float x) { return (float)rtm::log2d((double)x); }
+RT_HD float rt_sinf(float x) { double s, c; rtm::sincosd((double)x, s, c); return (float)s; }
+RT_HD float rt_cosf(float x) { double s, c; rtm::sincosd((double)x, s, c); return (float)c; }
+RT_HD void rt_sincosf(float x, float* s, float* c) {
+    double sd, cd; rtm::sincosd((double)x, sd, cd); *s = (float)sd; *c = (float)cd;
+}
+RT_HD float rt_tanf(float x) { double s, c; rtm::sincosd((double)x, s, c); return (float)(s / c); }
+RT_HD float rt_atanf(float x) { return (float)rtm::atand((double)x); }
+RT_HD float rt_atan2f(float y, float x) { return (float)rtm::atan2d((double)y, (double)x); }
+RT_HD float rt_asinf(float x) {
+    double d = (double)x;
+    if (!(d >= -1.0 && d <= 1.0)) return (float)rtm::d_nan();
+    return (float)rtm::atan2d(d, __builtin_sqrt((1.0 - d) * (1.0 + d)));
+}
+RT_HD float rt_acosf(float x) {
+    double d = (double)x;
+    if (!(d >= -1.0 && d <= 1.0)) return (float)rtm::d_nan();
+    return (float)rtm::atan2d(__builtin_sqrt((1.0 - d) * (1.0 + d)), d);
+}
+
+// powf with the C99 special cases that matter on the path (x >= 0 in practice)
+RT_HD float rt_powf(float xf, float yf) {
+    double x = (double)xf, y = (double)yf;
+    if (y == 0.0) return 1.0f;
+    if (x == 1.0) return 1.0f;
+    if (rtm::d_isnan(x) || rtm::d_isnan(y)) return (float)rtm::d_nan();
+    bool yint = false, yodd = false;
+    if (rtm::d_abs(y) < 9007199254740992.0) {
+        double t = (double)(int64_t)y;
+        yint = (t == y);
+        if (yint) yodd = ((int64_t)y & 1) != 0;
+    } else {
+        yint = true;
+    }
+    if (x == 0.0) {
+        bool neg0 = (rtm::double_to_bits(x) >> 63) != 0;
+        if (y > 0) return (neg0 && yodd) ? -0.0f : 0.0f;
+        return (neg0 && yodd) ? (float)-rtm::d_inf() : (float)rtm::d_inf();
+    }
+    double sign = 1.0;
+    if (x < 0.0) {
+        if (!yint) return (float)rtm::d_nan();
+        if (yodd) sign = -1.0;
+        x = -x;
+    }
+    if (x == rtm::d_inf()) return (float)(sign * (y > 0 ? rtm::d_inf() : 0.0));
+    return (float)(sign * rtm::exp2d(y * rtm::log2d(x)));
+}
+
+// IEEE float -> binary16, round to nearest even (matches __float2half_rn / v_cvt_f16_f32)
+RT_HD uint16_t rt_f2h(float f) {
+    uint32_t x = rtm::float_to_bits(f);
+    uint32_t sign = (x >> 16) & 0x8000u;
+    uint32_t ax = x & 0x7FFFFFFFu;
+    if (ax >= 0x7F800000u) return (uint16_t)(sign | (ax > 0x7F800000u ? 0x7E00u : 0x7C00u));
+    if (ax >= 0x477FF000u) return (uint16_t)(sign | 0x7C00u);  // rounds to >= 65520 -> inf
+    if (ax < 0x38800000u) {                                      // half subnormal or zero
+        if (ax < 0x33000000u) return (uint16_t)sign;             // < 2^-25 rounds to 0
+        uint32_t mant = (ax & 0x7FFFFFu) | 0x800000u;
+        int shift = 126 - (int)(ax >> 23);                       // 14..24
+        uint32_t h = mant >> (shift);
+        uint32_t rem = mant & ((1u << shift) - 1u);
+        uint32_t half = 1u << (shift - 1);
+        if (rem > half || (rem == half && (h & 1u))) h += 1u;
+        return (uint16_t)(sign | h);
+    }
+    uint32_t h = ((ax >> 13) - ((127u - 15u) << 10));
+    uint32_t rem = ax & 0x1FFFu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h += 1u;
+    return (uint16_t)(sign | h);
+}
+
+RT_HD float rt_h2f(uint16_t h) {
+    uint32_t sign = ((uint32_t)h & 0x8000u) << 16;
+    uint32_t e = ((uint32_t)h >> 10) & 0x1Fu;
+    uint32_t m = (uint32_t)h & 0x3FFu;
+    if (e == 0x1F) return rtm::bits_to_float(sign | 0x7F800000u | (m << 13));
+    if (e == 0) {
+        if (m == 0) return rtm::bits_to_float(sign);
+        // subnormal: m * 2^-24
+        float v = (float)m * 5.9604644775390625e-08f;
+        return sign ? -v : v;
+    }
+    return rtm::bits_to_float(sign | ((e + 112u) << 23) | (m << 13));
+}

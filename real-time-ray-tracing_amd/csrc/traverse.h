@@ -1,0 +1,296 @@
+// traverse.h — device-side two-level BVH traversal with the reference's semantics.
+//
+//   CreateRayBoxIntersectionHelper  geometry.cuh:519-583 (conservative Up/Dn rounding)
+//   RayAABBIntersect (pair)         geometry.cuh:585-629
+//   RayTriangleWatertight           geometry.cuh:375-472 (fp64 fallback on U/V/W == 0)
+//   TraverseBvh                     traverse.h:107-253: 16-entry stack whose overflowing
+//                                   pushes are dropped, 1024-iteration cap, nearer child
+//                                   first (tie -> right), pop while entry.t > tHit
+//   RaySceneIntersect tail          traverse.cuh:192-217 (normal flips, miss normal)
+//
+// GPU mapping: the per-ray box helper is re-expressed per world axis (near/far plane
+// selection by direction sign) so the inner loop indexes nothing dynamically; the stack
+// lives in LDS as [entry][thread] columns (conflict-free ds_read/write_b32); nodes are the
+// canonical 64-B records (4 x dwordx4), triangles 3 x float4.
+#pragma once
+#include "rt_device.h"
+
+namespace rtd {
+
+struct RayBox {
+    // per world axis a = x, y, z
+    float on[3], of[3], rn[3], rf[3];
+    bool neg[3];
+};
+
+RT_DEV int max_dim(F3 d) {
+    if (d.x > d.y) return d.z > d.x ? 2 : 0;
+    return d.z > d.y ? 2 : 1;
+}
+
+RT_DEV float Up(float a) { return a * (1.0f + 1.1920928955078125e-07f); }
+RT_DEV float Dn(float a) { return a * (1.0f - 1.1920928955078125e-07f); }
+RT_DEV float up_(float a) { return a > 0.0f ? Up(a) : Dn(a); }
+RT_DEV float dn_(float a) { return a > 0.0f ? Dn(a) : Up(a); }
+
+RT_DEV RayBox make_raybox(F3 org, F3 dir, const Box& scene, F3 inv) {
+    const int kz = max_dim(abs3(dir));
+    int kx = kz + 1; if (kx == 3) kx = 0;
+    int ky = kx + 1; if (ky == 3) ky = 0;
+    if (comp(dir, kz) < 0.0f) { const int t = kx; kx = ky; ky = t; }
+    const float eps = 5.0f * 5.9604644775390625e-08f;
+    const F3 lo = abs3(org - scene.mn), hi = abs3(org - scene.mx);
+    const F3 lower = f3(Dn(lo.x), Dn(lo.y), Dn(lo.z));
+    const F3 upper = f3(Up(hi.x), Up(hi.y), Up(hi.z));
+    const float max_z = fmx(comp(lower, kz), comp(upper, kz));
+    const float err_near_x = Up(comp(lower, kx) + max_z);
+    const float err_near_y = Up(comp(lower, ky) + max_z);
+    float onx = up_(comp(org, kx) + Up(eps * err_near_x));
+    float ony = up_(comp(org, ky) + Up(eps * err_near_y));
+    const float onz = comp(org, kz);
+    const float err_far_x = Up(comp(upper, kx) + max_z);
+    const float err_far_y = Up(comp(upper, ky) + max_z);
+    float ofx = dn_(comp(org, kx) - Up(eps * err_far_x));
+    float ofy = dn_(comp(org, ky) - Up(eps * err_far_y));
+    const float ofz = comp(org, kz);
+    if (comp(dir, kx) < 0.0f) { const float t = onx; onx = ofx; ofx = t; }
+    if (comp(dir, ky) < 0.0f) { const float t = ony; ony = ofy; ofy = t; }
+    RayBox h;
+    const float on_k[3] = {onx, ony, onz}, of_k[3] = {ofx, ofy, ofz};
+    const int ks[3] = {kx, ky, kz};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            if (ks[q] == a) {
+                h.on[a] = on_k[q];
+                h.of[a] = of_k[q];
+                const float ia = comp(inv, a);
+                h.rn[a] = Dn(Dn(ia));
+                h.rf[a] = Up(Up(ia));
+                h.neg[a] = comp(dir, a) < 0.0f;
+            }
+        }
+    }
+    return h;
+}
+
+// box test; min/max order is irrelevant here (no NaN can arise, and the sign of a zero
+// tNear is erased by max(tNear, 0)), so the hardware 3-operand min/max are used.
+RT_DEV bool box_test(const RayBox& h, float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float& tNear) {
+    const float tnx = ((h.neg[0] ? mxx : mnx) - h.on[0]) * h.rn[0];
+    const float tny = ((h.neg[1] ? mxy : mny) - h.on[1]) * h.rn[1];
+    const float tnz = ((h.neg[2] ? mxz : mnz) - h.on[2]) * h.rn[2];
+    const float tfx = ((h.neg[0] ? mnx : mxx) - h.of[0]) * h.rf[0];
+    const float tfy = ((h.neg[1] ? mny : mxy) - h.of[1]) * h.rf[1];
+    const float tfz = ((h.neg[2] ? mnz : mxz) - h.of[2]) * h.rf[2];
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz);
+    const float tf = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
+    const bool hit = tn <= tf && tf > 0.0f;
+    tNear = fmx(tn, 0.0f);
+    return hit;
+}
+
+struct TriRay {
+    int kx, ky, kz;
+    float Sx, Sy, Sz;
+};
+
+RT_DEV TriRay make_triray(F3 dir) {
+    TriRay r;
+    r.kz = max_dim(abs3(dir));
+    r.kx = r.kz + 1; if (r.kx == 3) r.kx = 0;
+    r.ky = r.kx + 1; if (r.ky == 3) r.ky = 0;
+    if (comp(dir, r.kz) < 0.0f) { const int t = r.kx; r.kx = r.ky; r.ky = t; }
+    r.Sx = comp(dir, r.kx) / comp(dir, r.kz);
+    r.Sy = comp(dir, r.ky) / comp(dir, r.kz);
+    r.Sz = 1.0f / comp(dir, r.kz);
+    return r;
+}
+
+RT_DEV float xorf(float a, uint32_t b) { return __uint_as_float(__float_as_uint(a) ^ b); }
+
+// RayTriangleWatertight (geometry.cuh:406-472); u, v, e are written whenever it returns true
+RT_DEV bool watertight(const TriRay& r, F3 org, F3 v1, F3 v2, F3 v3, float tCur, float& t, float& u, float& v, float& e) {
+    const F3 A = v1 - org, B = v2 - org, C = v3 - org;
+    const float Akz = comp(A, r.kz), Bkz = comp(B, r.kz), Ckz = comp(C, r.kz);
+    const float Ax = comp(A, r.kx) - r.Sx * Akz;
+    const float Ay = comp(A, r.ky) - r.Sy * Akz;
+    const float Bx = comp(B, r.kx) - r.Sx * Bkz;
+    const float By = comp(B, r.ky) - r.Sy * Bkz;
+    const float Cx = comp(C, r.kx) - r.Sx * Ckz;
+    const float Cy = comp(C, r.ky) - r.Sy * Ckz;
+    float U = Cx * By - Cy * Bx;
+    float V = Ax * Cy - Ay * Cx;
+    float W = Bx * Ay - By * Ax;
+    if (U == 0.0f || V == 0.0f || W == 0.0f) {
+        const double CxBy = (double)Cx * (double)By, CyBx = (double)Cy * (double)Bx;
+        U = (float)(CxBy - CyBx);
+        const double AxCy = (double)Ax * (double)Cy, AyCx = (double)Ay * (double)Cx;
+        V = (float)(AxCy - AyCx);
+        const double BxAy = (double)Bx * (double)Ay, ByAx = (double)By * (double)Ax;
+        W = (float)(BxAy - ByAx);
+    }
+    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
+    const float det = U + V + W;
+    if (det == 0.0f) return false;
+    const float Az = r.Sz * Akz, Bz = r.Sz * Bkz, Cz = r.Sz * Ckz;
+    const float T = U * Az + V * Bz + W * Cz;
+    const uint32_t ds = __float_as_uint(det) & 0x80000000u;
+    if ((xorf(T, ds) < 0.0f) || (xorf(T, ds) > tCur * xorf(det, ds))) return false;
+    const float rcp = 1.0f / det;
+    u = U * rcp;
+    v = V * rcp;
+    t = T * rcp;
+    e = err_gamma(16) * fabsf(t);
+    return true;
+}
+
+struct SceneView {
+    const float4* triPos;   // [N][3]
+    const float4* triNrm;   // [N][3]
+    const Node* nodes;      // BLAS, 1024 per batch
+    const Node* tlas;       // TLAS
+};
+
+struct HitInfo {
+    float t;
+    int objectIdx;
+    float u, v;
+    F3 normal, fakeNormal, pos;
+    float offset;
+    bool hit;
+    uint32_t visits, tests, dropped, iters;
+};
+
+RT_DEV Box node_merged(const Node& n) {
+    Box b;
+    b.mx = f3(fmx(n.q0.w, n.q2.y), fmx(n.q1.x, n.q2.z), fmx(n.q1.y, n.q2.w));
+    b.mn = f3(fmn(n.q0.x, n.q1.z), fmn(n.q0.y, n.q1.w), fmn(n.q0.z, n.q2.x));
+    return b;
+}
+
+RT_DEV F3 f3_of(float4 a) { return f3(a.x, a.y, a.z); }
+
+// stack entry: idx (15) | blasOffset (15) << 15 | isBlas << 30 | isLeaf << 31  + float t
+// stkA / stkT point at this thread's column: element k lives at [k * stride].
+RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint32_t* stkA, float* stkT, int stride, HitInfo& out) {
+    const F3 inv = f3(safe_divide(1.0f, dir.x), safe_divide(1.0f, dir.y), safe_divide(1.0f, dir.z));
+    float t = kRayMax;
+    int objectIdx = -1;
+    float u = 0.0f, v = 0.0f, errorT = 1e-7f;
+    int hitIdx = -1;
+    float hitU = 0.0f, hitV = 0.0f, hitErrT = 1e-7f;
+    uint32_t visits = 0, tests = 0, dropped = 0, iters = 0;
+
+    const Box sceneBox = node_merged(sc.tlas[0]);
+    const RayBox h = make_raybox(org, dir, sceneBox, inv);
+    const TriRay tr = make_triray(dir);
+
+    int top = -1;
+    uint32_t cIdx = 0, cOff = 0;
+    bool cBlas = false, cLeaf = false;
+    float cT = -kFltMax;
+
+    for (int it = 0; it < 1024; ++it) {
+        ++iters;
+        bool pop = false;
+        if (cLeaf) {
+            if (cBlas) {
+                const uint32_t li = cOff * 1024u + cIdx;
+                const float4 p0 = sc.triPos[3 * li], p1 = sc.triPos[3 * li + 1], p2 = sc.triPos[3 * li + 2];
+                ++tests;
+                float tt;
+                if (watertight(tr, org, f3_of(p0), f3_of(p1), f3_of(p2), t, tt, u, v, errorT) && tt < t) {
+                    t = tt;
+                    objectIdx = (int)li;
+                    hitIdx = (int)li;
+                    hitU = u; hitV = v; hitErrT = errorT;
+                }
+                pop = true;
+            } else {
+                cLeaf = false;
+                cBlas = true;
+                cOff = cIdx;
+                cIdx = 0;
+            }
+        } else {
+            const Node nd = cBlas ? sc.nodes[cOff * 1024u + cIdx] : sc.tlas[cIdx];
+            ++visits;
+            float t1, t2;
+            const bool i1 = box_test(h, nd.q0.x, nd.q0.y, nd.q0.z, nd.q0.w, nd.q1.x, nd.q1.y, t1);
+            const bool i2 = box_test(h, nd.q1.z, nd.q1.w, nd.q2.x, nd.q2.y, nd.q2.z, nd.q2.w, t2);
+            if (!i1 && !i2) {
+                pop = true;
+            } else if (i1 && !i2) {
+                cIdx = nd.q3.x; cLeaf = nd.q3.z != 0u; cT = t1;
+            } else if (!i1 && i2) {
+                cIdx = nd.q3.y; cLeaf = nd.q3.w != 0u; cT = t2;
+            } else {
+                const bool leftFirst = t1 < t2;
+                const uint32_t pIdx = leftFirst ? nd.q3.y : nd.q3.x;
+                const uint32_t pLeaf = leftFirst ? nd.q3.w : nd.q3.z;
+                const float pT = leftFirst ? t2 : t1;
+                if (top >= 15) {
+                    ++dropped;
+                } else {
+                    ++top;
+                    stkA[top * stride] = (pIdx & 0x7FFFu) | ((cOff & 0x7FFFu) << 15) | ((cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31);
+                    stkT[top * stride] = pT;
+                }
+                cIdx = leftFirst ? nd.q3.x : nd.q3.y;
+                cLeaf = (leftFirst ? nd.q3.z : nd.q3.w) != 0u;
+                cT = leftFirst ? t1 : t2;
+            }
+        }
+        if (pop) {  // TestForFinish (traverse.h:88-105)
+            bool finished = false;
+            do {
+                if (top < 0) { finished = true; break; }
+                const uint32_t a = stkA[top * stride];
+                cT = stkT[top * stride];
+                --top;
+                cIdx = a & 0x7FFFu;
+                cOff = (a >> 15) & 0x7FFFu;
+                cBlas = (a >> 30) & 1u;
+                cLeaf = (a >> 31) & 1u;
+            } while (cT > t);
+            if (finished) break;
+        }
+    }
+
+    // hit finalisation (traverse.h:161-174, traverse.cuh:192-217), once for the closest hit
+    F3 nrm = f3(0.0f), pos = f3(kRayMax), fake = f3(0.0f);
+    float offset = 1e-7f;
+    if (hitIdx >= 0) {
+        const F3 v1 = f3_of(sc.triPos[3 * hitIdx]), v2 = f3_of(sc.triPos[3 * hitIdx + 1]), v3 = f3_of(sc.triPos[3 * hitIdx + 2]);
+        nrm = normalize(cross(v2 - v1, v3 - v1));
+        const float w = -dot(nrm, v1);
+        const F3 p = org + dir * t;
+        pos = p - (dot(nrm, p) + w) * nrm;
+        const F3 ap = abs3(pos);
+        const float errorP = fmx(fmx(ap.x, ap.y), ap.z) * err_gamma(6);
+        offset = hitErrT + errorP;
+        const F3 n1 = normalize(f3_of(sc.triNrm[3 * hitIdx]));
+        const F3 n2 = normalize(f3_of(sc.triNrm[3 * hitIdx + 1]));
+        const F3 n3 = normalize(f3_of(sc.triNrm[3 * hitIdx + 2]));
+        fake = normalize(n3 * (1.0f - hitU - hitV) + n1 * hitU + n2 * hitV);
+    }
+    const float ndr = dot(nrm, dir);
+    if (!(ndr < 0.0f)) nrm = -nrm;
+    if (dot(fake, nrm) < 0.0f) fake = -fake;
+    const bool hit = t < kRayMax;
+    if (!hit) { nrm = f3(0.0f, -1.0f, 0.0f); fake = f3(0.0f, -1.0f, 0.0f); }
+    out.t = t;
+    out.objectIdx = objectIdx;
+    out.u = u;
+    out.v = v;
+    out.normal = nrm;
+    out.fakeNormal = fake;
+    out.pos = pos;
+    out.offset = offset;
+    out.hit = hit;
+    out.visits = visits; out.tests = tests; out.dropped = dropped; out.iters = iters;
+}
+
+}  // namespace rtd

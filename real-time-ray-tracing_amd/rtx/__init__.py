@@ -1,0 +1,242 @@
+"""rtx — Python host interface of the MI355X path tracer (ctypes over librtx.so).
+
+Mirrors the reference renderer API, ``class RayTracer`` (/root/reference/src/kernel.cuh:431-470):
+``RayTracer(screen_w, screen_h, config)`` -> ``init()`` -> ``draw()`` ... -> ``cleanup()``,
+plus the hot-path stages (``build_bvh``, ``trace_primary``) and array downloads used by the
+parity tests and bench.  Everything runs in librtx.so (hand-written HIP for gfx950); there
+is no CPU fallback: a missing or unloadable library raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG, "lib", "librtx.so")
+DATA_DIR = os.path.join(_PKG, "data")
+
+RT_OK = 0
+ERRORS = {-1: "RT_ERR_ARG", -2: "RT_ERR_HIP", -3: "RT_ERR_IO", -4: "RT_ERR_STATE", -5: "RT_ERR_NO_DEVICE"}
+
+# rt_array_name (include/rtx_amd.h)
+ARR = dict(VERTICES=0, INDICES=1, NORMALS=2, TRI_POS=3, AABBS=4, MORTON=5, REORDER=6, NODES=7, TLAS_AABBS=8,
+           TLAS_MORTON=9, TLAS_REORDER=10, TLAS_NODES=11, TLAS_SCENE_AABB=12, BATCH_SCENE_AABBS=13, HITS=14,
+           HIT_NORMALS=15, HIT_FAKE_NORMALS=16, HIT_STATS=17, TRI_NRM=18)
+# rt_buffer_name (Buffer2DName, kernel.cuh:286-315)
+BUF = dict(RENDER_COLOR=0, ACCUMULATION=1, HISTORY_COLOR=2, SCALED_COLOR=3, NORMAL=10, DEPTH=11, HISTORY_DEPTH=12,
+           MOTION=13, NOISE_LEVEL=14, NOISE_LEVEL16=15, SKY=16, SUN=17, ALBEDO=18)
+
+# canonical 64-byte BVH node as a numpy record (see RT_ARR_NODES)
+NODE_DTYPE = np.dtype([("lmin", "<f4", 3), ("lmax", "<f4", 3), ("rmin", "<f4", 3), ("rmax", "<f4", 3),
+                       ("idxLeft", "<u4"), ("idxRight", "<u4"), ("isLeftLeaf", "<u4"), ("isRightLeaf", "<u4")])
+
+
+class SkyParams(C.Structure):
+    _fields_ = [("needRegenerate", C.c_int32), ("timeOfDay", C.c_float), ("sunAxisAngle", C.c_float),
+                ("skyScalar", C.c_float), ("sunScalar", C.c_float), ("sunAngle", C.c_float)]
+
+
+class SampleParams(C.Structure):
+    _fields_ = [("sampleSurfaceVsLightUseMisWeight", C.c_int32), ("sampleSkyVsSunUseFluxWeight", C.c_int32),
+                ("sampleSurfaceVsLight", C.c_float), ("sampleSkyVsSun", C.c_float)]
+
+
+class RenderPassSettings(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "enableTemporalDenoising", "enableLocalSpatialFilter", "enableNoiseLevelVisualize",
+        "enableWideSpatialFilter", "enableTemporalDenoising2", "enablePostProcess", "enableDownScalePasses",
+        "enableHistogram", "enableAutoExposure", "enableBloomEffect", "enableLensFlare", "enableToneMapping",
+        "enableSharpening")]
+
+
+class PostProcessParams(C.Structure):
+    _fields_ = [("toneMappingType", C.c_int32), ("exposure", C.c_float), ("gain", C.c_float),
+                ("maxWhite", C.c_float), ("gamma", C.c_float)]
+
+
+class DenoisingParams(C.Structure):
+    _fields_ = [(n, C.c_float) for n in (
+        "local_denoise_sigma_normal", "local_denoise_sigma_depth", "local_denoise_sigma_material",
+        "large_denoise_sigma_normal", "large_denoise_sigma_depth", "large_denoise_sigma_material",
+        "temporal_denoise_sigma_normal", "temporal_denoise_sigma_depth", "temporal_denoise_sigma_material",
+        "noise_threshold_local", "noise_threshold_large")]
+
+
+class Params(C.Structure):
+    _fields_ = [("sky", SkyParams), ("sample", SampleParams), ("pass_", RenderPassSettings),
+                ("post", PostProcessParams), ("denoise", DenoisingParams)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("yaw", C.c_float), ("pitch", C.c_float), ("focal", C.c_float),
+                ("aperture", C.c_float), ("fovX", C.c_float)]
+
+
+class Info(C.Structure):
+    _fields_ = [("triCount", C.c_uint32), ("triCountPadded", C.c_uint32), ("batchCount", C.c_uint32),
+                ("vertexCount", C.c_uint32), ("renderWidth", C.c_int32), ("renderHeight", C.c_int32),
+                ("screenWidth", C.c_int32), ("screenHeight", C.c_int32), ("frameNum", C.c_int32),
+                ("deviceId", C.c_int32), ("spp", C.c_uint32)]
+
+
+# every entry point declared in include/rtx_amd.h, with its ctypes signature
+SIGNATURES = {
+    "rt_create": (C.c_int, [C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_void_p)]),
+    "rt_init": (C.c_int, [C.c_void_p]),
+    "rt_draw": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_destroy": (None, [C.c_void_p]),
+    "rt_last_error": (C.c_char_p, [C.c_void_p]),
+    "rt_get_params": (C.c_int, [C.c_void_p, C.POINTER(Params)]),
+    "rt_set_params": (C.c_int, [C.c_void_p, C.POINTER(Params)]),
+    "rt_get_camera": (C.c_int, [C.c_void_p, C.POINTER(Camera)]),
+    "rt_set_camera": (C.c_int, [C.c_void_p, C.POINTER(Camera)]),
+    "rt_set_frame_index": (C.c_int, [C.c_void_p, C.c_int]),
+    "rt_set_delta_time": (C.c_int, [C.c_void_p, C.c_float]),
+    "rt_get_info": (C.c_int, [C.c_void_p, C.POINTER(Info)]),
+    "rt_get_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
+    "rt_build_bvh": (C.c_int, [C.c_void_p]),
+    "rt_trace_primary": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "rt_sync": (C.c_int, [C.c_void_p]),
+    "rt_time_stage": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float)]),
+    "rt_download": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
+    "rt_array_bytes": (C.c_size_t, [C.c_void_p, C.c_int]),
+}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Load librtx.so; raises if it is missing (no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError("librtx.so not found at %s — run `make` (or __graft_entry__.build())" % path)
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class RtError(RuntimeError):
+    pass
+
+
+def write_config(path: str, width: int, height: int, dynamic: bool = False, chunk_dim: int = 1, spp: int = 1,
+                 extra: str = "") -> str:
+    """Write a config.toml with the reference's three tables (resources/config.toml) + extensions."""
+    with open(path, "w") as f:
+        f.write("[resolution]\nwidth = %d\nheight = %d\n\n" % (width, height))
+        f.write("[file]\nloadCameraAtInit = false\n\n")
+        f.write("[optimziation]\nuseDynamicResolution = %s\ntargetFps = 60.0\nmaxWidth = 3840\nmaxHeight = 2160\n"
+                "minWidth = 640\nminHeight = 480\n\n" % ("true" if dynamic else "false"))
+        f.write("[scene]\nchunkDim = %d\n\n[render]\nspp = %d\n" % (chunk_dim, spp))
+        f.write(extra)
+    return path
+
+
+class RayTracer:
+    """The reference's RayTracer lifecycle over the C-ABI (kernel.cuh:431-470)."""
+
+    def __init__(self, screen_width: int, screen_height: int, config: str | None = None):
+        self.lib = load_library()
+        h = C.c_void_p()
+        rc = self.lib.rt_create(screen_width, screen_height, config.encode() if config else None, C.byref(h))
+        if rc != RT_OK:
+            raise RtError("rt_create: %s %s" % (ERRORS.get(rc, rc), self.lib.rt_last_error(None).decode()))
+        self.h = h
+
+    # ---- lifecycle
+    def _check(self, rc, what):
+        if rc != RT_OK:
+            raise RtError("%s: %s %s" % (what, ERRORS.get(rc, rc), self.lib.rt_last_error(self.h).decode()))
+
+    def init(self):
+        self._check(self.lib.rt_init(self.h), "rt_init")
+        return self
+
+    def draw(self, rgba8: np.ndarray | None = None, hdr: np.ndarray | None = None):
+        self._check(self.lib.rt_draw(self.h, _ptr(rgba8), _ptr(hdr)), "rt_draw")
+
+    def cleanup(self):
+        if getattr(self, "h", None):
+            self.lib.rt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.cleanup()
+        except Exception:
+            pass
+
+    # ---- parameters
+    @property
+    def params(self) -> Params:
+        p = Params()
+        self._check(self.lib.rt_get_params(self.h, C.byref(p)), "rt_get_params")
+        return p
+
+    @params.setter
+    def params(self, p: Params):
+        self._check(self.lib.rt_set_params(self.h, C.byref(p)), "rt_set_params")
+
+    @property
+    def camera(self) -> Camera:
+        c = Camera()
+        self._check(self.lib.rt_get_camera(self.h, C.byref(c)), "rt_get_camera")
+        return c
+
+    @camera.setter
+    def camera(self, c: Camera):
+        self._check(self.lib.rt_set_camera(self.h, C.byref(c)), "rt_set_camera")
+
+    def set_frame_index(self, n: int):
+        self._check(self.lib.rt_set_frame_index(self.h, n), "rt_set_frame_index")
+
+    def set_delta_time(self, ms: float):
+        self._check(self.lib.rt_set_delta_time(self.h, ms), "rt_set_delta_time")
+
+    def info(self) -> Info:
+        i = Info()
+        self._check(self.lib.rt_get_info(self.h, C.byref(i)), "rt_get_info")
+        return i
+
+    # ---- hot-path stages
+    def build_bvh(self):
+        self._check(self.lib.rt_build_bvh(self.h), "rt_build_bvh")
+
+    def trace_primary(self, frame_num: int = 1, detail: bool = False):
+        self._check(self.lib.rt_trace_primary(self.h, frame_num, 1 if detail else 0), "rt_trace_primary")
+
+    def sync(self):
+        self._check(self.lib.rt_sync(self.h), "rt_sync")
+
+    def time_stage(self, stage: int, iters: int) -> float:
+        ms = C.c_float()
+        self._check(self.lib.rt_time_stage(self.h, stage, iters, C.byref(ms)), "rt_time_stage")
+        return ms.value
+
+    # ---- downloads
+    def download(self, name: str, dtype=np.uint8) -> np.ndarray:
+        what = ARR[name]
+        n = self.lib.rt_array_bytes(self.h, what)
+        buf = np.empty(n, dtype=np.uint8)
+        self._check(self.lib.rt_download(self.h, what, buf.ctypes.data, n), "rt_download(%s)" % name)
+        return buf.view(dtype)
+
+    def get_buffer(self, name: str, shape, dtype) -> np.ndarray:
+        out = np.empty(shape, dtype=dtype)
+        self._check(self.lib.rt_get_buffer(self.h, BUF[name], out.ctypes.data, out.nbytes), "rt_get_buffer")
+        return out
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data

@@ -1,0 +1,80 @@
+"""C-ABI boundary checks that need no GPU: librtx.so loads, exports every entry point the
+public header declares, and the host-side lifecycle/config handling behaves."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rtx_amd.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declares_the_renderer_api():
+    syms = declared_symbols()
+    for s in ("rt_create", "rt_init", "rt_draw", "rt_destroy", "rt_build_bvh", "rt_trace_primary",
+              "rt_get_buffer", "rt_set_params", "rt_set_camera"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol(rtx):
+    lib = rtx.load_library()
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    # and the Python mirror binds all of them
+    assert set(declared_symbols()) == set(rtx.SIGNATURES)
+
+
+def test_create_reads_config(rtx, tmp_path):
+    cfg = rtx.write_config(str(tmp_path / "c.toml"), 320, 200, dynamic=False, chunk_dim=2, spp=4)
+    rt = rtx.RayTracer(0, 0, cfg)
+    info = rt.info()
+    assert (info.screenWidth, info.screenHeight, info.renderWidth, info.renderHeight) == (320, 200, 320, 200)
+    assert info.spp == 4
+    p = rt.params
+    assert p.post.maxWhite == pytest.approx(7.0) and p.sky.timeOfDay == pytest.approx(0.25)
+    cam = rt.camera
+    assert list(cam.pos) == [-2.0, 2.0, -2.0] and cam.focal == 5.0
+    rt.cleanup()
+
+
+def test_dynamic_resolution_renders_at_max(rtx, tmp_path):
+    cfg = rtx.write_config(str(tmp_path / "c.toml"), 1920, 1080, dynamic=True)
+    rt = rtx.RayTracer(1920, 1080, cfg)
+    info = rt.info()
+    assert (info.renderWidth, info.renderHeight) == (3840, 2160)  # init.cu:58-62
+    rt.cleanup()
+
+
+def test_bad_config_is_an_error_not_an_exit(rtx, tmp_path):
+    with pytest.raises(rtx.RtError):
+        rtx.RayTracer(64, 64, str(tmp_path / "missing.toml"))
+    bad = tmp_path / "bad.toml"
+    bad.write_text("[resolution\nwidth = 3\n")
+    with pytest.raises(rtx.RtError):
+        rtx.RayTracer(64, 64, str(bad))
+
+
+def test_stage_calls_before_init_fail_cleanly(rtx):
+    rt = rtx.RayTracer(64, 64, None)
+    lib = rt.lib
+    assert lib.rt_build_bvh(rt.h) == -4
+    assert lib.rt_trace_primary(rt.h, 1, 0) == -4
+    rt.cleanup()
+
+
+def test_init_without_gpu_reports_no_device(rtx, tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    cfg = rtx.write_config(str(tmp_path / "c.toml"), 64, 64)
+    rt = rtx.RayTracer(64, 64, cfg)
+    with pytest.raises(rtx.RtError, match="RT_ERR_NO_DEVICE"):
+        rt.init()
+    rt.cleanup()

@@ -1,0 +1,67 @@
+"""GPU LBVH build (one fused launch) vs the CPU oracle: bit-exact Morton codes, reorder
+indices, node topology and boxes, TLAS — default scene and the ~1M-triangle variant."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def build_gpu(rtx, tmp_path, chunk_dim, w=64, h=64):
+    cfg = rtx.write_config(str(tmp_path / ("c%d.toml" % chunk_dim)), w, h, chunk_dim=chunk_dim)
+    rt = rtx.RayTracer(w, h, cfg).init()
+    rt.build_bvh()
+    rt.sync()
+    return rt
+
+
+def as_nodes(rtx, raw):
+    return raw.view(rtx.NODE_DTYPE)
+
+
+@pytest.mark.parametrize("chunk_dim", [1, 4])
+def test_bvh_bit_exact(rtx, oracle, tmp_path, chunk_dim):
+    v, i, n = oracle.scene(chunk_dim)
+    rt = build_gpu(rtx, tmp_path, chunk_dim)
+    info = rt.info()
+    assert info.triCount == n and info.triCountPadded == i.shape[0]
+    gv = rt.download("VERTICES", np.float32).reshape(-1, 3)
+    gi = rt.download("INDICES", np.uint32).reshape(-1, 3)
+    assert np.array_equal(gv, v) and np.array_equal(gi, i)
+    gn = rt.download("NORMALS", np.float32).reshape(-1, 3)
+    on = oracle.smooth_normals(v, i)
+    assert np.array_equal(gn.view(np.uint32), on.view(np.uint32)), "smooth normals differ"
+    ob = oracle.build_bvh(v, i, n, on)
+    B = ob["batch_count"]
+    assert info.batchCount == B
+    assert np.array_equal(rt.download("MORTON", np.uint32), ob["morton"])
+    assert np.array_equal(rt.download("REORDER", np.uint32), ob["reorder"])
+    aabbs = rt.download("AABBS", np.float32).reshape(-1, 6)
+    assert np.array_equal(aabbs.view(np.uint32), ob["aabbs"].view(np.uint32))
+    bs = rt.download("BATCH_SCENE_AABBS", np.float32).reshape(-1, 6)
+    assert np.array_equal(bs, ob["batch_scene_aabbs"])
+    gnodes = as_nodes(rtx, rt.download("NODES"))
+    for k in range(B):
+        cnt = 1024 if k < B - 1 else n - (B - 1) * 1024
+        g = gnodes[k * 1024:k * 1024 + cnt - 1]
+        o = ob["nodes"][k * 1024:k * 1024 + cnt - 1]
+        assert g.tobytes() == o.tobytes(), "batch %d nodes differ" % k
+    assert np.array_equal(rt.download("TLAS_AABBS", np.float32).reshape(-1, 6), ob["tlas_aabbs"])
+    assert np.array_equal(rt.download("TLAS_SCENE_AABB", np.float32), ob["tlas_scene_aabb"])
+    assert np.array_equal(rt.download("TLAS_MORTON", np.uint32), ob["tlas_morton"])
+    assert np.array_equal(rt.download("TLAS_REORDER", np.uint32), ob["tlas_reorder"])
+    assert as_nodes(rtx, rt.download("TLAS_NODES")).tobytes() == ob["tlas_nodes"].tobytes()
+    tp = rt.download("TRI_POS", np.float32).reshape(-1, 3, 4)[:, :, :3].reshape(-1, 9)
+    assert np.array_equal(tp, ob["triangles"][:, :9])
+    rt.cleanup()
+
+
+def test_bvh_rebuild_is_idempotent(rtx, tmp_path):
+    rt = build_gpu(rtx, tmp_path, 1)
+    first = rt.download("NODES").copy()
+    tlas = rt.download("TLAS_NODES").copy()
+    for _ in range(5):
+        rt.build_bvh()
+    rt.sync()
+    assert np.array_equal(rt.download("NODES"), first)
+    assert np.array_equal(rt.download("TLAS_NODES"), tlas)
+    rt.cleanup()

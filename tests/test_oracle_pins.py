@@ -1,0 +1,117 @@
+"""Pin the CPU oracle to the reference: known answers SURVEY.md recorded from the reference's
+own code and scene (tests/golden/golden.json "survey_pins"), plus regression digests."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+PINS = GOLD["survey_pins"]
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def leaf_depths(nodes):
+    """nodes on each root-to-leaf path, leaf included (SURVEY §0 #8c counts this way)"""
+    out, st = [], [(0, 1)]
+    while st:
+        v, d = st.pop()
+        nd = nodes[v]
+        for idx, leaf in ((nd["idxLeft"], nd["isLeftLeaf"]), (nd["idxRight"], nd["isRightLeaf"])):
+            if leaf:
+                out.append(d + 1)
+            else:
+                st.append((int(idx), d + 1))
+    return out
+
+
+def batch_slices(b):
+    B, n = b["batch_count"], b["tri_count"]
+    for k in range(B):
+        cnt = 1024 if k < B - 1 else n - (B - 1) * 1024
+        yield k, cnt
+
+
+def check_tree(nodes, n):
+    """valid binary tree over n leaves: every internal node except the root has one parent."""
+    parents = np.zeros(n - 1, np.int32)
+    leaves = np.zeros(n, np.int32)
+    for nd in nodes[:n - 1]:
+        for idx, leaf in ((nd["idxLeft"], nd["isLeftLeaf"]), (nd["idxRight"], nd["isRightLeaf"])):
+            if leaf:
+                leaves[idx] += 1
+            else:
+                parents[idx] += 1
+    assert parents[0] == 0 and (parents[1:] == 1).all() and (leaves == 1).all()
+
+
+def test_morton3_known_answer(oracle):
+    assert oracle.lib().orc_morton3(1023, 0, 0) == PINS["morton3_1023_0_0"]
+
+
+@pytest.mark.parametrize("key,cd", [("default", 1), ("chunk4", 4)])
+def test_scene_and_bvh_pins(oracle, key, cd):
+    pin = PINS[key]
+    v, i, n = oracle.scene(cd)
+    assert n == pin["triCount"]
+    b = oracle.build_bvh(v, i, n, oracle.smooth_normals(v, i))
+    assert b["batch_count"] == pin["batchCount"]
+    depths, dup = [], 0
+    for k, cnt in batch_slices(b):
+        keys = b["morton"][k * 1024:k * 1024 + cnt]
+        dup += cnt - len(np.unique(keys))
+        nodes = b["nodes"][k * 1024:k * 1024 + cnt - 1]
+        check_tree(nodes, cnt)
+        depths.append(max(leaf_depths(nodes)))
+    assert cnt == pin["lastBatch"]
+    assert dup == pin["dupKeys"]
+    assert [min(depths), int(np.median(depths)), max(depths)] == pin["blasDepthMinMedMax"]
+    check_tree(b["tlas_nodes"], b["batch_count"])
+    assert max(leaf_depths(b["tlas_nodes"])) == pin["tlasDepth"]
+    if "quirkBoxMaxXY" in pin:
+        sb = b["tlas_scene_aabb"]
+        assert [float(sb[3]), float(sb[4])] == pytest.approx(pin["quirkBoxMaxXY"], abs=1e-5)
+        ta = b["tlas_aabbs"]
+        assert [float(ta[:, 3].max()), float(ta[:, 4].max())] == pytest.approx(pin["trueBoxMaxXY"], abs=1e-5)
+        c = (ta[:, 3:] + ta[:, :3]) / np.float32(2)
+        u = (c - sb[:3]) / (sb[3:] - sb[:3])
+        assert int(((u < 0) | (u > 1)).any(1).sum()) == pin["tlasCentresOutside"]
+
+
+def test_sorted_keys_are_stable_sort_of_unsorted(default_scene):
+    b = default_scene["bvh"]
+    for k, cnt in batch_slices(b):
+        uns = b["morton_unsorted"][k * 1024:(k + 1) * 1024]
+        order = np.argsort(uns, kind="stable")
+        assert (b["reorder"][k * 1024:(k + 1) * 1024] == order).all()
+        assert (b["morton"][k * 1024:(k + 1) * 1024] == uns[order]).all()
+
+
+def test_oracle_regression_digests(default_scene, oracle):
+    g = GOLD["oracle"]["default"]
+    assert sha(default_scene["vertices"]) == g["vertices_sha256"]
+    assert sha(default_scene["indices"]) == g["indices_sha256"]
+    assert sha(default_scene["normals"]) == g["normals_sha256"]
+    b = default_scene["bvh"]
+    assert sha(b["morton"]) == g["morton_sha256"]
+    assert sha(b["reorder"]) == g["reorder_sha256"]
+    assert sha(b["tlas_nodes"]) == g["tlas_nodes_sha256"]
+    rays, _ = oracle.primary_rays(64, 64, 1)
+    assert sha(rays) == g["primary64_rays_sha256"]
+    assert sha(oracle.intersect(b, rays)) == g["primary64_hits_sha256"]
+
+
+def test_primary_rays_hit_terrain(default_scene, oracle):
+    rays, cone = oracle.primary_rays(64, 64, 1)
+    hits = oracle.intersect(default_scene["bvh"], rays)
+    # default camera (-2,2,-2) looks +z from below the terrain top (y 5..11): up-left rays hit
+    assert 0.05 < hits["hit"].mean() < 0.95
+    assert (hits["t"][hits["hit"] == 1] < 40).all()
+    assert (hits["objectIdx"][hits["hit"] == 0] == -1).all()
+    nz = np.linalg.norm(hits["normal"][hits["hit"] == 1], axis=1)
+    assert np.allclose(nz, 1, atol=1e-5)
+    assert (cone > 0).all()

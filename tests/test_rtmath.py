@@ -1,0 +1,57 @@
+"""rtmath.h (the deterministic transcendentals shared by kernels and oracle) vs float64 numpy."""
+import math
+
+import numpy as np
+import pytest
+
+FNS = {
+    "sin": (np.sin, (-50, 50)), "cos": (np.cos, (-50, 50)), "tan": (np.tan, (-1.5, 1.5)),
+    "atan": (np.arctan, (-100, 100)), "acos": (np.arccos, (-1, 1)), "asin": (np.arcsin, (-1, 1)),
+    "exp": (np.exp, (-80, 80)), "exp2": (np.exp2, (-120, 120)), "log": (np.log, (1e-30, 1e30)),
+    "log2": (np.log2, (1e-30, 1e30)),
+}
+
+
+def ulp_err(got, ref):
+    ref32 = np.float32(ref)
+    if not np.isfinite(ref32):
+        return 0 if got == ref32 else 99
+    return abs(int(np.float32(got).view(np.int32)) - int(ref32.view(np.int32)))
+
+
+@pytest.mark.parametrize("name", sorted(FNS))
+def test_rtmath_faithful(oracle, name):
+    f, (lo, hi) = FNS[name]
+    rng = np.random.default_rng(7)
+    if name in ("log", "log2"):
+        xs = np.float32(10.0) ** rng.uniform(-30, 30, 3000).astype(np.float32)
+    else:
+        xs = rng.uniform(lo, hi, 3000).astype(np.float32)
+    worst = 0
+    for x in xs:
+        worst = max(worst, ulp_err(oracle.rtmath(name, float(x)), f(np.float64(x))))
+    assert worst <= 1, "%s worst ulp %d" % (name, worst)
+
+
+def test_rtmath_pow_atan2(oracle):
+    rng = np.random.default_rng(3)
+    worst = 0
+    for _ in range(3000):
+        x, y = np.float32(rng.uniform(0, 20)), np.float32(rng.uniform(-8, 8))
+        worst = max(worst, ulp_err(oracle.rtmath("pow", float(x), float(y)), np.float64(x) ** np.float64(y)))
+        a, b = np.float32(rng.uniform(-5, 5)), np.float32(rng.uniform(-5, 5))
+        worst = max(worst, ulp_err(oracle.rtmath("atan2", float(a), float(b)), np.arctan2(np.float64(a), np.float64(b))))
+    assert worst <= 1
+
+
+def test_rtmath_special_cases(oracle):
+    assert oracle.rtmath("pow", 0.0, 2.0) == 0.0
+    assert oracle.rtmath("pow", 2.0, 0.0) == 1.0
+    assert math.isinf(oracle.rtmath("pow", 0.0, -1.0))
+    assert math.isnan(oracle.rtmath("acos", 1.5))
+    assert oracle.rtmath("acos", 1.0) == 0.0
+    assert oracle.rtmath("exp", -200.0) == 0.0
+    assert math.isinf(oracle.rtmath("exp", 200.0))
+    assert oracle.rtmath("log2", 8.0) == 3.0
+    assert math.isinf(oracle.rtmath("log", 0.0)) and oracle.rtmath("log", 0.0) < 0
+    assert oracle.rtmath("atan2", 0.0, -1.0) == np.float32(np.pi)

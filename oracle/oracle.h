@@ -60,6 +60,8 @@ typedef struct OrcHit {
     uint32_t triTests;    // ray/triangle tests
     uint32_t droppedPushes;  // pushes lost to the 16-entry stack (traverse.h:34-36)
     uint32_t iterations;     // loop iterations used (cap 1024, traverse.h:132)
+    uint32_t intoSurface;    // isRayIntoSurface (traverse.cuh:193)
+    float ndr;               // normalDotRayDir after the flip (traverse.cuh:192-198)
 } OrcHit;
 
 // RaySceneIntersect core (traverse.cuh:64-225 without the material bookkeeping) for n rays.
@@ -84,6 +86,65 @@ float orc_bluenoise(const uint8_t* tables, int px, int py, int sampleIdx, int di
 
 // deterministic math probes (rtmath.h), for tests
 float orc_rtmath(int fn, float x, float y);
+
+// ---------------------------------------------------------------- sky (sky.cpp)
+typedef struct OrcSkyTables {
+    const float* skyDataSets;            // 540
+    const float* skyDataSetsRad;         // 60
+    const float* solarDatasets;          // 1800
+    const float* limbDarkeningDatasets;  // 60
+    const float* cieX; const float* cieY; const float* cieZ;  // 10 each
+} OrcSkyTables;
+
+typedef struct OrcSkyParams {
+    float timeOfDay, sunAxisAngle, skyScalar, sunScalar, sunAngle;
+} OrcSkyParams;
+
+typedef struct OrcSkyOut {
+    float sunDir[3];
+    float* skyBuffer;   // [256][512][4]
+    float* skyPdf;      // [131072]
+    float* skyCdf;      // [131072]
+    float* sunBuffer;   // [32][32][4]
+    float* sunPdf;      // [1024]
+    float* sunCdf;      // [1024]
+    float sunArea, sunAngleCosThetaMax;
+} OrcSkyOut;
+
+void orc_sky(const OrcSkyTables* tables, const OrcSkyParams* params, OrcSkyOut* out);
+void orc_sun_dir(float timeOfDay, float sunAxisAngle, float* out);
+void orc_scan(const float* in, float* out, int size, int blockSize);
+
+// ---------------------------------------------------------------- path trace (pathtrace.cpp)
+typedef struct OrcFrame {
+    OrcScene scene;
+    uint32_t triCount;
+    int32_t materialOverride;    // < 0: reference materialsIdx (3 for every triangle)
+    OrcCamera cam;               // current camera
+    OrcCamera histCam;           // camera of the previous frame (HistoryCamera::Setup)
+    int frameNum;
+    uint32_t spp;                // samples per pixel (build definition)
+    const uint8_t* bluenoise;
+    const uint16_t* texAlbedoAo;       // ushort4, 11 mip levels concatenated (1024 >> l)
+    const uint16_t* texNormalRough;
+    const float* skyBuffer; const float* sunBuffer;
+    const float* skyCdf; const float* sunCdf;
+    float sunDir[3];
+    float sunAngleCosThetaMax;
+} OrcFrame;
+
+typedef struct OrcGBuffer {
+    uint16_t* color;    // [P][4] half rgb + ushort mask
+    uint16_t* normal;   // [P][4] half
+    uint16_t* albedo;   // [P][4] half
+    uint16_t* depth;    // [P] half
+    uint16_t* motion;   // [P][2] half
+    uint32_t* rays;     // [P] RaySceneIntersect calls that traced (may be NULL)
+} OrcGBuffer;
+
+void orc_pathtrace(const OrcFrame* f, uint32_t W, uint32_t H, uint32_t y0, uint32_t rows, OrcGBuffer* out,
+                   int threads);
+void orc_textures(uint16_t* albedoAo, uint16_t* normalRough);  // 1398101 ushort4 texels each
 
 #ifdef __cplusplus
 }

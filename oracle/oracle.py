@@ -37,7 +37,7 @@ class Scene(C.Structure):
 HIT_DTYPE = np.dtype([("t", "<f4"), ("objectIdx", "<i4"), ("u", "<f4"), ("v", "<f4"), ("normal", "<f4", 3),
                       ("fakeNormal", "<f4", 3), ("pos", "<f4", 3), ("offset", "<f4"), ("hit", "<u4"),
                       ("nodeVisits", "<u4"), ("triTests", "<u4"), ("droppedPushes", "<u4"),
-                      ("iterations", "<u4")])
+                      ("iterations", "<u4"), ("intoSurface", "<u4"), ("ndr", "<f4")])
 
 
 class CameraIn(C.Structure):
@@ -74,6 +74,7 @@ def lib() -> C.CDLL:
         L.orc_scene_generate.restype = C.c_int
         L.orc_scene_copy.argtypes = [C.c_void_p, C.c_void_p]
         L.orc_scene_copy.restype = None
+        _bind_frame_api(L)
         _lib = L
     return _lib
 
@@ -166,3 +167,118 @@ RTMATH = dict(sin=0, cos=1, tan=2, atan=3, atan2=4, acos=5, asin=6, exp=7, exp2=
 
 def rtmath(fn: str, x: float, y: float = 0.0) -> float:
     return lib().orc_rtmath(RTMATH[fn], x, y)
+
+
+# ---------------------------------------------------------------- sky (oracle/sky.cpp)
+class SkyTables(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("skyDataSets", "skyDataSetsRad", "solarDatasets",
+                                          "limbDarkeningDatasets", "cieX", "cieY", "cieZ")]
+
+
+class SkyParams(C.Structure):
+    _fields_ = [(n, C.c_float) for n in ("timeOfDay", "sunAxisAngle", "skyScalar", "sunScalar", "sunAngle")]
+
+
+class SkyOut(C.Structure):
+    _fields_ = [("sunDir", C.c_float * 3), ("skyBuffer", C.c_void_p), ("skyPdf", C.c_void_p),
+                ("skyCdf", C.c_void_p), ("sunBuffer", C.c_void_p), ("sunPdf", C.c_void_p), ("sunCdf", C.c_void_p),
+                ("sunArea", C.c_float), ("sunAngleCosThetaMax", C.c_float)]
+
+
+class Frame(C.Structure):
+    _fields_ = [("scene", Scene), ("triCount", C.c_uint32), ("materialOverride", C.c_int32), ("cam", CameraIn),
+                ("histCam", CameraIn), ("frameNum", C.c_int), ("spp", C.c_uint32), ("bluenoise", C.c_void_p),
+                ("texAlbedoAo", C.c_void_p), ("texNormalRough", C.c_void_p), ("skyBuffer", C.c_void_p),
+                ("sunBuffer", C.c_void_p), ("skyCdf", C.c_void_p), ("sunCdf", C.c_void_p),
+                ("sunDir", C.c_float * 3), ("sunAngleCosThetaMax", C.c_float)]
+
+
+class GBuffer(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("color", "normal", "albedo", "depth", "motion", "rays")]
+
+
+SKY_DEFAULTS = dict(timeOfDay=0.25, sunAxisAngle=45.0, skyScalar=0.01, sunScalar=0.01, sunAngle=0.6)  # settingParams.h:41-45
+TEX_TEXELS = 1398101  # 11-level mip chain of a 1024^2 ushort4 texture
+
+
+def _bind_frame_api(L):
+    L.orc_sky.argtypes = [C.POINTER(SkyTables), C.POINTER(SkyParams), C.POINTER(SkyOut)]
+    L.orc_sky.restype = None
+    L.orc_sun_dir.argtypes = [C.c_float, C.c_float, C.c_void_p]
+    L.orc_sun_dir.restype = None
+    L.orc_scan.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+    L.orc_scan.restype = None
+    L.orc_textures.argtypes = [C.c_void_p, C.c_void_p]
+    L.orc_textures.restype = None
+    L.orc_pathtrace.argtypes = [C.POINTER(Frame), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                C.POINTER(GBuffer), C.c_int]
+    L.orc_pathtrace.restype = None
+
+
+def sky_tables() -> list:
+    raw = np.fromfile(os.path.join(DATA_DIR, "sky_tables.bin"), dtype=np.uint8)
+    count = int(raw[:4].view(np.uint32)[0])
+    lens = raw[4:4 + 4 * count].view(np.uint32)
+    off = 4 + 4 * count
+    out = []
+    for n in lens:
+        out.append(raw[off:off + 4 * int(n)].view(np.float32).copy())
+        off += 4 * int(n)
+    return out
+
+
+def sky(params: dict | None = None) -> dict:
+    """Sky + sun buffers, luminance pdfs and their inclusive-scan CDFs (kernel.cu:280-307)."""
+    L = lib()
+    p = dict(SKY_DEFAULTS, **(params or {}))
+    t = sky_tables()
+    tabs = SkyTables(*[a.ctypes.data for a in t])
+    out = dict(sky=np.zeros((256, 512, 4), np.float32), sky_pdf=np.zeros(131072, np.float32),
+               sky_cdf=np.zeros(131072, np.float32), sun=np.zeros((32, 32, 4), np.float32),
+               sun_pdf=np.zeros(1024, np.float32), sun_cdf=np.zeros(1024, np.float32))
+    so = SkyOut((C.c_float * 3)(), out["sky"].ctypes.data, out["sky_pdf"].ctypes.data, out["sky_cdf"].ctypes.data,
+                out["sun"].ctypes.data, out["sun_pdf"].ctypes.data, out["sun_cdf"].ctypes.data, 0.0, 0.0)
+    L.orc_sky(C.byref(tabs), C.byref(SkyParams(*[p[k] for k in SKY_DEFAULTS])), C.byref(so))
+    out["sun_dir"] = np.array(so.sunDir[:], np.float32)
+    out["sun_area"] = np.float32(so.sunArea)
+    out["cos_theta_max"] = np.float32(so.sunAngleCosThetaMax)
+    return out
+
+
+def scan(x: np.ndarray, block: int) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.zeros_like(x)
+    lib().orc_scan(x.ctypes.data, y.ctypes.data, x.size, block)
+    return y
+
+
+def textures():
+    a = np.zeros((TEX_TEXELS, 4), np.uint16)
+    n = np.zeros((TEX_TEXELS, 4), np.uint16)
+    lib().orc_textures(a.ctypes.data, n.ctypes.data)
+    return a, n
+
+
+def pathtrace(bvh: dict, width: int, height: int, frame_num: int = 1, spp: int = 1, cam: CameraIn | None = None,
+              hist_cam: CameraIn | None = None, sky_out: dict | None = None, tex=None, y0: int = 0,
+              rows: int | None = None, material_override: int = -1, threads: int = 0) -> dict:
+    """PathTrace G-buffers (pathtrace.cuh:11-128) for rows [y0, y0+rows): raw half/ushort bits."""
+    cam = cam or default_camera(width, height)
+    hist_cam = hist_cam or cam
+    sky_out = sky_out or sky()
+    tex = tex or textures()
+    rows = height - y0 if rows is None else rows
+    bn = bluenoise_tables()
+    sc = Scene(bvh["triangles"].ctypes.data, bvh["nodes"].ctypes.data, bvh["tlas_nodes"].ctypes.data,
+               bvh["triangles"].shape[0], bvh["batch_count"])
+    f = Frame(sc, bvh["tri_count"], material_override, cam, hist_cam, frame_num, spp, bn.ctypes.data,
+              tex[0].ctypes.data, tex[1].ctypes.data, sky_out["sky"].ctypes.data, sky_out["sun"].ctypes.data,
+              sky_out["sky_cdf"].ctypes.data, sky_out["sun_cdf"].ctypes.data,
+              (C.c_float * 3)(*sky_out["sun_dir"].tolist()), float(sky_out["cos_theta_max"]))
+    P = width * height
+    g = dict(color=np.zeros((P, 4), np.uint16), normal=np.zeros((P, 4), np.uint16),
+             albedo=np.zeros((P, 4), np.uint16), depth=np.zeros(P, np.uint16), motion=np.zeros((P, 2), np.uint16),
+             rays=np.zeros(P, np.uint32))
+    gb = GBuffer(*[g[k].ctypes.data for k in ("color", "normal", "albedo", "depth", "motion", "rays")])
+    lib().orc_pathtrace(C.byref(f), width, height, y0, rows, C.byref(gb), threads)
+    return g

@@ -217,7 +217,8 @@ void intersect_one(const OrcScene* sc, F3 org, F3 dir, OrcHit& out) {
     }
     // RaySceneIntersect tail (traverse.cuh:192-217)
     float ndr = dot(nrm, dir);
-    if (!(ndr < 0)) { nrm = -nrm; }
+    const bool into = ndr < 0;
+    if (!into) { nrm = -nrm; ndr = -ndr; }
     if (dot(fake, nrm) < 0) fake = -fake;
     bool hit = t < kRayMax;
     if (!hit) { nrm = f3(0.0f, -1.0f, 0.0f); fake = f3(0.0f, -1.0f, 0.0f); }
@@ -229,6 +230,8 @@ void intersect_one(const OrcScene* sc, F3 org, F3 dir, OrcHit& out) {
     out.pos[0] = pos.x; out.pos[1] = pos.y; out.pos[2] = pos.z;
     out.offset = offset;
     out.hit = hit ? 1u : 0u;
+    out.intoSurface = into ? 1u : 0u;
+    out.ndr = ndr;
     out.nodeVisits = visits; out.triTests = tests; out.droppedPushes = dropped; out.iterations = iters;
 }
 

@@ -28,4 +28,17 @@ bool load_tiles(const std::string& path, std::vector<std::vector<float>>& tiles,
 // chunkDim = VoxelsGenerator::kChunkDim (1 for the default scene, 4 for the ~1M variant).
 bool generate(int chunkDim, const std::vector<std::vector<float>>& tiles, SceneMesh& out, std::string& err);
 
+// Synthetic stand-in for the soil texture pair the reference loads but does not ship
+// (init.cu:524-549, .MISSING_LARGE_BLOBS): SoilAlbedoAo and SoilNormalRoughness, 1024^2
+// ushort4, with the reference's 11-level mip chain (MipmapGen, mipgen.cu:144-163:
+// mean of 4 texels in float, min 65535, truncated to ushort).  Deterministic integer hash.
+struct TexturePair {
+    static constexpr int kLevels = 11;
+    int size[kLevels];                 // 1024 >> level
+    size_t offset[kLevels];            // texel offset of each level (ushort4 units)
+    std::vector<uint16_t> albedoAo;     // ushort4 texels, all levels concatenated
+    std::vector<uint16_t> normalRough;  // ushort4 texels, all levels concatenated
+};
+void make_textures(TexturePair& t);
+
 }  // namespace rtscene

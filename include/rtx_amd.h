@@ -147,6 +147,7 @@ enum rt_buffer_name {
     RT_BUF_ALBEDO = 18         /* half4 */
 };
 int rt_get_buffer(const rt_context* ctx, int name, void* dst, size_t bytes);
+size_t rt_buffer_bytes(const rt_context* ctx, int name); /* 0 for names not available */
 
 /* ---------------------------------------------------------------- hot-path stages */
 
@@ -158,6 +159,16 @@ int rt_build_bvh(rt_context* ctx);
  * blue-noise sample of frame_num (pathtrace.cuh:116-130), enqueued asynchronously.
  * with_detail != 0 also stores normals / shading normals / traversal counters. */
 int rt_trace_primary(rt_context* ctx, int frame_num, int with_detail);
+
+/* PathTrace (pathtrace.cuh:11-128) for frame_num into the G-buffers (RT_BUF_RENDER_COLOR,
+ * NORMAL, ALBEDO, DEPTH, MOTION), after UpdateFrame's sky/sun regeneration when the sky
+ * parameters changed (kernel.cu:286-307).  spp > 1 ([render] spp) averages spp reference
+ * samples (frame indices spp*(frame_num-1)+1 ...).  with_detail != 0 also stores the per-pixel
+ * traced-ray count (RT_ARR_RAYS).  Asynchronous; the history camera advances (kernel.cu:357). */
+int rt_path_trace(rt_context* ctx, int frame_num, int with_detail);
+
+/* Traced rays (RaySceneIntersect calls that ran a traversal) accumulated since the last reset. */
+int rt_get_ray_count(rt_context* ctx, uint64_t* rays, int reset);
 
 /* wait for all work on the context stream */
 int rt_sync(rt_context* ctx);
@@ -187,7 +198,13 @@ enum rt_array_name {
     RT_ARR_HIT_NORMALS = 15,     /* float4[W*H]: geometric normal, hit flag */
     RT_ARR_HIT_FAKE_NORMALS = 16,/* float4[W*H]: shading normal, ray offset */
     RT_ARR_HIT_STATS = 17,       /* uint32[W*H][4]: node visits, tri tests, dropped pushes, iterations */
-    RT_ARR_TRI_NRM = 18          /* float4[triCountPadded][3] */
+    RT_ARR_TRI_NRM = 18,         /* float4[triCountPadded][3] */
+    RT_ARR_RAYS = 19,            /* uint32[W*H] traced rays per pixel (rt_path_trace with_detail) */
+    RT_ARR_SKY_PDF = 20,         /* float[131072] sky luminance (Sky kernel, sky.cuh:296-297) */
+    RT_ARR_SKY_CDF = 21,         /* float[131072] inclusive scan of the sky pdf */
+    RT_ARR_SUN_PDF = 22,         /* float[1024] */
+    RT_ARR_SUN_CDF = 23,         /* float[1024] */
+    RT_ARR_SUN_DIR = 24          /* float[4]: sunDir xyz, cos(sun half-angle) (host values) */
 };
 int rt_download(const rt_context* ctx, int what, void* dst, size_t bytes);
 size_t rt_array_bytes(const rt_context* ctx, int what);

@@ -366,7 +366,7 @@ static void glossy(Ctx& c, RayState& rs, float rnd) {
     if (rs.hitLight || rs.isDiffuse || rs.isOccluded) return;
     rs.isHitProcessed = true;
     if (rs.matType == PERFECT_REFLECTION) {
-        rs.dir = normalize(rs.dir - rs.normal * (float)((double)dot(rs.dir, rs.normal) * 2.0));
+        rs.dir = normalize(rs.dir - rs.normal * dot(rs.dir, rs.normal) * 2.0f);
         rs.orig = rs.pos + rs.offset * rs.normal;
     } else if (rs.matType == FRESNEL_RR) {
         float etaI = 1.0f, etaT = 1.33f;
@@ -379,14 +379,14 @@ static void glossy(Ctx& c, RayState& rs, float rnd) {
         float cosT = sqrtf(max1f(0, (float)(1.0 - (double)sin2T)));
         F3 next;
         float off = rs.offset;
-        if ((double)sin2T >= 1.0) {
-            next = rs.dir - rs.normal * (float)((double)ndr * 2.0);
+        if (sin2T >= 1.0f) {
+            next = rs.dir - rs.normal * ndr * 2.0f;
         } else {
             float R1 = etaT * cosI, R2 = etaI * cosT, R3 = etaI * cosI, R4 = etaT * cosT;
             float Rparl = (R1 - R2) / (R1 + R2), Rperp = (R3 - R4) / (R3 + R4);
             float fres = (float)((double)(Rparl * Rparl + Rperp * Rperp) / 2.0);
-            if (rnd < fres) next = rs.dir - rs.normal * (float)((double)ndr * 2.0);
-            else { next = eta * rs.dir + (eta * cosI - cosT) * rs.normal; off = (float)((double)off * -1.0); }
+            if (rnd < fres) next = rs.dir - rs.normal * ndr * 2.0f;
+            else { next = eta * rs.dir + (eta * cosI - cosT) * rs.normal; off = -off; }
         }
         rs.dir = normalize(next);
         rs.orig = rs.pos + off * rs.normal;

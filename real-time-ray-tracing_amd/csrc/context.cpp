@@ -22,28 +22,6 @@ namespace {
 
 thread_local std::string g_createError;
 
-#define HIP_TRY(ctx, expr)                                                            \
-    do {                                                                              \
-        hipError_t e__ = (expr);                                                      \
-        if (e__ != hipSuccess) {                                                      \
-            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e__);          \
-            return RT_ERR_HIP;                                                        \
-        }                                                                             \
-    } while (0)
-
-template <typename T>
-int dalloc(rt_context* ctx, T** p, size_t bytes) {
-    void* q = nullptr;
-    hipError_t e = hipMalloc(&q, bytes < 16 ? 16 : bytes);
-    if (e != hipSuccess) {
-        ctx->err = std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e);
-        return RT_ERR_HIP;
-    }
-    ctx->allocations.push_back(q);
-    *p = (T*)q;
-    return RT_OK;
-}
-
 void default_params(rt_params& p) {
     // settingParams.h defaults
     p.sky.needRegenerate = 1;
@@ -121,6 +99,18 @@ bool load_triangle_bin(const std::string& path, rtscene::SceneMesh& m, std::stri
 }
 
 }  // namespace
+
+int rt_dalloc_bytes(rt_context* ctx, void** p, size_t bytes) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, bytes < 16 ? 16 : bytes);
+    if (e != hipSuccess) {
+        ctx->err = std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e);
+        return RT_ERR_HIP;
+    }
+    ctx->allocations.push_back(q);
+    *p = q;
+    return RT_OK;
+}
 
 std::string rt_data_dir() {
     Dl_info info;
@@ -236,6 +226,7 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
     ctx->device = rttoml::find_or_int(doc, "render", "device", -1);
     ctx->stripY0 = rttoml::find_or_int(doc, "render", "stripY0", 0);
     ctx->stripRows = rttoml::find_or_int(doc, "render", "stripRows", -1);
+    ctx->materialOverride = rttoml::find_or_int(doc, "render", "materialOverride", -1);
     if (ctx->screenW <= 0 || ctx->screenH <= 0 || ctx->screenW > 16384 || ctx->screenH > 16384 || ctx->spp < 1 ||
         ctx->spp > 64 || ctx->chunkDim < 1 || ctx->chunkDim > 8) {
         g_createError = "invalid resolution / spp / chunkDim";
@@ -347,6 +338,7 @@ int rt_init(rt_context* ctx) {
                                                ctx->dNormals, ctx->stream));
     }
 #undef ALLOC
+    if ((rc = rt_frame_init(ctx)) != RT_OK) return rc;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     ctx->inited = true;
     return RT_OK;
@@ -483,6 +475,7 @@ int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms) {
         int rc = RT_OK;
         if (stage == 0) rc = rt_build_bvh(ctx);
         else if (stage == 1) rc = rt_trace_primary(ctx, 1 + i, 0);
+        else if (stage == 2) rc = rt_path_trace(ctx, 1 + i, 0);
         else { ctx->err = "unknown stage"; return RT_ERR_ARG; }
         if (rc != RT_OK) return rc;
     }
@@ -515,6 +508,10 @@ size_t rt_array_bytes(const rt_context* ctx, int what) {
         case RT_ARR_HIT_NORMALS: return P * 16;
         case RT_ARR_HIT_FAKE_NORMALS: return P * 16;
         case RT_ARR_HIT_STATS: return P * 16;
+        case RT_ARR_RAYS: return P * 4;
+        case RT_ARR_SKY_PDF: case RT_ARR_SKY_CDF: return (size_t)kSkySize * 4;
+        case RT_ARR_SUN_PDF: case RT_ARR_SUN_CDF: return (size_t)kSunSize * 4;
+        case RT_ARR_SUN_DIR: return 16;
         default: return 0;
     }
 }
@@ -544,6 +541,18 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
         case RT_ARR_HIT_NORMALS: src = ctx->dHitNrm; break;
         case RT_ARR_HIT_FAKE_NORMALS: src = ctx->dHitFake; break;
         case RT_ARR_HIT_STATS: src = ctx->dHitStats; break;
+        case RT_ARR_RAYS: src = ctx->fr.rays; break;
+        case RT_ARR_SKY_PDF: src = ctx->fr.skyPdf; break;
+        case RT_ARR_SKY_CDF: src = ctx->fr.skyCdf; break;
+        case RT_ARR_SUN_PDF: src = ctx->fr.sunPdf; break;
+        case RT_ARR_SUN_CDF: src = ctx->fr.sunCdf; break;
+        case RT_ARR_SUN_DIR: {
+            if (bytes < 16) { ctx->err = "destination too small"; return RT_ERR_ARG; }
+            float* o = (float*)dst;
+            memcpy(o, ctx->fr.sunDir, 12);
+            o[3] = ctx->fr.cosThetaMax;
+            return RT_OK;
+        }
         default: ctx->err = "unknown array"; return RT_ERR_ARG;
     }
     const size_t need = rt_array_bytes(ctx, what);

@@ -18,6 +18,39 @@ struct HostCamera {  // Camera::update outputs (kernel.cuh:103-121)
     float adjustedLeft[3], adjustedUp[3], adjustedFront[3], apertureLeft[3], apertureUp[3];
 };
 
+// Device buffers of RayTracer::draw after the BVH (kernel.cu:259-398)
+struct FrameResources {
+    bool ready = false;
+    // sky / sun (kernel.cu:280-307)
+    float* solar = nullptr;
+    float* limb = nullptr;
+    float* cie = nullptr;
+    float4* sky = nullptr;
+    float* skyPdf = nullptr;
+    float* skyCdf = nullptr;
+    float4* sun = nullptr;
+    float* sunPdf = nullptr;
+    float* sunCdf = nullptr;
+    float* scanSums = nullptr;
+    bool skyValid = false;
+    rt_sky_params lastSky{};
+    float sunDir[3] = {0, 1, 0};
+    float cosThetaMax = 1.0f, sunArea = 0.0f;
+    // soil textures (init.cu:524-577)
+    uint2* texAlbedo = nullptr;
+    uint2* texNormal = nullptr;
+    // path-trace G-buffer (pathtrace.cuh:11-128)
+    uint2* color = nullptr;
+    uint2* normal = nullptr;
+    uint2* albedo = nullptr;
+    uint16_t* depth = nullptr;
+    uint32_t* motion = nullptr;
+    uint32_t* rays = nullptr;
+    unsigned long long* rayCounter = nullptr;
+    HistCamera hist{};
+    bool histValid = false;
+};
+
 struct rt_context {
     // ---- settings (GlobalSettings, globalSettings.h:5-22) + extensions
     int screenW = 1920, screenH = 1080;
@@ -33,6 +66,7 @@ struct rt_context {
     int spp = 1;
     int stripY0 = 0, stripRows = -1;  // [render] stripY0/stripRows: screen-strip split
     int device = -1;
+    int materialOverride = -1;  // [render] materialOverride: one material for every triangle (tests)
 
     std::string err;
     bool inited = false;
@@ -78,6 +112,24 @@ struct rt_context {
 };
 
 // helpers shared by the C-ABI translation units
+#define HIP_TRY(ctx, expr)                                                            \
+    do {                                                                              \
+        hipError_t e__ = (expr);                                                      \
+        if (e__ != hipSuccess) {                                                      \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e__);          \
+            return RT_ERR_HIP;                                                        \
+        }                                                                             \
+    } while (0)
+
+int rt_dalloc_bytes(rt_context* ctx, void** p, size_t bytes);  // hipMalloc, freed by rt_destroy
+template <typename T>
+int dalloc(rt_context* ctx, T** p, size_t bytes) {
+    void* q = nullptr;
+    const int rc = rt_dalloc_bytes(ctx, &q, bytes);
+    *p = (T*)q;
+    return rc;
+}
+int rt_frame_init(rt_context* ctx);  // frame.cpp: sky tables, textures, G-buffers
 std::string rt_data_dir();
 void rt_camera_update(const rt_camera& in, int renderW, int renderH, HostCamera& c);
 TraceCamera rt_trace_camera(const HostCamera& c);

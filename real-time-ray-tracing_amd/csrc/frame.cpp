@@ -1,18 +1,327 @@
-// frame.cpp — RayTracer::draw (kernel.cu:259-398) and GetBuffer2D behind the C-ABI.
-#include "context.h"
+// frame.cpp — the per-frame part of RayTracer::draw (kernel.cu:259-398) behind the C-ABI:
+// sky/sun regeneration, the path tracer, G-buffer access.  Denoise and post-processing
+// stages are dispatched from here as they land.
+//
+//   sun direction       UpdateFrame (kernel.cu:119-123), rotate3f (linearMath.h:650-716)
+//   UpdateSkyState      sky.cuh:124-146 (host, float + rtmath, like the reference's host code)
+//   sky regeneration    kernel.cu:286-307
+//   PathTrace launch    kernel.cu:330-350; HistoryCamera::Setup kernel.cu:133-136, 357
+#include <math.h>
+#include <string.h>
 
-extern "C" int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
+#include <fstream>
+#include <vector>
+
+#include "context.h"
+#include "rtmath.h"
+
+namespace {
+
+constexpr float kPi = 3.1415926535897932384626422832795028841971f;
+constexpr float kTwoPi = 6.2831853071795864769252867665590057683943f;
+constexpr float kPiOver180 = 0.01745329251f;
+
+// ---- host vector helpers with the device rounding policy (one rounding per op, fma only
+// where the reference's TwoProd/InnerProduct use it)
+struct V3 { float x, y, z; };
+V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+V3 operator*(float s, V3 a) { return v3(a.x * s, a.y * s, a.z * s); }
+V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+float dop(float a, float b, float c, float d) {
+    const float cd = c * d;
+    const float err = fmaf(-c, d, cd);
+    const float dp = fmaf(a, b, -cd);
+    return dp + err;
+}
+float inner3(float a, float b, float c, float d, float e, float f) {
+    const float ef = e * f, efe = fmaf(e, f, -ef);
+    const float cd = c * d, cde = fmaf(c, d, -cd);
+    const float s2 = cd + ef, dl2 = s2 - cd, s2e = (cd - (s2 - dl2)) + (ef - dl2);
+    const float tpv = s2, tpe = cde + (efe + s2e);
+    const float ab = a * b, abe = fmaf(a, b, -ab);
+    const float s1 = ab + tpv, dl1 = s1 - ab, s1e = (ab - (s1 - dl1)) + (tpv - dl1);
+    return s1 + (abe + (tpe + s1e));
+}
+float dot(V3 a, V3 b) { return inner3(a.x, b.x, a.y, b.y, a.z, b.z); }
+V3 cross(V3 a, V3 b) { return v3(dop(a.y, b.z, a.z, b.y), dop(a.z, b.x, a.x, b.z), dop(a.x, b.y, a.y, b.x)); }
+V3 normalize(V3 v) {
+    const float n = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
+    return v3(v.x / n, v.y / n, v.z / n);
+}
+
+struct Quat { V3 v; float w; };
+Quat qmul(const Quat& p, const Quat& q) { return Quat{p.w * q.v + q.w * p.v + cross(p.v, q.v), p.w * q.w - dot(p.v, q.v)}; }
+
+// sunDir = rotate3f(axis, angle, cross(up, axis)).normalized()
+V3 sun_direction(float timeOfDay, float sunAxisAngle) {
+    const V3 axis = normalize(v3(0.0f, rt_cosf(sunAxisAngle * kPiOver180), rt_sinf(sunAxisAngle * kPiOver180)));
+    const float angle = fmodf(timeOfDay * kPi, kTwoPi);
+    const V3 v = cross(v3(0.0f, 1.0f, 0.0f), axis);
+    const Quat q{normalize(axis) * rt_sinf(angle / 2), rt_cosf(angle / 2)};
+    const Quat r = qmul(qmul(q, Quat{v, 0.0f}), Quat{-q.v, q.w});
+    return normalize(r.v);
+}
+
+float fitting(const float* m, float s, int i) {  // GetFittingData (sky.cuh:90-99)
+    return (rt_powf(1.0f - s, 5.0f) * m[i] + 5.0f * rt_powf(1.0f - s, 4.0f) * s * m[i + 9] +
+            10.0f * rt_powf(1.0f - s, 3.0f) * rt_powf(s, 2.0f) * m[i + 18] +
+            10.0f * rt_powf(1.0f - s, 2.0f) * rt_powf(s, 3.0f) * m[i + 27] +
+            5.0f * (1.0f - s) * rt_powf(s, 4.0f) * m[i + 36] + rt_powf(s, 5.0f) * m[i + 45]);
+}
+float fitting2(const float* m, float s) {  // GetFittingData2 (sky.cuh:102-111)
+    return (rt_powf(1.0f - s, 5.0f) * m[0] + 5.0f * rt_powf(1.0f - s, 4.0f) * s * m[1] +
+            10.0f * rt_powf(1.0f - s, 3.0f) * rt_powf(s, 2.0f) * m[2] +
+            10.0f * rt_powf(1.0f - s, 2.0f) * rt_powf(s, 3.0f) * m[3] + 5.0f * (1.0f - s) * rt_powf(s, 4.0f) * m[4] +
+            rt_powf(s, 5.0f) * m[5]);
+}
+
+struct SkyTablesHost {
+    std::vector<float> skyDataSets, skyDataSetsRad, solar, limb, cieX, cieY, cieZ;
+};
+SkyTablesHost g_tables;  // immutable after the first successful load
+
+bool load_sky_tables(const std::string& path, SkyTablesHost& t, std::string& err) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) { err = "cannot read " + path; return false; }
+    uint32_t count = 0;
+    f.read((char*)&count, 4);
+    if (count != 7) { err = "bad sky table file " + path; return false; }
+    uint32_t len[7];
+    f.read((char*)len, sizeof(len));
+    const uint32_t expect[7] = {540, 60, 1800, 60, 10, 10, 10};
+    std::vector<float>* dst[7] = {&t.skyDataSets, &t.skyDataSetsRad, &t.solar, &t.limb, &t.cieX, &t.cieY, &t.cieZ};
+    for (int i = 0; i < 7; ++i) {
+        if (len[i] != expect[i]) { err = "bad sky table sizes in " + path; return false; }
+        dst[i]->resize(len[i]);
+        f.read((char*)dst[i]->data(), len[i] * 4);
+    }
+    if (!f) { err = "truncated " + path; return false; }
+    return true;
+}
+
+bool sky_params_equal(const rt_sky_params& a, const rt_sky_params& b) {
+    return a.timeOfDay == b.timeOfDay && a.sunAxisAngle == b.sunAxisAngle && a.skyScalar == b.skyScalar &&
+           a.sunScalar == b.sunScalar && a.sunAngle == b.sunAngle;
+}
+
+// kernel.cu:286-307 — regenerate when asked to, or when the sky parameters changed
+int update_sky(rt_context* ctx) {
+    FrameResources& fr = ctx->fr;
+    rt_sky_params& sp = ctx->params.sky;
+    const V3 sunDir = sun_direction(sp.timeOfDay, sp.sunAxisAngle);
+    fr.sunDir[0] = sunDir.x; fr.sunDir[1] = sunDir.y; fr.sunDir[2] = sunDir.z;
+    if (fr.skyValid && !sp.needRegenerate && sky_params_equal(sp, fr.lastSky)) return RT_OK;
+    sp.sunScalar = sp.sunScalar > 0.00001f ? sp.sunScalar : 0.00001f;
+    sp.skyScalar = sp.skyScalar > 0.00001f ? sp.skyScalar : 0.00001f;
+    sp.sunAngle = sp.sunAngle > 0.51f ? sp.sunAngle : 0.51f;
+    SkyGenParams p;
+    memcpy(p.sunDir, fr.sunDir, 12);
+    p.skyScalar = sp.skyScalar;
+    p.sunScalar = sp.sunScalar;
+    p.sunAngle = sp.sunAngle;
+    const float elevation = rt_acosf(sunDir.y);
+    const float se = rt_powf(elevation / (kPi / 2.0f), (1.0f / 3.0f));
+    for (int ch = 0; ch < 10; ++ch) {
+        for (int i = 0; i < 9; ++i) p.st.configs[ch * 9 + i] = fitting(g_tables.skyDataSets.data() + ch * 54, se, i);
+        p.st.radiances[ch] = fitting2(g_tables.skyDataSetsRad.data() + ch * 6, se);
+    }
+    const float sunRadius = sp.sunAngle * kPi / 180.0f / 2.0f;
+    p.cosThetaMax = rt_cosf(sunRadius);
+    p.solar = fr.solar;
+    p.limb = fr.limb;
+    p.cie = fr.cie;
+    p.skyBuffer = fr.sky;
+    p.skyPdf = fr.skyPdf;
+    p.skyCdf = fr.skyCdf;
+    p.sunBuffer = fr.sun;
+    p.sunPdf = fr.sunPdf;
+    p.sunCdf = fr.sunCdf;
+    p.scanSums = fr.scanSums;
+    HIP_TRY(ctx, rtk_launch_sky(&p, ctx->stream));
+    fr.sunArea = rt_powf(rt_tanf(sunRadius), 2.0f) * kPi;
+    fr.cosThetaMax = p.cosThetaMax;
+    fr.skyValid = true;
+    sp.needRegenerate = 0;
+    fr.lastSky = sp;
+    return RT_OK;
+}
+
+HistCamera hist_of(const HostCamera& c) {
+    HistCamera h;
+    memcpy(h.pos, c.pos, 12);
+    memcpy(h.left, c.left, 12);
+    memcpy(h.up, c.up, 12);
+    memcpy(h.dir, c.dir, 12);
+    return h;
+}
+
+}  // namespace
+
+int rt_frame_init(rt_context* ctx) {
+    FrameResources& fr = ctx->fr;
+    std::string err;
+    if (g_tables.solar.empty()) {
+        SkyTablesHost t;
+        if (!load_sky_tables(rt_data_dir() + "/sky_tables.bin", t, err)) { ctx->err = err; return RT_ERR_IO; }
+        g_tables = std::move(t);
+    }
+    int rc;
+#define ALLOC(p, bytes) if ((rc = dalloc(ctx, &(p), (bytes))) != RT_OK) return rc
+    ALLOC(fr.solar, 1800 * 4);
+    ALLOC(fr.limb, 60 * 4);
+    ALLOC(fr.cie, 30 * 4);
+    ALLOC(fr.sky, (size_t)kSkySize * 16);
+    ALLOC(fr.skyPdf, (size_t)kSkySize * 4);
+    ALLOC(fr.skyCdf, (size_t)kSkySize * 4);
+    ALLOC(fr.sun, (size_t)kSunSize * 16);
+    ALLOC(fr.sunPdf, (size_t)kSunSize * 4);
+    ALLOC(fr.sunCdf, (size_t)kSunSize * 4);
+    ALLOC(fr.scanSums, 512 * 4);
+    ALLOC(fr.texAlbedo, (size_t)kTexTexels * 8);
+    ALLOC(fr.texNormal, (size_t)kTexTexels * 8);
+    const size_t P = (size_t)ctx->renderW * ctx->renderH;
+    ALLOC(fr.color, P * 8);
+    ALLOC(fr.normal, P * 8);
+    ALLOC(fr.albedo, P * 8);
+    ALLOC(fr.depth, P * 2);
+    ALLOC(fr.motion, P * 4);
+    ALLOC(fr.rays, P * 4);
+    ALLOC(fr.rayCounter, 64);
+#undef ALLOC
+    HIP_TRY(ctx, hipMemcpy(fr.solar, g_tables.solar.data(), 1800 * 4, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, hipMemcpy(fr.limb, g_tables.limb.data(), 60 * 4, hipMemcpyHostToDevice));
+    std::vector<float> cie(30);
+    memcpy(cie.data(), g_tables.cieX.data(), 40);
+    memcpy(cie.data() + 10, g_tables.cieY.data(), 40);
+    memcpy(cie.data() + 20, g_tables.cieZ.data(), 40);
+    HIP_TRY(ctx, hipMemcpy(fr.cie, cie.data(), 30 * 4, hipMemcpyHostToDevice));
+    // soil texture pair (synthetic stand-in for the missing blobs, scene_gen.h)
+    {
+        rtscene::TexturePair t;
+        rtscene::make_textures(t);
+        if (t.albedoAo.size() != (size_t)kTexTexels * 4) { ctx->err = "texture chain size mismatch"; return RT_ERR_STATE; }
+        HIP_TRY(ctx, hipMemcpy(fr.texAlbedo, t.albedoAo.data(), (size_t)kTexTexels * 8, hipMemcpyHostToDevice));
+        HIP_TRY(ctx, hipMemcpy(fr.texNormal, t.normalRough.data(), (size_t)kTexTexels * 8, hipMemcpyHostToDevice));
+    }
+    HIP_TRY(ctx, hipMemset(fr.color, 0, P * 8));
+    HIP_TRY(ctx, hipMemset(fr.normal, 0, P * 8));
+    HIP_TRY(ctx, hipMemset(fr.albedo, 0, P * 8));
+    HIP_TRY(ctx, hipMemset(fr.depth, 0, P * 2));
+    HIP_TRY(ctx, hipMemset(fr.motion, 0, P * 4));
+    HIP_TRY(ctx, hipMemset(fr.rays, 0, P * 4));
+    HIP_TRY(ctx, hipMemset(fr.rayCounter, 0, 64));
+    fr.ready = true;
+    return RT_OK;
+}
+
+extern "C" {
+
+int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
+    if (!ctx || frame_num < 1) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_path_trace before rt_init"; return RT_ERR_STATE; }
+    FrameResources& fr = ctx->fr;
+    int rc = update_sky(ctx);
+    if (rc != RT_OK) return rc;
+    HostCamera hc;
+    rt_camera_update(ctx->camera, ctx->renderW, ctx->renderH, hc);
+    if (frame_num == 1 || !fr.histValid) fr.hist = hist_of(hc);  // kernel.cu:133-136
+    PathTraceParams p;
+    p.cam = rt_trace_camera(hc);
+    p.tanHalfFov[0] = hc.tanHalfFov[0];
+    p.tanHalfFov[1] = hc.tanHalfFov[1];
+    p.res[0] = hc.res[0];
+    p.res[1] = hc.res[1];
+    p.hist = fr.hist;
+    p.width = (uint32_t)ctx->renderW;
+    p.height = (uint32_t)ctx->renderH;
+    p.y0 = (uint32_t)ctx->stripY0;
+    p.rows = (uint32_t)ctx->stripRows;
+    p.frameNum = frame_num;
+    p.spp = (uint32_t)ctx->spp;
+    p.materialOverride = ctx->materialOverride;
+    p.triCount = ctx->mesh.triCount;
+    p.bluenoise = ctx->dBlueNoise;
+    p.triPos = ctx->dTriPos;
+    p.triNrm = ctx->dTriNrm;
+    p.nodes = ctx->dNodes;
+    p.tlasNodes = ctx->dTlasNodes;
+    p.texAlbedo = fr.texAlbedo;
+    p.texNormal = fr.texNormal;
+    p.skyBuffer = fr.sky;
+    p.sunBuffer = fr.sun;
+    p.skyCdf = fr.skyCdf;
+    p.sunCdf = fr.sunCdf;
+    memcpy(p.sunDir, fr.sunDir, 12);
+    p.cosThetaMax = fr.cosThetaMax;
+    p.colorOut = fr.color;
+    p.normalOut = fr.normal;
+    p.albedoOut = fr.albedo;
+    p.depthOut = fr.depth;
+    p.motionOut = fr.motion;
+    p.raysOut = with_detail ? fr.rays : nullptr;
+    p.rayCounter = fr.rayCounter;
+    HIP_TRY(ctx, rtk_launch_pathtrace(&p, ctx->stream));
+    fr.hist = hist_of(hc);  // HistoryCamera::Setup after PathTrace (kernel.cu:357)
+    fr.histValid = true;
+    ctx->lastFrame = frame_num;
+    return RT_OK;
+}
+
+int rt_get_ray_count(rt_context* ctx, uint64_t* rays, int reset) {
+    if (!ctx || !rays) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_get_ray_count before rt_init"; return RT_ERR_STATE; }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    unsigned long long v = 0;
+    HIP_TRY(ctx, hipMemcpy(&v, ctx->fr.rayCounter, 8, hipMemcpyDeviceToHost));
+    *rays = v;
+    if (reset) HIP_TRY(ctx, hipMemset(ctx->fr.rayCounter, 0, 8));
+    return RT_OK;
+}
+
+int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
     (void)rgba8_out;
     (void)hdr_out;
     if (!ctx) return RT_ERR_ARG;
-    ctx->err = "rt_draw: path tracer not built in this revision";
+    ctx->err = "rt_draw: denoise/post stages not built in this revision";
     return RT_ERR_STATE;
 }
 
-extern "C" int rt_get_buffer(const rt_context* ctx, int name, void* dst, size_t bytes) {
-    (void)name;
-    (void)dst;
-    (void)bytes;
-    if (!ctx) return RT_ERR_ARG;
-    return RT_ERR_STATE;
+size_t rt_buffer_bytes(const rt_context* ctx, int name) {
+    if (!ctx) return 0;
+    const size_t P = (size_t)ctx->renderW * ctx->renderH;
+    switch (name) {
+        case RT_BUF_RENDER_COLOR: case RT_BUF_NORMAL: case RT_BUF_ALBEDO: return P * 8;
+        case RT_BUF_DEPTH: return P * 2;
+        case RT_BUF_MOTION: return P * 4;
+        case RT_BUF_SKY: return (size_t)kSkySize * 16;
+        case RT_BUF_SUN: return (size_t)kSunSize * 16;
+        default: return 0;
+    }
 }
+
+int rt_get_buffer(const rt_context* cctx, int name, void* dst, size_t bytes) {
+    rt_context* ctx = const_cast<rt_context*>(cctx);
+    if (!ctx || !dst) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_get_buffer before rt_init"; return RT_ERR_STATE; }
+    const FrameResources& fr = ctx->fr;
+    const void* src = nullptr;
+    switch (name) {
+        case RT_BUF_RENDER_COLOR: src = fr.color; break;
+        case RT_BUF_NORMAL: src = fr.normal; break;
+        case RT_BUF_ALBEDO: src = fr.albedo; break;
+        case RT_BUF_DEPTH: src = fr.depth; break;
+        case RT_BUF_MOTION: src = fr.motion; break;
+        case RT_BUF_SKY: src = fr.sky; break;
+        case RT_BUF_SUN: src = fr.sun; break;
+        default: ctx->err = "buffer not available in this revision"; return RT_ERR_ARG;
+    }
+    const size_t need = rt_buffer_bytes(ctx, name);
+    if (bytes < need) { ctx->err = "destination too small"; return RT_ERR_ARG; }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipMemcpy(dst, src, need, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+}  // extern "C"

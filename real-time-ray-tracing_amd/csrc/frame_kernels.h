@@ -1,8 +1,84 @@
-// frame_kernels.h — launch interface of the per-frame path-trace, denoise and post kernels.
+// frame_kernels.h — launch parameters of the per-frame kernels after the BVH build:
+// sky/sun generation + CDF scan, the path tracer, the SVGF denoiser and post-processing.
+// Plain-old-data structs passed by value as kernel arguments; device pointers only.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-struct FrameResources {
-    int dummy;
+#include "bvh_kernels.h"
+
+constexpr int kSkyW = 512, kSkyH = 256, kSkySize = kSkyW * kSkyH;  // kernel.cuh SKY_WIDTH/HEIGHT
+constexpr int kSunW = 32, kSunH = 32, kSunSize = kSunW * kSunH;    // SUN_WIDTH/HEIGHT
+constexpr int kSkyScanBlock = 256, kSunScanBlock = 32;               // SKY/SUN_SCAN_BLOCK_SIZE
+constexpr int kTexLevels = 11, kTexSize = 1024;                      // soil textures, 11 mips
+
+// ushort4-texel offset of mip level l in the concatenated chain
+__host__ __device__ constexpr uint32_t tex_level_offset(int l) {
+    uint32_t off = 0;
+    for (int k = 0; k < l; ++k) off += (uint32_t)(kTexSize >> k) * (uint32_t)(kTexSize >> k);
+    return off;
+}
+constexpr uint32_t kTexTexels = tex_level_offset(kTexLevels);
+
+// Hosek-Wilkie sky state (UpdateSkyState, sky.cuh:90-146), evaluated on the host
+struct SkyState {
+    float configs[90];   // 10 spectral channels x 9 coefficients
+    float radiances[10];
 };
+
+struct SkyGenParams {
+    float sunDir[3];
+    float skyScalar, sunScalar, sunAngle;  // already clamped (kernel.cu:291-293)
+    float cosThetaMax;                     // cos(sunAngle * pi / 360) in float
+    SkyState st;
+    const float* solar;   // [10][180] h_solarDatasets
+    const float* limb;    // [10][6]  h_limbDarkeningDatasets
+    const float* cie;     // [3][10]  spectrumCieX | Y | Z
+    float4* skyBuffer;    // [256][512]
+    float* skyPdf;        // [131072]
+    float* skyCdf;        // [131072]
+    float4* sunBuffer;    // [32][32]
+    float* sunPdf;        // [1024]
+    float* sunCdf;        // [1024]
+    float* scanSums;      // [>= 512] block totals
+};
+
+struct HistCamera { float pos[3], left[3], up[3], dir[3]; };  // HistoryCamera (kernel.cuh:135-155)
+
+struct PathTraceParams {
+    TraceCamera cam;
+    float tanHalfFov[2];
+    float res[2];
+    HistCamera hist;
+    uint32_t width, height;     // full render size (strides)
+    uint32_t y0, rows;          // rows [y0, y0 + rows) are traced
+    int frameNum;
+    uint32_t spp;               // samples per pixel (>= 1), frame index spp*(frameNum-1)+1+s
+    int materialOverride;       // < 0: reference material table (material 3 everywhere)
+    uint32_t triCount;
+    const uint8_t* bluenoise;
+    const float4* triPos;
+    const float4* triNrm;
+    const void* nodes;
+    const void* tlasNodes;
+    const uint2* texAlbedo;     // ushort4 texels, kTexLevels levels concatenated
+    const uint2* texNormal;
+    const float4* skyBuffer;
+    const float4* sunBuffer;
+    const float* skyCdf;
+    const float* sunCdf;
+    float sunDir[3];
+    float cosThetaMax;
+    uint2* colorOut;            // [W*H] half3 demodulated colour + ushort material mask
+    uint2* normalOut;           // [W*H] half4
+    uint2* albedoOut;           // [W*H] half4
+    uint16_t* depthOut;         // [W*H] half
+    uint32_t* motionOut;        // [W*H] half2
+    uint32_t* raysOut;          // optional [W*H] RaySceneIntersect calls that traced
+    unsigned long long* rayCounter;  // optional: total traced rays (one atomic per workgroup)
+};
+
+extern "C" hipError_t rtk_launch_sky(const SkyGenParams* p, hipStream_t stream);
+extern "C" hipError_t rtk_launch_scan(const float* in, float* out, float* sums, int size, int blockSize,
+                                      hipStream_t stream);
+extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream);

@@ -159,6 +159,8 @@ struct HitInfo {
     float u, v;
     F3 normal, fakeNormal, pos;
     float offset;
+    float ndr;   // normalDotRayDir after the flip (<= 0)
+    bool into;   // isRayIntoSurface
     bool hit;
     uint32_t visits, tests, dropped, iters;
 };
@@ -276,8 +278,9 @@ RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint32_t* stkA, float
         const F3 n3 = normalize(f3_of(sc.triNrm[3 * hitIdx + 2]));
         fake = normalize(n3 * (1.0f - hitU - hitV) + n1 * hitU + n2 * hitV);
     }
-    const float ndr = dot(nrm, dir);
-    if (!(ndr < 0.0f)) nrm = -nrm;
+    float ndr = dot(nrm, dir);
+    const bool into = ndr < 0.0f;
+    if (!into) { nrm = -nrm; ndr = -ndr; }
     if (dot(fake, nrm) < 0.0f) fake = -fake;
     const bool hit = t < kRayMax;
     if (!hit) { nrm = f3(0.0f, -1.0f, 0.0f); fake = f3(0.0f, -1.0f, 0.0f); }
@@ -289,6 +292,8 @@ RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint32_t* stkA, float
     out.fakeNormal = fake;
     out.pos = pos;
     out.offset = offset;
+    out.ndr = ndr;
+    out.into = into;
     out.hit = hit;
     out.visits = visits; out.tests = tests; out.dropped = dropped; out.iters = iters;
 }

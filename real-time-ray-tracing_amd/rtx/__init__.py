@@ -23,7 +23,8 @@ ERRORS = {-1: "RT_ERR_ARG", -2: "RT_ERR_HIP", -3: "RT_ERR_IO", -4: "RT_ERR_STATE
 # rt_array_name (include/rtx_amd.h)
 ARR = dict(VERTICES=0, INDICES=1, NORMALS=2, TRI_POS=3, AABBS=4, MORTON=5, REORDER=6, NODES=7, TLAS_AABBS=8,
            TLAS_MORTON=9, TLAS_REORDER=10, TLAS_NODES=11, TLAS_SCENE_AABB=12, BATCH_SCENE_AABBS=13, HITS=14,
-           HIT_NORMALS=15, HIT_FAKE_NORMALS=16, HIT_STATS=17, TRI_NRM=18)
+           HIT_NORMALS=15, HIT_FAKE_NORMALS=16, HIT_STATS=17, TRI_NRM=18, RAYS=19, SKY_PDF=20, SKY_CDF=21,
+           SUN_PDF=22, SUN_CDF=23, SUN_DIR=24)
 # rt_buffer_name (Buffer2DName, kernel.cuh:286-315)
 BUF = dict(RENDER_COLOR=0, ACCUMULATION=1, HISTORY_COLOR=2, SCALED_COLOR=3, NORMAL=10, DEPTH=11, HISTORY_DEPTH=12,
            MOTION=13, NOISE_LEVEL=14, NOISE_LEVEL16=15, SKY=16, SUN=17, ALBEDO=18)
@@ -96,6 +97,9 @@ SIGNATURES = {
     "rt_set_delta_time": (C.c_int, [C.c_void_p, C.c_float]),
     "rt_get_info": (C.c_int, [C.c_void_p, C.POINTER(Info)]),
     "rt_get_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
+    "rt_buffer_bytes": (C.c_size_t, [C.c_void_p, C.c_int]),
+    "rt_path_trace": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "rt_get_ray_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "rt_build_bvh": (C.c_int, [C.c_void_p]),
     "rt_trace_primary": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "rt_sync": (C.c_int, [C.c_void_p]),
@@ -213,6 +217,14 @@ class RayTracer:
     def trace_primary(self, frame_num: int = 1, detail: bool = False):
         self._check(self.lib.rt_trace_primary(self.h, frame_num, 1 if detail else 0), "rt_trace_primary")
 
+    def path_trace(self, frame_num: int = 1, detail: bool = False):
+        self._check(self.lib.rt_path_trace(self.h, frame_num, 1 if detail else 0), "rt_path_trace")
+
+    def ray_count(self, reset: bool = False) -> int:
+        v = C.c_uint64()
+        self._check(self.lib.rt_get_ray_count(self.h, C.byref(v), 1 if reset else 0), "rt_get_ray_count")
+        return v.value
+
     def sync(self):
         self._check(self.lib.rt_sync(self.h), "rt_sync")
 
@@ -229,7 +241,10 @@ class RayTracer:
         self._check(self.lib.rt_download(self.h, what, buf.ctypes.data, n), "rt_download(%s)" % name)
         return buf.view(dtype)
 
-    def get_buffer(self, name: str, shape, dtype) -> np.ndarray:
+    def get_buffer(self, name: str, shape=None, dtype=np.uint8) -> np.ndarray:
+        if shape is None:
+            n = self.lib.rt_buffer_bytes(self.h, BUF[name])
+            shape = (n // np.dtype(dtype).itemsize,)
         out = np.empty(shape, dtype=dtype)
         self._check(self.lib.rt_get_buffer(self.h, BUF[name], out.ctypes.data, out.nbytes), "rt_get_buffer")
         return out

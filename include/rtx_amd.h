@@ -167,6 +167,13 @@ int rt_trace_primary(rt_context* ctx, int frame_num, int with_detail);
  * traced-ray count (RT_ARR_RAYS).  Asynchronous; the history camera advances (kernel.cu:357). */
 int rt_path_trace(rt_context* ctx, int frame_num, int with_detail);
 
+/* TemporalSpatialDenoising + PostProcessing + CopyToOutput (denoising.cu:5-189,
+ * postprocessing.cu:5-161, kernel.cu:376-381) on the G-buffers of the last rt_path_trace, for
+ * frame_num (frame 1 skips the temporal passes).  Afterwards RT_BUF_RENDER_COLOR holds the
+ * denoised HDR colour and RT_BUF_SCALED_COLOR the tone-mapped screen image; the RGBA8 image and
+ * (with_hdr) a float4 HDR copy are kept on the device for rt_draw.  Asynchronous. */
+int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr);
+
 /* Traced rays (RaySceneIntersect calls that ran a traversal) accumulated since the last reset. */
 int rt_get_ray_count(rt_context* ctx, uint64_t* rays, int reset);
 
@@ -174,7 +181,8 @@ int rt_get_ray_count(rt_context* ctx, uint64_t* rays, int reset);
 int rt_sync(rt_context* ctx);
 
 /* HIP-event timing on the context stream: runs `iters` back-to-back launches of a stage
- * (0 = BVH build, 1 = primary rays, 2 = path trace, 3 = full frame) and returns the total
+ * (0 = BVH build, 1 = primary rays, 2 = path trace, 3 = full frame: BVH + path trace + denoise
+ * + post, 4 = denoise + post) and returns the total
  * milliseconds between the first launch and the end of the last. */
 int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms);
 
@@ -204,7 +212,13 @@ enum rt_array_name {
     RT_ARR_SKY_CDF = 21,         /* float[131072] inclusive scan of the sky pdf */
     RT_ARR_SUN_PDF = 22,         /* float[1024] */
     RT_ARR_SUN_CDF = 23,         /* float[1024] */
-    RT_ARR_SUN_DIR = 24          /* float[4]: sunDir xyz, cos(sun half-angle) (host values) */
+    RT_ARR_SUN_DIR = 24,         /* float[4]: sunDir xyz, cos(sun half-angle) (host values) */
+    RT_ARR_HISTOGRAM = 25,       /* uint32[64] luminance histogram (Histogram2) */
+    RT_ARR_EXPOSURE = 26,        /* float[4] exposure, adapted lum, bright lum, bright bin lum */
+    RT_ARR_COLOR4 = 27,          /* half4 [ceil(W/4) * ceil(H/4)] DownScale4 chain */
+    RT_ARR_COLOR16 = 28,         /* half4 [ceil(W/16) * ceil(H/16)] */
+    RT_ARR_COLOR64 = 29,         /* half4 [ceil(W/64) * ceil(H/64)] */
+    RT_ARR_RGBA8 = 30            /* uint8[Ws*Hs][4] final output of the last rt_draw / rt_denoise_post */
 };
 int rt_download(const rt_context* ctx, int what, void* dst, size_t bytes);
 size_t rt_array_bytes(const rt_context* ctx, int what);

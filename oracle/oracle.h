@@ -146,6 +146,37 @@ void orc_pathtrace(const OrcFrame* f, uint32_t W, uint32_t H, uint32_t y0, uint3
                    int threads);
 void orc_textures(uint16_t* albedoAo, uint16_t* normalRough);  // 1398101 ushort4 texels each
 
+// ---------------------------------------------------------------- denoise + post (denoise.cpp)
+struct rt_params;  // include/rtx_amd.h
+
+typedef struct OrcPostState {  // persists across frames
+    uint16_t* accum;       // [P][4] AccumulationColorBuffer
+    uint16_t* histColor;   // [P][4] HistoryColorBuffer
+    uint16_t* histDepth;   // [P]    HistoryDepthBuffer
+    float exposure[4];     // d_exposure (init.cu:331-333: 1,1,1,1)
+} OrcPostState;
+
+typedef struct OrcDrawIO {
+    uint32_t W, H;          // render size
+    uint32_t Ws, Hs;        // screen (output) size
+    int frameNum;
+    float deltaTime;        // ms, AutoExposure's adaptation step
+    const struct rt_params* params;
+    const uint8_t* bluenoise;
+    uint16_t* color;        // in: PathTrace colour (half3 + mask); out: RenderColorBuffer after denoise
+    const uint16_t* normal; const uint16_t* albedo; const uint16_t* depth; const uint16_t* motion;
+    uint16_t* noise8;       // out [ceil(W/8) * ceil(H/8)] half (last computed)
+    uint16_t* noise16;      // out [ceil(W/16) * ceil(H/16)] half
+    uint16_t* c4; uint16_t* c16; uint16_t* c64;   // out DownScale4 chain, half4
+    uint32_t* histogram;    // out [64]
+    uint16_t* scaled;       // out [Ws*Hs][4] half (ScaledColorBuffer, tone mapped)
+    uint8_t* rgba;          // out [Ws*Hs][4] (may be NULL)
+    OrcPostState* state;
+} OrcDrawIO;
+
+// TemporalSpatialDenoising + PostProcessing + CopyToOutput; returns < 0 for unsupported settings
+int orc_denoise_post(const OrcDrawIO* io);
+
 #ifdef __cplusplus
 }
 #endif

@@ -213,6 +213,8 @@ def _bind_frame_api(L):
     L.orc_pathtrace.argtypes = [C.POINTER(Frame), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                 C.POINTER(GBuffer), C.c_int]
     L.orc_pathtrace.restype = None
+    L.orc_denoise_post.argtypes = [C.c_void_p]
+    L.orc_denoise_post.restype = C.c_int
 
 
 def sky_tables() -> list:
@@ -282,3 +284,97 @@ def pathtrace(bvh: dict, width: int, height: int, frame_num: int = 1, spp: int =
     gb = GBuffer(*[g[k].ctypes.data for k in ("color", "normal", "albedo", "depth", "motion", "rays")])
     lib().orc_pathtrace(C.byref(f), width, height, y0, rows, C.byref(gb), threads)
     return g
+
+
+# ---------------------------------------------------------------- denoise + post (oracle/denoise.cpp)
+class RtParams(C.Structure):
+    """Layout of rt_params (include/rtx_amd.h) with the reference defaults (settingParams.h)."""
+    _fields_ = [("sky_needRegenerate", C.c_int32)] + [(n, C.c_float) for n in (
+        "timeOfDay", "sunAxisAngle", "skyScalar", "sunScalar", "sunAngle")] + [
+        ("sampleSurfaceVsLightUseMisWeight", C.c_int32), ("sampleSkyVsSunUseFluxWeight", C.c_int32),
+        ("sampleSurfaceVsLight", C.c_float), ("sampleSkyVsSun", C.c_float)] + [(n, C.c_int32) for n in (
+        "enableTemporalDenoising", "enableLocalSpatialFilter", "enableNoiseLevelVisualize",
+        "enableWideSpatialFilter", "enableTemporalDenoising2", "enablePostProcess", "enableDownScalePasses",
+        "enableHistogram", "enableAutoExposure", "enableBloomEffect", "enableLensFlare", "enableToneMapping",
+        "enableSharpening")] + [("toneMappingType", C.c_int32)] + [(n, C.c_float) for n in (
+        "exposure", "gain", "maxWhite", "gamma",
+        "local_denoise_sigma_normal", "local_denoise_sigma_depth", "local_denoise_sigma_material",
+        "large_denoise_sigma_normal", "large_denoise_sigma_depth", "large_denoise_sigma_material",
+        "temporal_denoise_sigma_normal", "temporal_denoise_sigma_depth", "temporal_denoise_sigma_material",
+        "noise_threshold_local", "noise_threshold_large")]
+
+
+def default_params() -> RtParams:
+    p = RtParams()
+    p.sky_needRegenerate = 1
+    for k, v in SKY_DEFAULTS.items():
+        setattr(p, k, v)
+    p.sampleSurfaceVsLightUseMisWeight = p.sampleSkyVsSunUseFluxWeight = 1
+    p.sampleSurfaceVsLight = p.sampleSkyVsSun = 0.5
+    for k in ("enableTemporalDenoising", "enableLocalSpatialFilter", "enableWideSpatialFilter",
+              "enableTemporalDenoising2", "enablePostProcess", "enableDownScalePasses", "enableHistogram",
+              "enableAutoExposure", "enableToneMapping", "enableSharpening"):
+        setattr(p, k, 1)
+    p.toneMappingType = 3
+    p.exposure, p.gain, p.maxWhite, p.gamma = 1.0, 40.0, 7.0, 2.2
+    p.local_denoise_sigma_normal, p.local_denoise_sigma_depth, p.local_denoise_sigma_material = 100.0, 0.1, 100.0
+    p.large_denoise_sigma_normal, p.large_denoise_sigma_depth, p.large_denoise_sigma_material = 100.0, 0.01, 100.0
+    p.temporal_denoise_sigma_normal, p.temporal_denoise_sigma_depth = 100.0, 0.1
+    p.temporal_denoise_sigma_material = 100.0
+    p.noise_threshold_local = p.noise_threshold_large = 0.001
+    return p
+
+
+class PostState(C.Structure):
+    _fields_ = [("accum", C.c_void_p), ("histColor", C.c_void_p), ("histDepth", C.c_void_p),
+                ("exposure", C.c_float * 4)]
+
+
+class DrawIO(C.Structure):
+    _fields_ = [("W", C.c_uint32), ("H", C.c_uint32), ("Ws", C.c_uint32), ("Hs", C.c_uint32),
+                ("frameNum", C.c_int), ("deltaTime", C.c_float), ("params", C.c_void_p), ("bluenoise", C.c_void_p),
+                ("color", C.c_void_p), ("normal", C.c_void_p), ("albedo", C.c_void_p), ("depth", C.c_void_p),
+                ("motion", C.c_void_p), ("noise8", C.c_void_p), ("noise16", C.c_void_p), ("c4", C.c_void_p),
+                ("c16", C.c_void_p), ("c64", C.c_void_p), ("histogram", C.c_void_p), ("scaled", C.c_void_p),
+                ("rgba", C.c_void_p), ("state", C.c_void_p)]
+
+
+class Denoiser:
+    """Frame-persistent oracle state for TemporalSpatialDenoising + PostProcessing."""
+
+    def __init__(self, W: int, H: int, Ws: int | None = None, Hs: int | None = None):
+        self.W, self.H = W, H
+        self.Ws, self.Hs = Ws or W, Hs or H
+        P = W * H
+        self.accum = np.zeros((P, 4), np.uint16)
+        self.hist_color = np.zeros((P, 4), np.uint16)
+        self.hist_depth = np.zeros(P, np.uint16)
+        self.state = PostState(self.accum.ctypes.data, self.hist_color.ctypes.data, self.hist_depth.ctypes.data,
+                               (C.c_float * 4)(1.0, 1.0, 1.0, 1.0))
+        self.bn = bluenoise_tables()
+
+    def draw(self, g: dict, frame_num: int, params=None, delta_time: float = 1000.0 / 60.0) -> dict:
+        params = params if params is not None else default_params()
+        W, H, Ws, Hs = self.W, self.H, self.Ws, self.Hs
+        d = lambda n: (n + 3) // 4
+        W4, H4 = d(W), d(H)
+        W16, H16 = d(W4), d(H4)
+        W64, H64 = d(W16), d(H16)
+        out = dict(color=np.ascontiguousarray(g["color"]).copy(),
+                   noise8=np.zeros(((H + 7) // 8) * ((W + 7) // 8), np.uint16),
+                   noise16=np.zeros(((H + 15) // 16) * ((W + 15) // 16), np.uint16),
+                   c4=np.zeros((W4 * H4, 4), np.uint16), c16=np.zeros((W16 * H16, 4), np.uint16),
+                   c64=np.zeros((W64 * H64, 4), np.uint16), histogram=np.zeros(64, np.uint32),
+                   scaled=np.zeros((Ws * Hs, 4), np.uint16), rgba=np.zeros((Ws * Hs, 4), np.uint8))
+        src = {k: np.ascontiguousarray(g[k]) for k in ("normal", "albedo", "depth", "motion")}
+        io = DrawIO(W, H, Ws, Hs, frame_num, delta_time, C.addressof(params), self.bn.ctypes.data,
+                    out["color"].ctypes.data, src["normal"].ctypes.data, src["albedo"].ctypes.data,
+                    src["depth"].ctypes.data, src["motion"].ctypes.data, out["noise8"].ctypes.data,
+                    out["noise16"].ctypes.data, out["c4"].ctypes.data, out["c16"].ctypes.data,
+                    out["c64"].ctypes.data, out["histogram"].ctypes.data, out["scaled"].ctypes.data,
+                    out["rgba"].ctypes.data, C.addressof(self.state))
+        rc = lib().orc_denoise_post(C.byref(io))
+        if rc < 0:
+            raise RuntimeError("orc_denoise_post: unsupported settings")
+        out["exposure"] = np.array(self.state.exposure[:], np.float32)
+        return out

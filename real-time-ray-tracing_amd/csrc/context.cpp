@@ -476,6 +476,11 @@ int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms) {
         if (stage == 0) rc = rt_build_bvh(ctx);
         else if (stage == 1) rc = rt_trace_primary(ctx, 1 + i, 0);
         else if (stage == 2) rc = rt_path_trace(ctx, 1 + i, 0);
+        else if (stage == 3) {
+            const int f = ctx->nextFrame++;
+            if ((rc = rt_build_bvh(ctx)) == RT_OK && (rc = rt_path_trace(ctx, f, 0)) == RT_OK)
+                rc = rt_denoise_post(ctx, f, 0);
+        } else if (stage == 4) rc = rt_denoise_post(ctx, 2 + i, 0);
         else { ctx->err = "unknown stage"; return RT_ERR_ARG; }
         if (rc != RT_OK) return rc;
     }
@@ -512,6 +517,15 @@ size_t rt_array_bytes(const rt_context* ctx, int what) {
         case RT_ARR_SKY_PDF: case RT_ARR_SKY_CDF: return (size_t)kSkySize * 4;
         case RT_ARR_SUN_PDF: case RT_ARR_SUN_CDF: return (size_t)kSunSize * 4;
         case RT_ARR_SUN_DIR: return 16;
+        case RT_ARR_HISTOGRAM: return 256;
+        case RT_ARR_EXPOSURE: return 16;
+        case RT_ARR_COLOR4: return (size_t)((ctx->renderW + 3) / 4) * ((ctx->renderH + 3) / 4) * 8;
+        case RT_ARR_COLOR16: return (size_t)((((ctx->renderW + 3) / 4) + 3) / 4) * ((((ctx->renderH + 3) / 4) + 3) / 4) * 8;
+        case RT_ARR_COLOR64: {
+            const size_t w16 = (((size_t)ctx->renderW + 3) / 4 + 3) / 4, h16 = (((size_t)ctx->renderH + 3) / 4 + 3) / 4;
+            return ((w16 + 3) / 4) * ((h16 + 3) / 4) * 8;
+        }
+        case RT_ARR_RGBA8: return (size_t)ctx->screenW * ctx->screenH * 4;
         default: return 0;
     }
 }
@@ -546,6 +560,12 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
         case RT_ARR_SKY_CDF: src = ctx->fr.skyCdf; break;
         case RT_ARR_SUN_PDF: src = ctx->fr.sunPdf; break;
         case RT_ARR_SUN_CDF: src = ctx->fr.sunCdf; break;
+        case RT_ARR_HISTOGRAM: src = ctx->fr.histogram; break;
+        case RT_ARR_EXPOSURE: src = ctx->fr.exposure; break;
+        case RT_ARR_COLOR4: src = ctx->fr.c4; break;
+        case RT_ARR_COLOR16: src = ctx->fr.c16; break;
+        case RT_ARR_COLOR64: src = ctx->fr.c64; break;
+        case RT_ARR_RGBA8: src = ctx->fr.rgba; break;
         case RT_ARR_SUN_DIR: {
             if (bytes < 16) { ctx->err = "destination too small"; return RT_ERR_ARG; }
             float* o = (float*)dst;

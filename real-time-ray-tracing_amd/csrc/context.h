@@ -49,6 +49,25 @@ struct FrameResources {
     unsigned long long* rayCounter = nullptr;
     HistCamera hist{};
     bool histValid = false;
+    // denoise + post (denoising.cu, postprocessing.cu)
+    uint2* colorB = nullptr;       // ping-pong partner of color
+    uint2* accum = nullptr;        // AccumulationColorBuffer
+    uint2* histColor = nullptr;    // HistoryColorBuffer
+    uint16_t* histDepth = nullptr; // HistoryDepthBuffer
+    uint16_t* noise8 = nullptr;
+    uint16_t* noise16 = nullptr;
+    uint2* c4 = nullptr;
+    uint2* c16 = nullptr;
+    uint2* c64 = nullptr;
+    uint32_t* histogram = nullptr;
+    float* exposure = nullptr;
+    uint2* scaledA = nullptr;
+    uint2* scaledB = nullptr;
+    uint32_t* rgba = nullptr;
+    float4* hdr = nullptr;
+    uint2* renderColor = nullptr;  // buffer that currently holds RenderColorBuffer
+    uint2* scaledColor = nullptr;  // buffer that currently holds ScaledColorBuffer
+    double lastDrawTime = -1.0;    // wall clock of the previous rt_draw (s)
 };
 
 struct rt_context {

@@ -1,0 +1,732 @@
+// denoise.hip — SVGF-style temporal + à-trous denoiser, histogram auto-exposure and the
+// post chain (scale, sharpen, tone map, dither to RGBA8) for gfx950.
+//
+// Pass order and arithmetic follow the reference (denoising.cu:5-189, temporalDenoising.cuh,
+// postprocessing.cu:5-161, postprocessing.cuh, kernel.cu:26-59, 376-381).  Differences that
+// are deliberate: every filter reads its input from the previous pass's buffer
+// and writes a second buffer (the reference filters in place while neighbouring workgroups
+// read the same surface), and only in-image pixels are written (the reference's edge threads
+// write clamped texels).  Buffer reads clamp to the image edge like CUDA surfaces.
+//
+// Data layout (render size W x H, screen Ws x Hs), all row-major:
+//   colour      uint2  = half r | half g << 16, half b | ushort mask << 16
+//   normal      uint2  = half4, albedo uint2 = half4, depth ushort = half, motion uint = half2
+//   noise8/16   ushort = half per 8x8 / 16x16 tile
+//   c4/c16/c64  uint2  = half4 (DownScale4 chain), histogram uint32[64], exposure float[4]
+//   scaled      uint2  = half4 at screen size, rgba uint32 = RGBA8
+#include "frame_kernels.h"
+#include "pt_common.h"
+#include "rt_device.h"
+#include "rtmath.h"
+
+using namespace rtd;
+
+namespace {
+
+constexpr float kRayMaxF = 10e10f;
+
+// gaussian.cuh:12-47 (double literals converted to float, as the reference's float arrays)
+__constant__ float cG3[9] = {(float)0.0578968, (float)0.0921378, (float)0.0584323, (float)0.0921378, (float)0.146629,
+                             (float)0.09299,   (float)0.0584322, (float)0.0929898, (float)0.0589727};
+__constant__ float cG5[25] = {
+    (float)0.00360466, (float)0.0144464, (float)0.0229902, (float)0.01458,   (float)0.0036719,
+    (float)0.0144464,  (float)0.0578968, (float)0.0921378, (float)0.0584323, (float)0.0147159,
+    (float)0.0229902,  (float)0.0921378, (float)0.146629,  (float)0.09299,   (float)0.023419,
+    (float)0.01458,    (float)0.0584322, (float)0.0929898, (float)0.0589727, (float)0.014852,
+    (float)0.00367191, (float)0.0147158, (float)0.0234191, (float)0.0148519, (float)0.0037404};
+__constant__ float cG7[49] = {
+    (float)3.47404e-05, (float)0.000353875, (float)0.00141822, (float)0.00225698, (float)0.00143134,
+    (float)0.000360475, (float)3.57221e-05, (float)0.000353875, (float)0.00360466, (float)0.0144464,
+    (float)0.0229902,   (float)0.01458,     (float)0.0036719,  (float)0.000363875, (float)0.00141822,
+    (float)0.0144464,   (float)0.0578968,   (float)0.0921378,  (float)0.0584323,  (float)0.0147159,
+    (float)0.0014583,   (float)0.00225698,  (float)0.0229902,  (float)0.0921378,  (float)0.146629,
+    (float)0.09299,     (float)0.023419,    (float)0.00232076, (float)0.00143134, (float)0.01458,
+    (float)0.0584322,   (float)0.0929898,   (float)0.0589727,  (float)0.014852,   (float)0.00147179,
+    (float)0.000360475, (float)0.00367191,  (float)0.0147158,  (float)0.0234191,  (float)0.0148519,
+    (float)0.0037404,   (float)0.000370662, (float)3.57221e-05, (float)0.000363875, (float)0.0014583,
+    (float)0.00232075,  (float)0.00147179,  (float)0.000370662, (float)3.67315e-05};
+
+RT_DEV float h2f(uint32_t h) { return rt_h2f((uint16_t)h); }
+RT_DEV uint32_t f2h(float f) { return rt_f2h(f); }
+RT_DEV int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+RT_DEV bool isnan3(F3 v) { return v.x != v.x || v.y != v.y || v.z != v.z; }
+RT_DEV float clampf(float a, float lo = 0.0f, float hi = 1.0f) { return a < lo ? lo : a > hi ? hi : a; }
+RT_DEV F3 clamp3(F3 a, F3 lo, F3 hi) { return f3(clampf(a.x, lo.x, hi.x), clampf(a.y, lo.y, hi.y), clampf(a.z, lo.z, hi.z)); }
+RT_DEV F3 fmax3(F3 a, F3 b) { return f3(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z)); }
+RT_DEV F3 fmin3(F3 a, F3 b) { return f3(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z)); }
+RT_DEV F3 ycocg(F3 c) {
+    const float t1 = c.x + c.z, t2 = c.y * 2.0f;
+    return f3(t1 + t2, (c.x - c.z) * 2.0f, t2 - t1);
+}
+RT_DEV F3 ycocg_inv(F3 c) {
+    const float t = c.x - c.z;
+    return f3(t + c.y, c.x + c.z, t - c.y) * 0.25f;
+}
+
+RT_DEV F3 rgb_of(uint2 q) { return f3(h2f(q.x & 0xFFFFu), h2f(q.x >> 16), h2f(q.y & 0xFFFFu)); }
+RT_DEV uint32_t mask_of(uint2 q) { return q.y >> 16; }
+RT_DEV uint2 pack_color(F3 c, uint32_t mask) {
+    return make_uint2(f2h(c.x) | (f2h(c.y) << 16), f2h(c.z) | (mask << 16));
+}
+
+struct View2 {  // clamped reads of a W x H uint2 image
+    const uint2* p;
+    int W, H;
+    RT_DEV uint2 at(int x, int y) const { return p[(size_t)clampi(y, 0, H - 1) * W + clampi(x, 0, W - 1)]; }
+};
+struct View1 {
+    const uint16_t* p;
+    int W, H;
+    RT_DEV float at(int x, int y) const { return h2f(p[(size_t)clampi(y, 0, H - 1) * W + clampi(x, 0, W - 1)]); }
+};
+
+RT_DEV F3 bicubic_smooth(const View2& im, F2 uv) {
+    const F2 UV = {uv.x * (float)im.W, uv.y * (float)im.H};
+    const float fx0 = floorf(UV.x - 0.5f), fy0 = floorf(UV.y - 0.5f);
+    const F2 f = {UV.x - (fx0 + 0.5f), UV.y - (fy0 + 0.5f)};
+    const F2 f2 = {f.x * f.x, f.y * f.y};
+    const F2 f3v = {f2.x * f.x, f2.y * f.y};
+    const F2 w1 = {f3v.x * -2.0f + f2.x * 3.0f, f3v.y * -2.0f + f2.y * 3.0f};
+    const F2 w0 = {1.0f - w1.x, 1.0f - w1.y};
+    const int t0x = (int)fx0, t0y = (int)fy0;
+    const float wt[4] = {w0.x * w0.y, w1.x * w0.y, w0.x * w1.y, w1.x * w1.y};
+    F3 o = f3(0.0f);
+    float sw = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        sw += wt[i];
+        o = o + rgb_of(im.at(t0x + (i & 1), t0y + (i >> 1))) * wt[i];
+    }
+    return o / sw;
+}
+
+// ------------------------------------------------------------------ TemporalFilter
+__global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uint2* in, uint2* out) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const int W = (int)P.W, H = (int)P.H;
+    if (x >= W || y >= H) return;
+    const View2 col{in, W, H}, nrm{P.normal, W, H}, acc{P.accum, W, H};
+    const View1 dep{P.depth, W, H};
+    const size_t p = (size_t)y * W + x;
+    const uint2 c0 = in[p];
+    uint2 res = c0;
+    F3 cV = rgb_of(c0);
+    float dV = dep.at(x, y);
+    F3 nV = rgb_of(nrm.at(x, y));
+    const uint32_t mV = mask_of(c0);
+    if (dV != dV) dV = 0.0f;
+    if (isnan3(nV)) nV = f3(0.0f);
+    if (!isnan3(cV) && dV < kRayMaxF) {
+        F3 nMax = ycocg(cV), nMin = ycocg(cV);
+        F3 filt = f3(0.0f);
+        float wsum = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            const int xo = j % 3, yo = j / 3;
+            const int sx = x + xo - 1, sy = y + yo - 1;
+            const uint2 q = col.at(sx, sy);
+            const F3 cc = rgb_of(q);
+            const float d = dep.at(sx, sy);
+            const F3 n = rgb_of(nrm.at(sx, sy));
+            float w = 1.0f;
+            w *= rt_powf(fmaxf(dot(nV, n), 0.0f), P.dn.temporal_denoise_sigma_normal);
+            const float dd = (dV - d) / P.dn.temporal_denoise_sigma_depth;
+            w *= rt_expf(-0.5f * dd * dd);
+            w *= (mV != mask_of(q)) ? 1.0f / P.dn.temporal_denoise_sigma_material : 1.0f;
+            w *= cG3[xo + yo * 3];
+            filt = filt + cc * w;
+            wsum += w;
+            const F3 nc = ycocg(cc);
+            nMax = fmax3(nMax, nc);
+            nMin = fmin3(nMin, nc);
+        }
+        if (wsum > 0) filt = filt / wsum;
+        else filt = f3(0.0f);
+        if (isnan3(filt)) filt = f3(0.0f);
+        const uint32_t mvq = P.motion[p];
+        const F2 mv = {h2f(mvq & 0xFFFFu) - 0.5f, h2f(mvq >> 16) - 0.5f};
+        const F2 inv = {1.0f / (float)W, 1.0f / (float)H};
+        const F2 uv = {((float)x + 0.5f) * inv.x, ((float)y + 0.5f) * inv.y};
+        const F2 huv = {uv.x + mv.x, uv.y + mv.y};
+        if (huv.x < 0 || huv.y < 0 || huv.x > 1.0f || huv.y > 1.0f) {
+            res = pack_color(filt, mV);
+        } else {
+            F3 cH = bicubic_smooth(acc, huv);
+            const F3 cHy = clamp3(ycocg(cH), nMin, nMax);
+            cH = ycocg_inv(cHy);
+            const float lumaMin = nMin.x, lumaMax = nMax.x, lumaC = ycocg(cV).x;
+            float discard = 0.0f;
+            const int hx = (int)floorf(huv.x * (float)W), hy = (int)floorf(huv.y * (float)H);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) discard += (mV != mask_of(acc.at(hx + i % 2, hy + i / 2))) ? 1.0f : 0.0f;
+            discard /= 4.0f;
+            cH = cH * (1.0f - discard) + filt * discard;
+            const float lumaH = ycocg(cH).x;
+            if (isnan3(cH)) cH = f3(0.0f);
+            float blend = 1.0f / 8.0f;
+            blend *= 0.2f + 0.8f * clampf(0.5f * fminf(fabsf(lumaH - lumaMin), fabsf(lumaH - lumaMax)) /
+                                         fmaxf(fmaxf(lumaH, lumaC), 1e-4f));
+            float wA = blend * fmaxf(0.0001f, 1.0f / (lumaC + 4.0f));
+            float wB = (1.0f - blend) * fmaxf(0.0001f, 1.0f / (lumaH + 4.0f));
+            const float ws = safe_divide(1.0f, wA + wB);
+            wA *= ws;
+            wB *= ws;
+            F3 o = cV * wA + cH * wB;
+            if (isnan3(o)) o = f3(0.0f);
+            res = pack_color(o, mV);
+        }
+    }
+    out[p] = res;
+}
+
+// ------------------------------------------------------------------ tile noise level
+// One 32-lane group per 8x8 tile (two per wave64): lane L = tx + 8*ty covers rows 2ty, 2ty+1.
+// Sums use the reference's __shfl_down tree (offsets 16..1) so lane 0 gets its exact order.
+template <typename T>
+RT_DEV T tree_sum32(T v) {
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) v = v + __shfl_down(v, off, 32);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_tile_noise(DenoisePostParams P, const uint2* color) {
+    const int W = (int)P.W, H = (int)P.H;
+    const int W8 = (W + 7) / 8, H8 = (H + 7) / 8;
+    const int tile = blockIdx.x * 8 + (threadIdx.x >> 5), lane = threadIdx.x & 31;
+    const bool valid = tile < W8 * H8;
+    const int bx = valid ? tile % W8 : 0, by = valid ? tile / W8 : 0;
+    const View2 col{color, W, H};
+    const View1 dep{P.depth, W, H};
+    const int x = bx * 8 + (lane & 7), ya = by * 8 + 2 * (lane >> 3), yb = ya + 1;
+    const F3 ca = rgb_of(col.at(x, ya)), cb = rgb_of(col.at(x, yb));
+    const uint32_t bg = (dep.at(x, ya) >= kRayMaxF ? 1u : 0u), bg2 = (dep.at(x, yb) >= kRayMaxF ? 1u : 0u);
+    const float l1 = fmaxf(fmaxf(ca.x, ca.y), ca.z), l2 = fmaxf(fmaxf(cb.x, cb.y), cb.z);
+    const uint32_t b1s = tree_sum32(bg), b2s = tree_sum32(bg2);
+    const float s1 = tree_sum32(l1), s12 = tree_sum32(l1 * l1), s2 = tree_sum32(l2), s22 = tree_sum32(l2 * l2);
+    if (lane == 0 && valid) {
+        const float notSky = 1.0f - (float)(b1s + b2s) / 64.0f;
+        const float lumAve = (s1 + s2) / 64.0f;
+        const float lumAveSq = lumAve * lumAve;
+        const float lumSqAve = (s12 + s22) / 64.0f;
+        const float var = fmaxf(1e-20f, lumSqAve - lumAveSq);
+        float noise = var / fmaxf(lumAveSq, 1e-20f);
+        noise *= notSky;
+        P.noise8[tile] = (uint16_t)f2h(noise);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_noise16(DenoisePostParams P) {
+    const int W8 = ((int)P.W + 7) / 8, H8 = ((int)P.H + 7) / 8, W16 = ((int)P.W + 15) / 16, H16 = ((int)P.H + 15) / 16;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= W16 * H16) return;
+    const int x = i % W16, y = i / W16;
+    const View1 n8{P.noise8, W8, H8};
+    const float v1 = n8.at(2 * x, 2 * y), v2 = n8.at(2 * x + 1, 2 * y), v3 = n8.at(2 * x, 2 * y + 1),
+                v4 = n8.at(2 * x + 1, 2 * y + 1);
+    P.noise16[i] = (uint16_t)f2h((v1 + v2 + v3 + v4) / 4);
+}
+
+// TileNoiseLevelVisualize (debug pass): outline 16x16 tiles above the noise threshold
+__global__ __launch_bounds__(256) void k_noise_visualize(DenoisePostParams P, uint2* color, int level) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= (int)P.W || y >= (int)P.H) return;
+    const int tx = x & 15, ty = y & 15;
+    if (!(tx == 0 || tx == 15 || ty == 0 || ty == 15)) return;
+    const int W16 = ((int)P.W + 15) / 16;
+    const float thr = level == 1 ? P.dn.noise_threshold_local : P.dn.noise_threshold_large;
+    if (!(h2f(P.noise16[(y >> 4) * W16 + (x >> 4)]) > thr)) return;
+    const size_t p = (size_t)y * P.W + x;
+    color[p] = pack_color(level == 1 ? f3(1.0f, 0.5f, 0.0f) : f3(1.0f, 0.0f, 0.0f), 0xFFFFu);
+    P.normal[p] = make_uint2(0u, 0u);
+    P.depth[p] = (uint16_t)f2h(kRayMaxF);
+}
+
+// ------------------------------------------------------------------ SpatialFilter7x7
+// 16x16 tile + 3-pixel apron staged in LDS (22 x 22 entries of colour, normal, depth).
+struct Tap7 { uint2 c; uint2 n; float d; };
+
+__global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uint2* in, uint2* out) {
+    __shared__ uint2 sC[22 * 22];
+    __shared__ uint2 sN[22 * 22];
+    __shared__ float sD[22 * 22];
+    const int W = (int)P.W, H = (int)P.H;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int x = blockIdx.x * 16 + tx, y = blockIdx.y * 16 + ty;
+    const int W16 = (W + 15) / 16;
+    const bool gated = h2f(P.noise16[blockIdx.y * W16 + blockIdx.x]) < P.dn.noise_threshold_local;
+    const View2 col{in, W, H}, nrm{P.normal, W, H};
+    const View1 dep{P.depth, W, H};
+    if (!gated) {
+        for (int i = threadIdx.x; i < 22 * 22; i += 256) {
+            const int lx = blockIdx.x * 16 - 3 + i % 22, ly = blockIdx.y * 16 - 3 + i / 22;
+            sC[i] = col.at(lx, ly);
+            sN[i] = nrm.at(lx, ly);
+            sD[i] = dep.at(lx, ly);
+        }
+    }
+    __syncthreads();
+    if (x >= W || y >= H) return;
+    const size_t p = (size_t)y * W + x;
+    if (gated) { out[p] = in[p]; return; }
+    const int ci = (tx + 3) + (ty + 3) * 22;
+    const uint2 c0 = sC[ci];
+    uint2 res = c0;
+    const F3 cV = rgb_of(c0);
+    float dV = sD[ci];
+    F3 nV = rgb_of(sN[ci]);
+    const uint32_t mV = mask_of(c0);
+    if (dV != dV) dV = 0.0f;
+    if (isnan3(nV)) nV = f3(0.0f);
+    if (!isnan3(cV) && dV < kRayMaxF) {
+        F3 sum = f3(0.0f);
+        float sw = 0.0f;
+        int j = P.frameNum % 2;
+        for (int i = 0; i < 24; ++i) {
+            const int xo = j % 7, yo = j / 7;
+            j += 2;
+            const int li = (tx + xo) + (ty + yo) * 22;
+            const uint2 q = sC[li];
+            F3 cc = rgb_of(q);
+            float d = sD[li];
+            F3 n = rgb_of(sN[li]);
+            if (isnan3(cc)) cc = f3(0.0f);
+            if (d != d) d = 0.0f;
+            if (isnan3(n)) n = f3(0.0f);
+            float w = 1.0f;
+            w *= rt_powf(fmaxf(dot(nV, n), 0.0001f), P.dn.local_denoise_sigma_normal);
+            const float dd = (dV - d) / P.dn.local_denoise_sigma_depth;
+            w *= rt_expf(-0.5f * dd * dd);
+            w *= (mV != mask_of(q)) ? 1.0f / P.dn.local_denoise_sigma_material : 1.0f;
+            w *= cG7[xo + yo * 7];
+            sum = sum + cc * w;
+            sw += w;
+        }
+        if (isnan3(sum)) sum = f3(0.0f);
+        if (sw != sw) sw = 0.0f;
+        F3 fin = sw == 0 ? f3(0.0f) : sum / sw;
+        if (isnan3(fin)) fin = f3(0.0f);
+        res = pack_color(fin, mV);
+    }
+    out[p] = res;
+}
+
+// ------------------------------------------------------------------ SpatialFilterGlobal5x5<S>
+template <int S>
+__global__ __launch_bounds__(256) void k_spatial5(DenoisePostParams P, const uint2* in, uint2* out) {
+    const int W = (int)P.W, H = (int)P.H;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const size_t p = (size_t)y * W + x;
+    const int W16 = (W + 15) / 16;
+    const uint2 c0 = in[p];
+    uint2 res = c0;
+    if (!(h2f(P.noise16[blockIdx.y * W16 + blockIdx.x]) < P.dn.noise_threshold_large)) {
+        const View2 col{in, W, H}, nrm{P.normal, W, H};
+        const View1 dep{P.depth, W, H};
+        F3 nV = rgb_of(P.normal[p]);
+        F3 cV = rgb_of(c0);
+        const uint32_t mV = mask_of(c0);
+        float dV = h2f(P.depth[p]);
+        if (isnan3(cV)) cV = f3(0.0f);
+        if (dV != dV) dV = 0.0f;
+        if (isnan3(nV)) nV = f3(0.0f);
+        if (dV < 10e9f) {
+            F3 sum = f3(0.0f);
+            float sw = 0.0f;
+#pragma unroll 5
+            for (int k = 0; k < 25; ++k) {
+                const int i = k % 5, j = k / 5;
+                const int sx = x + (i - 2) * S, sy = y + (j - 2) * S;
+                const uint2 q = col.at(sx, sy);
+                F3 cc = rgb_of(q);
+                const float d = dep.at(sx, sy);
+                const F3 n = rgb_of(nrm.at(sx, sy));
+                float w = 1.0f;
+                w *= rt_powf(fmaxf(dot(nV, n), 0.0f), P.dn.large_denoise_sigma_normal);
+                const float dd = (dV - d) / P.dn.large_denoise_sigma_depth;
+                w *= rt_expf(-0.5f * dd * dd);
+                w *= (mV != mask_of(q)) ? 1.0f / P.dn.large_denoise_sigma_material : 1.0f;
+                w *= cG5[i + j * 5];
+                if (isnan3(cc)) { cc = f3(0.0f); w = 0.0f; }
+                sum = sum + cc * w;
+                sw += w;
+            }
+            if (isnan3(sum)) sum = f3(0.0f);
+            if (sw != sw) sw = 0.0f;
+            F3 fin = sw == 0 ? f3(0.0f) : sum / sw;
+            if (isnan3(fin)) fin = f3(0.0f);
+            res = pack_color(fin, mV);
+        }
+    }
+    out[p] = res;
+}
+
+// ------------------------------------------------------------------ ApplyAlbedo (in place, pointwise)
+__global__ __launch_bounds__(256) void k_apply_albedo(DenoisePostParams P, uint2* color) {
+    const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= (size_t)P.W * P.H) return;
+    const F3 c = rgb_of(color[p]);
+    const F3 a = rgb_of(P.albedo[p]);
+    color[p] = pack_color(c * a, 0x3C00u);  // w = half(1.0)
+}
+
+// ------------------------------------------------------------------ TemporalFilter2
+__global__ __launch_bounds__(256) void k_temporal2(DenoisePostParams P, const uint2* in, uint2* out) {
+    const int W = (int)P.W, H = (int)P.H;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const size_t p = (size_t)y * W + x;
+    const View2 col{in, W, H}, hc{P.histColor, W, H};
+    const uint2 c0 = in[p];
+    out[p] = c0;
+    const F3 cV = ycocg_inv(ycocg(rgb_of(c0)));
+    const int mV = (int)mask_of(c0);
+    const float FLTMIN = 1.17549435e-38f, FLTMAX = 3.402823466e+38f;
+    F3 nMax = f3(FLTMIN), nMin = f3(FLTMAX), nMax2 = f3(FLTMIN), nMin2 = f3(FLTMAX);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        const int xo = j % 3, yo = j / 3;
+        const uint2 q = col.at(x + xo - 1, y + yo - 1);
+        if ((int)mask_of(q) == mV) {
+            const F3 cc = ycocg(rgb_of(q));
+            nMax = fmax3(nMax, cc);
+            nMin = fmin3(nMin, cc);
+            if (abs(xo - 1) + abs(yo - 1) <= 1) {
+                nMax2 = fmax3(nMax2, cc);
+                nMin2 = fmin3(nMin2, cc);
+            }
+        }
+    }
+    nMax = (nMax + nMax2) / 2.0f;
+    nMin = (nMin + nMin2) / 2.0f;
+    const uint32_t mvq = P.motion[p];
+    const F2 mv = {h2f(mvq & 0xFFFFu) - 0.5f, h2f(mvq >> 16) - 0.5f};
+    const F2 inv = {1.0f / (float)W, 1.0f / (float)H};
+    const F2 uv = {((float)x + 0.5f) * inv.x, ((float)y + 0.5f) * inv.y};
+    const F2 huv = {uv.x + mv.x, uv.y + mv.y};
+    if (huv.x < 0 || huv.y < 0 || huv.x > 1.0f || huv.y > 1.0f) return;
+    F3 cH = bicubic_smooth(hc, huv);
+    const F3 cHy = clamp3(ycocg(cH), nMin, nMax);
+    cH = ycocg_inv(cHy);
+    const float lumaMin = nMin.x, lumaMax = nMax.x, lumaC = ycocg(cV).x;
+    float discard = 0.0f;
+    const int hx = (int)floorf(huv.x * (float)W), hy = (int)floorf(huv.y * (float)H);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) discard += (mV != (int)mask_of(hc.at(hx + i % 2, hy + i / 2))) ? 1.0f : 0.0f;
+    discard /= 4.0f;
+    if (discard == 1.0f) return;
+    cH = cH * (1.0f - discard) + cV * discard;
+    const float lumaH = ycocg(cH).x;
+    float blend = 3.0f / 4.0f;
+    blend *= 0.2f + 0.8f * clampf(0.5f * fminf(fabsf(lumaH - lumaMin), fabsf(lumaH - lumaMax)) /
+                                 fmaxf(fmaxf(lumaH, lumaC), 1e-4f));
+    float wA = blend * fmaxf(0.0001f, 1.0f / (lumaC + 4.0f));
+    float wB = (1.0f - blend) * fmaxf(0.0001f, 1.0f / (lumaH + 4.0f));
+    const float ws = safe_divide(1.0f, wA + wB);
+    wA *= ws;
+    wB *= ws;
+    F3 o = cV * wA + cH * wB;
+    if (isnan3(o)) o = f3(0.0f);
+    out[p] = pack_color(o, (uint32_t)mV & 0xFFFFu);
+}
+
+// ------------------------------------------------------------------ post
+struct H4 { float x, y, z, w; };
+RT_DEV H4 h4_of(uint2 q) { return H4{h2f(q.x & 0xFFFFu), h2f(q.x >> 16), h2f(q.y & 0xFFFFu), h2f(q.y >> 16)}; }
+RT_DEV H4 add4(H4 a, H4 b) { return H4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+RT_DEV uint2 pack_h4(H4 v) { return make_uint2(f2h(v.x) | (f2h(v.y) << 16), f2h(v.z) | (f2h(v.w) << 16)); }
+
+// DownScale4: output texel = 4x4 box of inputs, summed as the reference's 2x2-of-2x2 tree
+__global__ __launch_bounds__(256) void k_downscale4(const uint2* in, int Wi, int Hi, uint2* out, int Wo, int Ho) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= Wo * Ho) return;
+    const int ox = i % Wo, oy = i / Wo;
+    const View2 im{in, Wi, Hi};
+    H4 q[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            H4 s[2][2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const H4 t = h4_of(im.at(4 * ox + 2 * a + u, 4 * oy + 2 * b + v));
+                    s[u][v] = H4{t.x / 16, t.y / 16, t.z / 16, t.z / 16};  // Float4::operator/ (linearMath.h:423)
+                }
+            q[a][b] = add4(add4(add4(s[0][0], s[1][0]), s[0][1]), s[1][1]);
+        }
+    out[i] = pack_h4(add4(add4(add4(q[0][0], q[1][0]), q[0][1]), q[1][1]));
+}
+
+// Histogram2: one 32x32 workgroup over the top-left min(W64,32) x min(H64,32) texels
+__global__ __launch_bounds__(1024) void k_histogram(const uint2* c64, int W64, int H64, uint32_t* hist) {
+    __shared__ uint32_t h[64];
+    if (threadIdx.x < 64) h[threadIdx.x] = 0u;
+    __syncthreads();
+    const int x = threadIdx.x & 31, y = threadIdx.x >> 5;
+    const int tw = W64 < 32 ? W64 : 32, th = H64 < 32 ? H64 : 32;
+    if (x < tw && y < th) {
+        const H4 v = h4_of(c64[y * W64 + x]);
+        const float lum = dot(f3(v.x, v.y, v.z), f3((float)0.3, (float)0.6, (float)0.1));
+        const float logL = (float)((double)rt_log2f(lum) * 0.1 + 0.75);
+        const float sc = (float)((double)(clampf(logL, 0.0f, 1.0f) * 63) * 0.99999);
+        atomicAdd(&h[(uint32_t)rintf(sc)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) hist[threadIdx.x] = h[threadIdx.x];
+}
+
+RT_DEV float bin_to_lum(int i) { return rt_exp2f((float)(((double)(float)i / (63 * 0.99999) - 0.75) / 0.1)); }
+
+__global__ void k_auto_exposure(float* e, const uint32_t* hist, float area, float deltaTime, float gain, int enabled,
+                                float fixedExposure) {
+    if (threadIdx.x != 0) return;
+    if (!enabled) {
+        e[0] = fixedExposure;
+        e[1] = e[2] = e[3] = 1.0f;
+        return;
+    }
+    const float darkT = (float)0.4, brightT = (float)0.9;
+    float lumiSum = 0, lumiSumArea = 0, accu = 0, brightLum = 0;
+    int i = 0;
+    for (; i < 64; ++i) {
+        const float fHist = (float)hist[i] / area;
+        const float lum = bin_to_lum(i);
+        accu += fHist;
+        const float dark = accu - darkT;
+        if (dark > 0) {
+            lumiSumArea += dark;
+            lumiSum += dark * lum;
+            break;
+        }
+    }
+    for (; i < 64; ++i) {
+        const float fHist = (float)hist[i] / area;
+        const float lum = bin_to_lum(i);
+        accu += fHist;
+        const float bright = accu - brightT;
+        if (bright > 0) {
+            const float partial = brightT - (accu - fHist);
+            lumiSumArea += partial;
+            lumiSum += partial * lum;
+            brightLum = lum;
+            break;
+        } else {
+            lumiSumArea += fHist;
+            lumiSum += fHist * lum;
+        }
+    }
+    float aveLum = clampf(lumiSum / lumiSumArea, 0.1f, 100.0f);
+    float lumTemp = e[1], lumBright = e[2];
+    const float k = 1.0f - rt_expf(-deltaTime * 0.001f);
+    lumTemp = lumTemp + (aveLum - lumTemp) * k;
+    lumBright = lumBright + (brightLum - lumBright) * k;
+    const float EC = 1.03f - 2.0f / (rt_log10f(lumTemp + 1.0f) + 2.0f);
+    e[0] = gain * EC / lumTemp;
+    e[1] = lumTemp;
+    e[2] = lumBright;
+    e[3] = brightLum;
+}
+
+// BicubicScale with SampleBicubicCatmullRom (16 taps, clamped)
+__global__ __launch_bounds__(256) void k_bicubic_scale(const uint2* in, int W, int H, uint2* out, int Ws, int Hs) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= Ws || y >= Hs) return;
+    const View2 im{in, W, H};
+    const F2 uv = {(float)x / Ws, (float)y / Hs};
+    const F2 UV = {uv.x * (float)W, uv.y * (float)H};
+    const float fx0 = floorf(UV.x - 0.5f), fy0 = floorf(UV.y - 0.5f);
+    const F2 f = {UV.x - (fx0 + 0.5f), UV.y - (fy0 + 0.5f)};
+    const F2 f2 = {f.x * f.x, f.y * f.y};
+    const F2 f3v = {f2.x * f.x, f2.y * f.y};
+    const F2 w0 = {f2.x - 0.5f * (f3v.x + f.x), f2.y - 0.5f * (f3v.y + f.y)};
+    const F2 w1 = {1.5f * f3v.x - 2.5f * f2.x + 1.0f, 1.5f * f3v.y - 2.5f * f2.y + 1.0f};
+    const F2 w3 = {0.5f * (f3v.x - f2.x), 0.5f * (f3v.y - f2.y)};
+    const F2 w2 = {1.0f - w0.x - w1.x - w3.x, 1.0f - w0.y - w1.y - w3.y};
+    const int t1x = (int)fx0, t1y = (int)fy0;
+    const float wx[4] = {w0.x, w1.x, w2.x, w3.x}, wy[4] = {w0.y, w1.y, w2.y, w3.y};
+    F3 o = f3(0.0f);
+    float sw = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float w = wx[i] * wy[j];
+            sw += w;
+            o = o + rgb_of(im.at(t1x - 1 + i, t1y - 1 + j)) * w;
+        }
+    o = o / sw;
+    out[(size_t)y * Ws + x] = pack_color(o, 0x3C00u);
+}
+
+// SharpeningFilter (FidelityFX CAS), then the selected tone mapper and CopyToOutput's dither,
+// fused: the sharpened and tone-mapped values are rounded to half in between, as the
+// reference's separate passes store and reload them.
+__global__ __launch_bounds__(256) void k_sharpen_tonemap_output(DenoisePostParams P, const uint2* in, uint2* out) {
+    const int Ws = (int)P.Ws, Hs = (int)P.Hs;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= Ws || y >= Hs) return;
+    const size_t p = (size_t)y * Ws + x;
+    const View2 im{in, Ws, Hs};
+    uint2 cur = in[p];
+    if (P.sharpen) {
+        F3 c[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) c[i][j] = rgb_of(im.at(x + i - 1, y + j - 1));
+        F3 t1 = fmax3(fmax3(c[1][1], c[0][1]), c[2][1]);
+        F3 t2 = fmax3(fmax3(t1, c[1][0]), c[1][2]);
+        F3 t3 = fmax3(fmax3(t2, c[0][0]), c[0][2]);
+        F3 t4 = fmax3(fmax3(t3, c[2][0]), c[2][2]);
+        const F3 smax = t2 + t4;
+        t1 = fmin3(fmin3(c[1][1], c[0][1]), c[2][1]);
+        t2 = fmin3(fmin3(t1, c[1][0]), c[1][2]);
+        t3 = fmin3(fmin3(t2, c[0][0]), c[0][2]);
+        t4 = fmin3(fmin3(t3, c[2][0]), c[2][2]);
+        const F3 smin = t2 + t4;
+        F3 amp = clamp3(fmin3(smin, f3(2.0f - smax.x, 2.0f - smax.y, 2.0f - smax.z)) / smax, f3(0.0f), f3(1.0f));
+        amp = f3(1.0f / __builtin_sqrtf(amp.x), 1.0f / __builtin_sqrtf(amp.y), 1.0f / __builtin_sqrtf(amp.z));
+        const float peak = 8.0f - 3.0f * 1.0f;
+        const F3 w = f3(-1.0f) / (amp * peak);
+        F3 o = (((c[0][1] + c[2][1]) + c[1][0]) + c[1][2]) * w + c[1][1];
+        o = o / (f3(1.0f) + f3(4.0f) * w);
+        cur = pack_color(o, 0x3C00u);
+    }
+    if (P.tonemap) {  // ToneMappingReinhardExtended
+        F3 c = rgb_of(cur) * P.exposure[0];
+        const F3 wl = f3(0.2126f, 0.7152f, 0.0722f);
+        const float lo = dot(c, wl);
+        const float num = lo * (1.0f + (lo / (P.maxWhite * P.maxWhite)));
+        const float ln = num / (1.0f + lo);
+        c = c * (ln / dot(c, wl));
+        const float g = 1.0f / P.gamma;
+        c = clamp3(f3(rt_powf(c.x, g), rt_powf(c.y, g), rt_powf(c.z, g)), f3(0.0f), f3(1.0f));
+        cur = pack_color(c, 0x3C00u);
+    }
+    out[p] = cur;
+    // CopyToOutput (kernel.cu:26-59): blue-noise dither (bn/256; the -1/512 is integer 0)
+    const int s = P.frameNum;
+    F3 c = rgb_of(cur) + f3(bluenoise(P.bluenoise, x, y, s, 0) / 256, bluenoise(P.bluenoise, x, y, s, 1) / 256,
+                            bluenoise(P.bluenoise, x, y, s, 2) / 256);
+    const float hi = 1.0f - 1.1920928955078125e-07f;
+    c = clamp3(c, f3(0.0f), f3(hi));
+    P.rgba[p] = (uint32_t)(uint8_t)(c.x * 256) | ((uint32_t)(uint8_t)(c.y * 256) << 8) |
+                ((uint32_t)(uint8_t)(c.z * 256) << 16) | (1u << 24);
+}
+
+__global__ __launch_bounds__(256) void k_hdr_out(const uint2* color, float4* hdr, size_t n) {
+    const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    const F3 c = rgb_of(color[p]);
+    hdr[p] = make_float4(c.x, c.y, c.z, 1.0f);
+}
+
+}  // namespace
+
+#define LAUNCH_CHECK()                          \
+    do {                                        \
+        hipError_t e__ = hipGetLastError();     \
+        if (e__ != hipSuccess) return e__;      \
+    } while (0)
+
+extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
+    const int W = (int)P->W, H = (int)P->H, Ws = (int)P->Ws, Hs = (int)P->Hs;
+    const size_t Pn = (size_t)W * H;
+    const dim3 g16((W + 15) / 16, (H + 15) / 16), b256(256);
+    uint2* cur = P->colorA;
+    uint2* alt = P->colorB;
+    auto swap = [&]() { uint2* t = cur; cur = alt; alt = t; };
+    const int W8 = (W + 7) / 8, H8 = (H + 7) / 8, W16 = (W + 15) / 16, H16 = (H + 15) / 16;
+    // ---- TemporalSpatialDenoising (denoising.cu:51-188)
+    if (P->temporal && P->frameNum != 1) {
+        hipLaunchKernelGGL(k_temporal, g16, b256, 0, s, *P, (const uint2*)cur, alt);
+        LAUNCH_CHECK();
+        swap();
+    }
+    auto noise = [&](int level) -> hipError_t {
+        hipLaunchKernelGGL(k_tile_noise, dim3((W8 * H8 + 7) / 8), b256, 0, s, *P, (const uint2*)cur);
+        LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_noise16, dim3((W16 * H16 + 255) / 256), b256, 0, s, *P);
+        LAUNCH_CHECK();
+        if (P->visualize) {
+            hipLaunchKernelGGL(k_noise_visualize, g16, b256, 0, s, *P, cur, level);
+            LAUNCH_CHECK();
+        }
+        return hipSuccess;
+    };
+    hipError_t e;
+    if (P->localSpatial) {
+        if ((e = noise(1)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_spatial7, g16, b256, 0, s, *P, (const uint2*)cur, alt);
+        LAUNCH_CHECK();
+        swap();
+    }
+    if (P->temporal) {
+        if ((e = hipMemcpyAsync(P->accum, cur, Pn * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    }
+    if (P->wideSpatial) {
+        if ((e = noise(2)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_spatial5<3>, g16, b256, 0, s, *P, (const uint2*)cur, alt);
+        LAUNCH_CHECK();
+        swap();
+        hipLaunchKernelGGL(k_spatial5<6>, g16, b256, 0, s, *P, (const uint2*)cur, alt);
+        LAUNCH_CHECK();
+        swap();
+        hipLaunchKernelGGL(k_spatial5<12>, g16, b256, 0, s, *P, (const uint2*)cur, alt);
+        LAUNCH_CHECK();
+        swap();
+    }
+    hipLaunchKernelGGL(k_apply_albedo, dim3((unsigned)((Pn + 255) / 256)), b256, 0, s, *P, cur);
+    LAUNCH_CHECK();
+    if (P->temporal2) {
+        if (P->frameNum != 1) {
+            hipLaunchKernelGGL(k_temporal2, g16, b256, 0, s, *P, (const uint2*)cur, alt);
+            LAUNCH_CHECK();
+            swap();
+        }
+        if ((e = hipMemcpyAsync(P->histColor, cur, Pn * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(P->histDepth, P->depth, Pn * 2, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    }
+    P->finalColor = cur;
+    if (P->hdrOut) {
+        hipLaunchKernelGGL(k_hdr_out, dim3((unsigned)((Pn + 255) / 256)), b256, 0, s, (const uint2*)cur, P->hdrOut, Pn);
+        LAUNCH_CHECK();
+    }
+    // ---- PostProcessing (postprocessing.cu:5-161)
+    const int W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16b = (W4 + 3) / 4, H16b = (H4 + 3) / 4, W64 = (W16b + 3) / 4,
+              H64 = (H16b + 3) / 4;
+    if (P->postProcess) {
+        if (P->downScale) {
+            hipLaunchKernelGGL(k_downscale4, dim3((W4 * H4 + 255) / 256), b256, 0, s, (const uint2*)cur, W, H, P->c4, W4, H4);
+            LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_downscale4, dim3((W16b * H16b + 255) / 256), b256, 0, s, (const uint2*)P->c4, W4, H4,
+                               P->c16, W16b, H16b);
+            LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_downscale4, dim3((W64 * H64 + 255) / 256), b256, 0, s, (const uint2*)P->c16, W16b,
+                               H16b, P->c64, W64, H64);
+            LAUNCH_CHECK();
+        }
+        if (P->histogramOn) {
+            hipLaunchKernelGGL(k_histogram, dim3(1), dim3(1024), 0, s, (const uint2*)P->c64, W64, H64, P->histogram);
+            LAUNCH_CHECK();
+        } else if ((e = hipMemsetAsync(P->histogram, 0, 256, s)) != hipSuccess) {
+            return e;
+        }
+        hipLaunchKernelGGL(k_auto_exposure, dim3(1), dim3(64), 0, s, P->exposure, (const uint32_t*)P->histogram,
+                           (float)(W64 * H64), P->deltaTime, P->gain, P->autoExposure, P->fixedExposure);
+        LAUNCH_CHECK();
+    }
+    const dim3 gs((Ws + 15) / 16, (Hs + 15) / 16);
+    hipLaunchKernelGGL(k_bicubic_scale, gs, b256, 0, s, (const uint2*)cur, W, H, P->scaledA, Ws, Hs);
+    LAUNCH_CHECK();
+    DenoisePostParams Q = *P;
+    Q.sharpen = P->postProcess && P->sharpen;
+    Q.tonemap = P->postProcess && P->tonemap;
+    hipLaunchKernelGGL(k_sharpen_tonemap_output, gs, b256, 0, s, Q, (const uint2*)P->scaledA, P->scaledB);
+    LAUNCH_CHECK();
+    P->finalScaled = P->scaledB;
+    return hipSuccess;
+}

@@ -9,6 +9,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <chrono>
 #include <fstream>
 #include <vector>
 
@@ -189,6 +190,24 @@ int rt_frame_init(rt_context* ctx) {
     ALLOC(fr.motion, P * 4);
     ALLOC(fr.rays, P * 4);
     ALLOC(fr.rayCounter, 64);
+    ALLOC(fr.colorB, P * 8);
+    ALLOC(fr.accum, P * 8);
+    ALLOC(fr.histColor, P * 8);
+    ALLOC(fr.histDepth, P * 2);
+    const size_t W = (size_t)ctx->renderW, H = (size_t)ctx->renderH;
+    const size_t W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16 = (W4 + 3) / 4, H16 = (H4 + 3) / 4;
+    ALLOC(fr.noise8, ((W + 7) / 8) * ((H + 7) / 8) * 2);
+    ALLOC(fr.noise16, ((W + 15) / 16) * ((H + 15) / 16) * 2);
+    ALLOC(fr.c4, W4 * H4 * 8);
+    ALLOC(fr.c16, W16 * H16 * 8);
+    ALLOC(fr.c64, ((W16 + 3) / 4) * ((H16 + 3) / 4) * 8);
+    ALLOC(fr.histogram, 256);
+    ALLOC(fr.exposure, 16);
+    const size_t Ps = (size_t)ctx->screenW * ctx->screenH;
+    ALLOC(fr.scaledA, Ps * 8);
+    ALLOC(fr.scaledB, Ps * 8);
+    ALLOC(fr.rgba, Ps * 4);
+    ALLOC(fr.hdr, P * 16);
 #undef ALLOC
     HIP_TRY(ctx, hipMemcpy(fr.solar, g_tables.solar.data(), 1800 * 4, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(fr.limb, g_tables.limb.data(), 60 * 4, hipMemcpyHostToDevice));
@@ -212,6 +231,15 @@ int rt_frame_init(rt_context* ctx) {
     HIP_TRY(ctx, hipMemset(fr.motion, 0, P * 4));
     HIP_TRY(ctx, hipMemset(fr.rays, 0, P * 4));
     HIP_TRY(ctx, hipMemset(fr.rayCounter, 0, 64));
+    HIP_TRY(ctx, hipMemset(fr.colorB, 0, P * 8));
+    HIP_TRY(ctx, hipMemset(fr.accum, 0, P * 8));
+    HIP_TRY(ctx, hipMemset(fr.histColor, 0, P * 8));
+    HIP_TRY(ctx, hipMemset(fr.histDepth, 0, P * 2));
+    HIP_TRY(ctx, hipMemset(fr.histogram, 0, 256));
+    const float exposure0[4] = {1.0f, 1.0f, 1.0f, 1.0f};  // init.cu:331-333
+    HIP_TRY(ctx, hipMemcpy(fr.exposure, exposure0, 16, hipMemcpyHostToDevice));
+    fr.renderColor = fr.color;
+    fr.scaledColor = fr.scaledB;
     fr.ready = true;
     return RT_OK;
 }
@@ -263,6 +291,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.raysOut = with_detail ? fr.rays : nullptr;
     p.rayCounter = fr.rayCounter;
     HIP_TRY(ctx, rtk_launch_pathtrace(&p, ctx->stream));
+    fr.renderColor = fr.color;
     fr.hist = hist_of(hc);  // HistoryCamera::Setup after PathTrace (kernel.cu:357)
     fr.histValid = true;
     ctx->lastFrame = frame_num;
@@ -280,20 +309,103 @@ int rt_get_ray_count(rt_context* ctx, uint64_t* rays, int reset) {
     return RT_OK;
 }
 
+// TemporalSpatialDenoising + PostProcessing + CopyToOutput for the frame just path traced
+int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
+    if (!ctx || frame_num < 1) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_denoise_post before rt_init"; return RT_ERR_STATE; }
+    const rt_render_pass_settings& ps = ctx->params.pass;
+    if (ps.enableBloomEffect || ps.enableLensFlare) {
+        ctx->err = "bloom / lens flare passes are not part of this build (off by default, settingParams.h:96-97)";
+        return RT_ERR_ARG;
+    }
+    if (ps.enablePostProcess && ps.enableToneMapping && ctx->params.post.toneMappingType != 3) {
+        ctx->err = "only the default tone mapper (Reinhard extended, type 3) is built";
+        return RT_ERR_ARG;
+    }
+    FrameResources& fr = ctx->fr;
+    DenoisePostParams p;
+    p.W = (uint32_t)ctx->renderW;
+    p.H = (uint32_t)ctx->renderH;
+    p.Ws = (uint32_t)ctx->screenW;
+    p.Hs = (uint32_t)ctx->screenH;
+    p.frameNum = frame_num;
+    float dt = ctx->deltaMs;
+    if (dt <= 0.0f) {  // wall clock between draws (UpdateFrame's timer, kernel.cu:67-71)
+        const double now = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        dt = fr.lastDrawTime < 0 ? 1000.0f / 60.0f : (float)((now - fr.lastDrawTime) * 1000.0);
+        fr.lastDrawTime = now;
+    }
+    p.deltaTime = dt;
+    p.temporal = ps.enableTemporalDenoising;
+    p.localSpatial = ps.enableLocalSpatialFilter;
+    p.visualize = ps.enableNoiseLevelVisualize;
+    p.wideSpatial = ps.enableWideSpatialFilter;
+    p.temporal2 = ps.enableTemporalDenoising2;
+    p.postProcess = ps.enablePostProcess;
+    p.downScale = ps.enableDownScalePasses;
+    p.histogramOn = ps.enableHistogram;
+    p.autoExposure = ps.enableAutoExposure;
+    p.sharpen = ps.enableSharpening;
+    p.tonemap = ps.enableToneMapping;
+    p.gain = ctx->params.post.gain;
+    p.fixedExposure = ctx->params.post.exposure;
+    p.maxWhite = ctx->params.post.maxWhite;
+    p.gamma = ctx->params.post.gamma;
+    p.dn = ctx->params.denoise;
+    p.colorA = fr.color;
+    p.colorB = fr.colorB;
+    p.normal = fr.normal;
+    p.albedo = fr.albedo;
+    p.depth = fr.depth;
+    p.motion = fr.motion;
+    p.accum = fr.accum;
+    p.histColor = fr.histColor;
+    p.histDepth = fr.histDepth;
+    p.noise8 = fr.noise8;
+    p.noise16 = fr.noise16;
+    p.c4 = fr.c4;
+    p.c16 = fr.c16;
+    p.c64 = fr.c64;
+    p.histogram = fr.histogram;
+    p.exposure = fr.exposure;
+    p.scaledA = fr.scaledA;
+    p.scaledB = fr.scaledB;
+    p.rgba = fr.rgba;
+    p.bluenoise = ctx->dBlueNoise;
+    p.hdrOut = with_hdr ? fr.hdr : nullptr;
+    HIP_TRY(ctx, rtk_denoise_post(&p, ctx->stream));
+    fr.renderColor = p.finalColor;
+    fr.scaledColor = p.finalScaled;
+    return RT_OK;
+}
+
+// RayTracer::draw (kernel.cu:259-398): BVH rebuild, path trace, denoise, post, output
 int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
-    (void)rgba8_out;
-    (void)hdr_out;
     if (!ctx) return RT_ERR_ARG;
-    ctx->err = "rt_draw: denoise/post stages not built in this revision";
-    return RT_ERR_STATE;
+    if (!ctx->inited) { ctx->err = "rt_draw before rt_init"; return RT_ERR_STATE; }
+    const int frame = ctx->nextFrame++;
+    int rc;
+    if ((rc = rt_build_bvh(ctx)) != RT_OK) return rc;
+    if ((rc = rt_path_trace(ctx, frame, 0)) != RT_OK) return rc;
+    if ((rc = rt_denoise_post(ctx, frame, hdr_out != nullptr)) != RT_OK) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (rgba8_out)
+        HIP_TRY(ctx, hipMemcpy(rgba8_out, ctx->fr.rgba, (size_t)ctx->screenW * ctx->screenH * 4, hipMemcpyDeviceToHost));
+    if (hdr_out)
+        HIP_TRY(ctx, hipMemcpy(hdr_out, ctx->fr.hdr, (size_t)ctx->renderW * ctx->renderH * 16, hipMemcpyDeviceToHost));
+    return RT_OK;
 }
 
 size_t rt_buffer_bytes(const rt_context* ctx, int name) {
     if (!ctx) return 0;
     const size_t P = (size_t)ctx->renderW * ctx->renderH;
     switch (name) {
-        case RT_BUF_RENDER_COLOR: case RT_BUF_NORMAL: case RT_BUF_ALBEDO: return P * 8;
-        case RT_BUF_DEPTH: return P * 2;
+        case RT_BUF_RENDER_COLOR: case RT_BUF_NORMAL: case RT_BUF_ALBEDO: case RT_BUF_ACCUMULATION:
+        case RT_BUF_HISTORY_COLOR: return P * 8;
+        case RT_BUF_SCALED_COLOR: return (size_t)ctx->screenW * ctx->screenH * 8;
+        case RT_BUF_DEPTH: case RT_BUF_HISTORY_DEPTH: return P * 2;
+        case RT_BUF_NOISE_LEVEL: return (size_t)((ctx->renderW + 7) / 8) * ((ctx->renderH + 7) / 8) * 2;
+        case RT_BUF_NOISE_LEVEL16: return (size_t)((ctx->renderW + 15) / 16) * ((ctx->renderH + 15) / 16) * 2;
         case RT_BUF_MOTION: return P * 4;
         case RT_BUF_SKY: return (size_t)kSkySize * 16;
         case RT_BUF_SUN: return (size_t)kSunSize * 16;
@@ -308,7 +420,13 @@ int rt_get_buffer(const rt_context* cctx, int name, void* dst, size_t bytes) {
     const FrameResources& fr = ctx->fr;
     const void* src = nullptr;
     switch (name) {
-        case RT_BUF_RENDER_COLOR: src = fr.color; break;
+        case RT_BUF_RENDER_COLOR: src = fr.renderColor; break;
+        case RT_BUF_ACCUMULATION: src = fr.accum; break;
+        case RT_BUF_HISTORY_COLOR: src = fr.histColor; break;
+        case RT_BUF_HISTORY_DEPTH: src = fr.histDepth; break;
+        case RT_BUF_SCALED_COLOR: src = fr.scaledColor; break;
+        case RT_BUF_NOISE_LEVEL: src = fr.noise8; break;
+        case RT_BUF_NOISE_LEVEL16: src = fr.noise16; break;
         case RT_BUF_NORMAL: src = fr.normal; break;
         case RT_BUF_ALBEDO: src = fr.albedo; break;
         case RT_BUF_DEPTH: src = fr.depth; break;

@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "bvh_kernels.h"
+#include "rtx_amd.h"
 
 constexpr int kSkyW = 512, kSkyH = 256, kSkySize = kSkyW * kSkyH;  // kernel.cuh SKY_WIDTH/HEIGHT
 constexpr int kSunW = 32, kSunH = 32, kSunSize = kSunW * kSunH;    // SUN_WIDTH/HEIGHT
@@ -77,6 +78,43 @@ struct PathTraceParams {
     uint32_t* raysOut;          // optional [W*H] RaySceneIntersect calls that traced
     unsigned long long* rayCounter;  // optional: total traced rays (one atomic per workgroup)
 };
+
+// TemporalSpatialDenoising + PostProcessing + CopyToOutput (denoise.hip)
+struct DenoisePostParams {
+    uint32_t W, H;              // render size
+    uint32_t Ws, Hs;            // screen size
+    int frameNum;
+    float deltaTime;            // ms
+    int temporal, localSpatial, visualize, wideSpatial, temporal2;   // RenderPassSettings
+    int postProcess, downScale, histogramOn, autoExposure, sharpen, tonemap;
+    float gain, fixedExposure, maxWhite, gamma;                      // PostProcessParams
+    rt_denoising_params dn;
+    uint2* colorA;              // path-trace colour in; ping-pong pair
+    uint2* colorB;
+    uint2* normal;              // written only by the noise-visualize debug pass
+    const uint2* albedo;
+    uint16_t* depth;            // written only by the noise-visualize debug pass
+    const uint32_t* motion;
+    uint2* accum;               // AccumulationColorBuffer
+    uint2* histColor;           // HistoryColorBuffer
+    uint16_t* histDepth;        // HistoryDepthBuffer
+    uint16_t* noise8;
+    uint16_t* noise16;
+    uint2* c4;
+    uint2* c16;
+    uint2* c64;
+    uint32_t* histogram;        // [64]
+    float* exposure;            // [4], persistent
+    uint2* scaledA;             // screen-size pair
+    uint2* scaledB;
+    uint32_t* rgba;             // screen-size RGBA8
+    const uint8_t* bluenoise;
+    float4* hdrOut;             // optional render-size float4 copy of the denoised HDR colour
+    uint2* finalColor;          // out: buffer holding RenderColorBuffer after denoising
+    uint2* finalScaled;         // out: buffer holding ScaledColorBuffer after tone mapping
+};
+
+extern "C" hipError_t rtk_denoise_post(DenoisePostParams* p, hipStream_t stream);
 
 extern "C" hipError_t rtk_launch_sky(const SkyGenParams* p, hipStream_t stream);
 extern "C" hipError_t rtk_launch_scan(const float* in, float* out, float* sums, int size, int blockSize,

@@ -223,6 +223,7 @@ RT_HD float rt_expf(float x) { return (float)rtm::expd((double)x); }
 RT_HD float rt_exp2f(float x) { return (float)rtm::exp2d((double)x); }
 RT_HD float rt_logf(float x) { return (float)rtm::logd((double)x); }
 RT_HD float rt_log2f(float x) { return (float)rtm::log2d((double)x); }
+RT_HD float rt_log10f(float x) { return (float)(rtm::logd((double)x) * 0.43429448190325182765); }
 RT_HD float rt_sinf(float x) { double s, c; rtm::sincosd((double)x, s, c); return (float)s; }
 RT_HD float rt_cosf(float x) { double s, c; rtm::sincosd((double)x, s, c); return (float)c; }
 RT_HD void rt_sincosf(float x, float* s, float* c) {

@@ -24,7 +24,8 @@ ERRORS = {-1: "RT_ERR_ARG", -2: "RT_ERR_HIP", -3: "RT_ERR_IO", -4: "RT_ERR_STATE
 ARR = dict(VERTICES=0, INDICES=1, NORMALS=2, TRI_POS=3, AABBS=4, MORTON=5, REORDER=6, NODES=7, TLAS_AABBS=8,
            TLAS_MORTON=9, TLAS_REORDER=10, TLAS_NODES=11, TLAS_SCENE_AABB=12, BATCH_SCENE_AABBS=13, HITS=14,
            HIT_NORMALS=15, HIT_FAKE_NORMALS=16, HIT_STATS=17, TRI_NRM=18, RAYS=19, SKY_PDF=20, SKY_CDF=21,
-           SUN_PDF=22, SUN_CDF=23, SUN_DIR=24)
+           SUN_PDF=22, SUN_CDF=23, SUN_DIR=24, HISTOGRAM=25, EXPOSURE=26, COLOR4=27, COLOR16=28, COLOR64=29,
+           RGBA8=30)
 # rt_buffer_name (Buffer2DName, kernel.cuh:286-315)
 BUF = dict(RENDER_COLOR=0, ACCUMULATION=1, HISTORY_COLOR=2, SCALED_COLOR=3, NORMAL=10, DEPTH=11, HISTORY_DEPTH=12,
            MOTION=13, NOISE_LEVEL=14, NOISE_LEVEL16=15, SKY=16, SUN=17, ALBEDO=18)
@@ -99,6 +100,7 @@ SIGNATURES = {
     "rt_get_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     "rt_buffer_bytes": (C.c_size_t, [C.c_void_p, C.c_int]),
     "rt_path_trace": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "rt_denoise_post": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "rt_get_ray_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "rt_build_bvh": (C.c_int, [C.c_void_p]),
     "rt_trace_primary": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
@@ -132,13 +134,13 @@ class RtError(RuntimeError):
 
 
 def write_config(path: str, width: int, height: int, dynamic: bool = False, chunk_dim: int = 1, spp: int = 1,
-                 extra: str = "") -> str:
+                 extra: str = "", max_size=(3840, 2160)) -> str:
     """Write a config.toml with the reference's three tables (resources/config.toml) + extensions."""
     with open(path, "w") as f:
         f.write("[resolution]\nwidth = %d\nheight = %d\n\n" % (width, height))
         f.write("[file]\nloadCameraAtInit = false\n\n")
-        f.write("[optimziation]\nuseDynamicResolution = %s\ntargetFps = 60.0\nmaxWidth = 3840\nmaxHeight = 2160\n"
-                "minWidth = 640\nminHeight = 480\n\n" % ("true" if dynamic else "false"))
+        f.write("[optimziation]\nuseDynamicResolution = %s\ntargetFps = 60.0\nmaxWidth = %d\nmaxHeight = %d\n"
+                "minWidth = 640\nminHeight = 480\n\n" % ("true" if dynamic else "false", max_size[0], max_size[1]))
         f.write("[scene]\nchunkDim = %d\n\n[render]\nspp = %d\n" % (chunk_dim, spp))
         f.write(extra)
     return path
@@ -219,6 +221,9 @@ class RayTracer:
 
     def path_trace(self, frame_num: int = 1, detail: bool = False):
         self._check(self.lib.rt_path_trace(self.h, frame_num, 1 if detail else 0), "rt_path_trace")
+
+    def denoise_post(self, frame_num: int, hdr: bool = False):
+        self._check(self.lib.rt_denoise_post(self.h, frame_num, 1 if hdr else 0), "rt_denoise_post")
 
     def ray_count(self, reset: bool = False) -> int:
         v = C.c_uint64()

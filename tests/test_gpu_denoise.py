@@ -1,0 +1,137 @@
+"""GPU denoiser + post-processing (denoising.cu, postprocessing.cu, CopyToOutput) vs the oracle.
+
+Multi-frame sequences with a moving camera exercise the temporal passes (reprojection through
+the motion vectors, history clamping, accumulation/history buffers); every intermediate the
+C-ABI exposes is compared bit-exactly: noise tiles, denoised HDR colour, history buffers,
+DownScale4 chain, luminance histogram, the persistent exposure state, the tone-mapped screen
+image and the dithered RGBA8 output.
+"""
+import numpy as np
+import pytest
+
+from test_gpu_pathtrace import make_rt, terrain_camera
+
+pytestmark = pytest.mark.gpu
+
+DT = 16.667
+
+
+def cams(rtx, oracle, w, h, n):
+    return [terrain_camera(rtx, oracle, w, h, pos=(8.0 + 0.15 * k, 15.0, -6.0 + 0.1 * k), yaw=0.02 * k,
+                           pitch=-0.7 + 0.01 * k) for k in range(n)]
+
+
+def gpu_state(rt, w, h, ws, hs):
+    g = dict(color=rt.get_buffer("RENDER_COLOR", (w * h, 4), np.uint16),
+             accum=rt.get_buffer("ACCUMULATION", (w * h, 4), np.uint16),
+             hist_color=rt.get_buffer("HISTORY_COLOR", (w * h, 4), np.uint16),
+             hist_depth=rt.get_buffer("HISTORY_DEPTH", (w * h,), np.uint16),
+             noise8=rt.get_buffer("NOISE_LEVEL", dtype=np.uint16),
+             noise16=rt.get_buffer("NOISE_LEVEL16", dtype=np.uint16),
+             scaled=rt.get_buffer("SCALED_COLOR", (ws * hs, 4), np.uint16),
+             c4=rt.download("COLOR4", np.uint16).reshape(-1, 4), c16=rt.download("COLOR16", np.uint16).reshape(-1, 4),
+             c64=rt.download("COLOR64", np.uint16).reshape(-1, 4), histogram=rt.download("HISTOGRAM", np.uint32),
+             exposure=rt.download("EXPOSURE", np.float32), rgba=rt.download("RGBA8", np.uint8).reshape(-1, 4))
+    return g
+
+
+def assert_state(g, o, dn):
+    pairs = [("color", o["color"]), ("accum", dn.accum), ("hist_color", dn.hist_color),
+             ("hist_depth", dn.hist_depth), ("noise8", o["noise8"]), ("noise16", o["noise16"]),
+             ("scaled", o["scaled"]), ("c4", o["c4"]), ("c16", o["c16"]), ("c64", o["c64"]),
+             ("histogram", o["histogram"]), ("rgba", o["rgba"])]
+    for k, ref in pairs:
+        a = g[k]
+        assert a.shape == ref.shape, (k, a.shape, ref.shape)
+        bad = np.nonzero((a != ref).reshape(a.shape[0], -1).any(axis=1))[0]
+        assert bad.size == 0, "%s differs at %d entries, first %s: gpu %s oracle %s" % (
+            k, bad.size, bad[:5], a[bad[:2]], ref[bad[:2]])
+    assert np.array_equal(g["exposure"].view(np.uint32), o["exposure"].view(np.uint32)), (g["exposure"], o["exposure"])
+
+
+def run_sequence(rtx, oracle, tmp_path, default_scene, w, h, frames, spp=1, extra="", params_fn=None, ws=None,
+                 hs=None, dynamic=False):
+    ws, hs = ws or w, hs or h
+    s, tex = oracle.sky(), oracle.textures()
+    if dynamic:
+        cfg = rtx.write_config(str(tmp_path / "c.toml"), ws, hs, dynamic=True, spp=spp, extra=extra,
+                               max_size=(w, h))
+        rt = rtx.RayTracer(ws, hs, cfg).init()
+        rt.build_bvh()
+    else:
+        rt = make_rt(rtx, tmp_path, w, h, spp=spp, extra=extra)
+    rt.set_delta_time(DT)
+    op = oracle.default_params()
+    if params_fn:
+        p = rt.params
+        params_fn(p, op)
+        rt.params = p
+    dn = oracle.Denoiser(w, h, ws, hs)
+    cs = cams(rtx, oracle, w, h, frames)
+    for f in range(1, frames + 1):
+        oc, rc = cs[f - 1]
+        rt.camera = rc
+        rt.build_bvh()
+        rt.path_trace(f)
+        rt.denoise_post(f)
+        rt.sync()
+        g = gpu_state(rt, w, h, ws, hs)
+        hist_cam = cs[f - 2][0] if f > 1 else oc
+        gb = oracle.pathtrace(default_scene["bvh"], w, h, frame_num=f, spp=spp, cam=oc, hist_cam=hist_cam,
+                              sky_out=s, tex=tex)
+        o = dn.draw(gb, f, params=op, delta_time=DT)
+        assert_state(g, o, dn)
+    rt.cleanup()
+    return g
+
+
+def test_denoise_post_sequence(rtx, oracle, tmp_path, default_scene):
+    g = run_sequence(rtx, oracle, tmp_path, default_scene, 160, 96, 3)
+    assert g["rgba"][:, 3].min() == 1
+
+
+def test_denoise_post_odd_size_spp2(rtx, oracle, tmp_path, default_scene):
+    """Sizes that are not multiples of the 8/16/64 tiles (clamped reads at every level)."""
+    run_sequence(rtx, oracle, tmp_path, default_scene, 150, 86, 2, spp=2)
+
+
+def test_denoise_post_settings(rtx, oracle, tmp_path, default_scene):
+    """Fixed exposure, noise-level visualisation and no sharpening."""
+    def tweak(p, op):
+        p.pass_.enableAutoExposure = 0
+        p.pass_.enableNoiseLevelVisualize = 1
+        p.pass_.enableSharpening = 0
+        p.post.exposure = 3.5
+        op.enableAutoExposure = 0
+        op.enableNoiseLevelVisualize = 1
+        op.enableSharpening = 0
+        op.exposure = 3.5
+    run_sequence(rtx, oracle, tmp_path, default_scene, 128, 72, 2, params_fn=tweak)
+
+
+def test_denoise_post_scaled_output(rtx, oracle, tmp_path, default_scene):
+    """Render size != screen size (dynamic-resolution configuration): BicubicScale resamples."""
+    run_sequence(rtx, oracle, tmp_path, default_scene, 192, 108, 2, ws=160, hs=90, dynamic=True)
+
+
+def test_draw_1080p_4spp(rtx, oracle, tmp_path, default_scene):
+    """BASELINE config 3 (1080p, 4 spp, SVGF, tone map) through rt_draw, two frames."""
+    w, h = 1920, 1080
+    cfg = rtx.write_config(str(tmp_path / "c.toml"), w, h, spp=4)
+    rt = rtx.RayTracer(w, h, cfg).init()
+    rt.set_delta_time(DT)
+    (oc1, rc1), (oc2, rc2) = cams(rtx, oracle, w, h, 2)
+    rgba = np.zeros((h, w, 4), np.uint8)
+    hdr = np.zeros((h, w, 4), np.float32)
+    s, tex = oracle.sky(), oracle.textures()
+    dn = oracle.Denoiser(w, h)
+    for f, (oc, rc), hc in ((1, (oc1, rc1), oc1), (2, (oc2, rc2), oc1)):
+        rt.camera = rc
+        rt.draw(rgba, hdr)
+        gb = oracle.pathtrace(default_scene["bvh"], w, h, frame_num=f, spp=4, cam=oc, hist_cam=hc, sky_out=s, tex=tex)
+        o = dn.draw(gb, f, delta_time=DT)
+        assert np.array_equal(rgba.reshape(-1, 4), o["rgba"])
+        ref = o["color"][:, :3].view(np.float16).astype(np.float32)
+        got = hdr.reshape(-1, 4)[:, :3]
+        assert np.array_equal(got, ref)  # bit-exact (the north-star bar is 1e-3 relative L2)
+    rt.cleanup()

@@ -1,17 +1,20 @@
 #!/usr/bin/env python3
-"""Benchmark of the hot path on MI355X; prints ONE JSON line (rank 0).
+"""Benchmark of the per-frame hot path on MI355X; prints ONE JSON line (rank 0).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload primary]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--width 1920 --height 1080 --spp 4]
 
-Workload "primary" = BASELINE config 2 on the default procedural scene: per step one
-per-frame LBVH rebuild (the reference rebuilds every frame, kernel.cu:330-331) plus
-GenerateRay + RaySceneIntersect for every pixel of a 1920x1080 frame (1 spp).  The metric
-is BASELINE.json's: Mray/s (+ ms/frame and the LBVH build ms as extra fields).
+A step is one full frame of BASELINE config 3 on the reference's default procedural scene and
+camera: per-frame two-level LBVH rebuild (kernel.cu:330-331), the path tracer at 4 spp
+(4 reference PathTrace evaluations per pixel), the SVGF-style denoiser and the post chain
+(auto-exposure, scale, sharpen, tone map, dither to RGBA8).  The metric is BASELINE.json's:
+Mray/s (every RaySceneIntersect that ran a traversal: primary, bounce and shadow rays, counted
+on the GPU) with ms/frame and the LBVH build ms as extra fields.
 
-With N ranks (torch.distributed.run, one per GPU) the frame is split into N horizontal
-strips (screen-tile split): each rank traces its rows; no collective sits on
-the data path of this workload.  Timing: barrier + device sync on both sides of exactly K
-steps, max over ranks.
+N ranks (torch.distributed.run, one per GPU): each rank rebuilds the BVH, path traces its
+horizontal strip of the frame, the strips' G-buffers are all-gathered in place over RCCL
+(rtx/dist.py), and every rank runs the denoise/post chain on the full frame (exact vs 1 GPU).
+Total work per frame is fixed as N grows ("strong" scaling).  Timing: barrier + device sync on
+both sides of exactly K frames, max over ranks; value = rays of all ranks / that time.
 """
 import argparse
 import json
@@ -28,43 +31,62 @@ for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (spec peak)
+DELTA_MS = 16.667      # fixed AutoExposure step (SURVEY §8d determinism settings)
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_pathtrace.json")
+
+# algorithmic bytes of one k_pathtrace launch: per traced ray the node and
+# triangle records a traversal must read, per pixel the G-buffer it writes, per diffuse event
+# the 48 texel taps of the triplanar soil textures
+NODE_B, TRI_B, GBUF_B, TEX_B = 64, 48, 30, 48 * 8
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="primary", choices=["primary"])
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the per-stage and 1M-triangle side measurements")
     return ap.parse_args()
 
 
-def cpu_baseline(width, height):
-    """Oracle (CPU restatement) traversal of a bounded sample of the same primary rays."""
+def cpu_baseline(width, height, spp):
+    """Oracle (CPU restatement) path trace of a bounded sample of the same frame."""
     from oracle import oracle as O
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = 16
     v, i, n = O.scene(1)
     bvh = O.build_bvh(v, i, n, O.smooth_normals(v, i))
-    rows = min(height, 540)
-    rays, _ = O.primary_rays(width, height, 1)
-    sample = np.ascontiguousarray(rays[: width * rows])
+    sky, tex = O.sky(), O.textures()
+    rows = min(height, 32)
+    y0 = height // 2 - rows // 2
+    rays = 0
     reps = 0
     t0 = time.perf_counter()
     while True:
-        O.intersect(bvh, sample, threads)
+        g = O.pathtrace(bvh, width, height, frame_num=1 + reps, spp=spp, sky_out=sky, tex=tex, y0=y0, rows=rows,
+                        threads=threads)
+        rays += int(g["rays"].sum(dtype=np.uint64))
         reps += 1
-        if time.perf_counter() - t0 > 10.0 or reps >= 200:
+        if time.perf_counter() - t0 > 10.0 or reps >= 50:
             break
     dt = time.perf_counter() - t0
-    return {"value": round(sample.shape[0] * reps / dt / 1e6, 3), "unit": "Mray/s", "cores": threads,
-            "kind": "port",
-            "sample": "%d x %d primary rays of the 1080p default-camera frame, traversed %d times by the "
-                      "oracle (oracle/traverse.cpp) on %d host threads" % (width, rows, reps, threads)}
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": "%d x %d centre rows of the %dx%d frame at %d spp, path traced %d times by the oracle "
+                      "(oracle/pathtrace.cpp, full PathTrace incl. traversal, textures, sky) on %d host threads"
+                      % (width, rows, width, height, spp, reps, threads)}
+
+
+def pmc_traffic():
+    if not os.path.exists(PMC_FILE):
+        return None, None
+    with open(PMC_FILE) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(PMC_FILE, ROOT)
 
 
 def main():
@@ -73,62 +95,59 @@ def main():
     import torch.distributed as dist
 
     import rtx
+    from rtx.dist import StripGather, strip_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=dev)
 
-    W, H = args.width, args.height
+    W, H, S = args.width, args.height, args.spp
+    y0, rows, _ = strip_rows(H, world, rank)
     tmp = tempfile.mkdtemp(prefix="rtxbench")
-    y0, rows = (H * rank) // world, (H * (rank + 1)) // world - (H * rank) // world
-    cfg = rtx.write_config(os.path.join(tmp, "bench.toml"), W, H, dynamic=False, chunk_dim=1,
+    cfg = rtx.write_config(os.path.join(tmp, "bench.toml"), W, H, dynamic=False, chunk_dim=1, spp=S,
                            extra="stripY0 = %d\nstripRows = %d\n" % (y0, rows))
     rt = rtx.RayTracer(W, H, cfg).init()
+    rt.set_delta_time(DELTA_MS)
+    rt.set_stream(torch.cuda.current_stream(dev).cuda_stream)  # collectives order with the renderer
+    sg = StripGather(W, H, world, rank, dev, rt) if world > 1 else None
 
-    def step(frame):
+    def frame(f):
         rt.build_bvh()
-        rt.trace_primary(frame, detail=False)
+        rt.path_trace(f)
+        if sg is not None:
+            sg.gather()
+        rt.denoise_post(f)
 
     for k in range(args.warmup):
-        step(1 + k)
+        frame(1 + k)
     rt.sync()
+    rt.ray_count(reset=True)
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(1 + k)
-    rt.sync()
+        frame(args.warmup + 1 + k)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
     dt = t1 - t0
+    rays = rt.ray_count()
     if world > 1:
-        tt = torch.tensor([dt], device="cuda", dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        r = torch.tensor([rays], device=dev, dtype=torch.int64)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        rays = int(r.item())
     ms_per_step = dt * 1e3 / args.steps
-    rays_total = W * H * args.steps
-    value = rays_total / dt / 1e6
-
-    # ---- roofline of the dominant kernel (primary traversal), HIP events on the ctx stream
-    rt.trace_primary(1, detail=True)
-    stats = rt.download("HIT_STATS", np.uint32).reshape(-1, 4)[y0 * W:(y0 + rows) * W]
-    visits, tests = int(stats[:, 0].sum(dtype=np.uint64)), int(stats[:, 1].sum(dtype=np.uint64))
-    nrays = W * rows
-    alg_bytes = 24 * nrays + 16 * nrays + 64 * visits + 48 * tests
-    iters = 100
-    ms = rt.time_stage(1, iters) / iters
-    achieved = alg_bytes / (ms * 1e-3) / 1e9
-    build_ms = rt.time_stage(0, 50) / 50
-    info = rt.info()
-    build_bytes = 348 * info.triCount  # BASELINE.md algorithmic bytes per triangle
-    rt.cleanup()
+    value = rays / dt / 1e6
 
     result = {
         "metric": "Mray/s + ms/frame at 1080p 4spp (1/2/4/8 GPU); LBVH build ms",
@@ -142,22 +161,60 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: the reference's default procedural scene (Perlin terrain, 60,800 triangles) "
-                "and default camera",
-        "config": {"workload": "BASELINE config 2: 1920x1080, 1 spp primary rays only + per-frame LBVH rebuild",
-                   "width": W, "height": H, "spp": 1, "parallelism": "screen strips x%d" % world},
-        "lbvh_build_ms": round(build_ms, 5),
-        "lbvh_build_roofline": {"bound": "hbm", "achieved": round(build_bytes / (build_ms * 1e-3) / 1e9, 2),
-                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": round(build_bytes / (build_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
-                                "traffic": None},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                     "kernel": "k_trace_primary", "kernel_ms": round(ms, 5),
-                     "algorithmic_bytes": alg_bytes, "node_visits": visits, "tri_tests": tests},
+        "data": "synthetic: the reference's default procedural scene (Perlin terrain, 60,800 triangles), "
+                "default camera and sky, deterministic stand-in soil textures",
+        "config": {"workload": "BASELINE config 3: %dx%d, %d spp path trace + SVGF denoise + auto-exposure/"
+                               "tone map, per-frame LBVH rebuild" % (W, H, S),
+                   "width": W, "height": H, "spp": S,
+                   "parallelism": "screen strips x%d + RCCL all-gather of G-buffers" % world if world > 1
+                   else "single GPU"},
+        "fps": round(1000.0 / ms_per_step, 2),
+        "rays_per_frame": int(rays // args.steps),
     }
+
+    # ---- roofline of the dominant kernel (k_pathtrace) over this rank's strip
+    rt.path_trace(args.warmup + args.steps + 1, detail=True)
+    st = rt.download("PT_STATS", np.uint32).reshape(-1, 4)[y0 * W:(y0 + rows) * W].astype(np.uint64)
+    n_rays, visits, tests, diffuse = (int(st[:, k].sum()) for k in range(4))
+    alg_bytes = NODE_B * visits + TRI_B * tests + GBUF_B * W * rows + TEX_B * diffuse
+    iters = 20
+    pt_ms = rt.time_stage(2, iters) / iters
+    achieved = alg_bytes / (pt_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic()
+    result["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                          "kernel": "k_pathtrace", "kernel_ms": round(pt_ms, 5), "algorithmic_bytes": alg_bytes,
+                          "rays": n_rays, "node_visits": visits, "tri_tests": tests, "diffuse_events": diffuse}
+    if traffic_src:
+        result["roofline"]["traffic_source"] = traffic_src
+
+    if not args.no_extras:
+        build_ms = rt.time_stage(0, 50) / 50
+        info = rt.info()
+        result["lbvh_build_ms"] = round(build_ms, 5)
+        result["lbvh_build_tris"] = int(info.triCount)
+        result["stage_ms"] = {"lbvh_build": round(build_ms, 5), "path_trace": round(pt_ms, 5),
+                              "denoise_post": round(rt.time_stage(4, 20) / 20, 5),
+                              "primary_rays_1spp": round(rt.time_stage(1, 20) / 20, 5)}
+        result["primary_mray_s"] = round(W * rows / (result["stage_ms"]["primary_rays_1spp"] * 1e-3) / 1e6, 2)
+    rt.cleanup()
+
+    if not args.no_extras and rank == 0:
+        # BASELINE config 4: per-frame rebuild of the ~1M-triangle variant (chunkDim 4)
+        cfg4 = rtx.write_config(os.path.join(tmp, "c4.toml"), 256, 144, chunk_dim=4)
+        r4 = rtx.RayTracer(256, 144, cfg4).init()
+        r4.build_bvh()
+        r4.sync()
+        ms4 = r4.time_stage(0, 30) / 30
+        n4 = r4.info().triCount
+        r4.cleanup()
+        result["lbvh_build_1m"] = {"tris": int(n4), "ms": round(ms4, 5),
+                                   "roofline": {"bound": "hbm", "achieved": round(348 * n4 / (ms4 * 1e-3) / 1e9, 2),
+                                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                                "frac": round(348 * n4 / (ms4 * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                                                "traffic": None}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(W, H)
+        result["cpu_baseline"] = cpu_baseline(W, H, S)
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

@@ -177,6 +177,15 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr);
 /* Traced rays (RaySceneIntersect calls that ran a traversal) accumulated since the last reset. */
 int rt_get_ray_count(rt_context* ctx, uint64_t* rays, int reset);
 
+/* Enqueue every later stage on `stream` (a hipStream_t, e.g. the caller's framework stream so
+ * its collectives order with the renderer); NULL restores the context's own stream. */
+int rt_set_stream(rt_context* ctx, void* stream);
+
+/* Use caller-owned device memory (>= rt_buffer_bytes, 16-B aligned) as one of the path-trace
+ * G-buffers (RT_BUF_RENDER_COLOR / NORMAL / ALBEDO / DEPTH / MOTION), e.g. so a multi-GPU host
+ * can all-gather screen strips in place.  The memory must outlive the context's use of it. */
+int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes);
+
 /* wait for all work on the context stream */
 int rt_sync(rt_context* ctx);
 
@@ -218,7 +227,9 @@ enum rt_array_name {
     RT_ARR_COLOR4 = 27,          /* half4 [ceil(W/4) * ceil(H/4)] DownScale4 chain */
     RT_ARR_COLOR16 = 28,         /* half4 [ceil(W/16) * ceil(H/16)] */
     RT_ARR_COLOR64 = 29,         /* half4 [ceil(W/64) * ceil(H/64)] */
-    RT_ARR_RGBA8 = 30            /* uint8[Ws*Hs][4] final output of the last rt_draw / rt_denoise_post */
+    RT_ARR_RGBA8 = 30,           /* uint8[Ws*Hs][4] final output of the last rt_draw / rt_denoise_post */
+    RT_ARR_PT_STATS = 31         /* uint32[W*H][4] rays, node visits, triangle tests, diffuse events
+                                    (rt_path_trace with_detail) */
 };
 int rt_download(const rt_context* ctx, int what, void* dst, size_t bytes);
 size_t rt_array_bytes(const rt_context* ctx, int what);

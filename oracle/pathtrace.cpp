@@ -117,10 +117,10 @@ static float tex_channel(const uint16_t* tex, int level, int x, int y, int ch) {
     return (float)tex[(off + (size_t)y * n + x) * 4 + ch] / 65535.0f;
 }
 
-static int wrap(int v, int size) {  // BoundaryFuncRepeat (sampler.cuh:313-326)
+static int wrap(int v, int size) {  // BoundaryFuncRepeat (sampler.cuh:313-326) + surface clamp
     if (v >= size) v %= size;
-    if (v < 0) v = size - (-v) % size;
-    return v;
+    if (v < 0) v = size - (-v) % size;  // yields `size` for multiples of -size ...
+    return v < size ? v : size - 1;     // ... which surf2Dread's cudaBoundaryModeClamp clamps
 }
 
 struct F4 { float x, y, z, w; };
@@ -167,6 +167,7 @@ static F4 sample_lod(const uint16_t* tex, F2 uv, float lod) {
 static F3 sky_texel(const float* buf, int x, int y) {  // BoundaryFuncRepeatXClampY, 512x256
     if (x >= 512) x %= 512;
     if (x < 0) x = 512 - (-x) % 512;
+    if (x >= 512) x = 511;
     if (y >= 256) y = 255;
     if (y < 0) y = 0;
     const float* p = buf + ((size_t)y * 512 + x) * 4;

@@ -281,7 +281,8 @@ int rt_init(rt_context* ctx) {
     if (ctx->B >= 1024) { ctx->err = "batch count must stay below 1024 (init.cu:126)"; return RT_ERR_ARG; }
     ctx->nv = (uint32_t)(ctx->mesh.vertices.size() / 3);
 
-    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->ownStream, hipStreamNonBlocking));
+    ctx->stream = ctx->ownStream;
     HIP_TRY(ctx, hipEventCreate(&ctx->ev0));
     HIP_TRY(ctx, hipEventCreate(&ctx->ev1));
 
@@ -350,7 +351,10 @@ void rt_destroy(rt_context* ctx) {
     for (void* p : ctx->allocations) (void)hipFree(p);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->ownStream) {
+        (void)hipStreamSynchronize(ctx->ownStream);
+        (void)hipStreamDestroy(ctx->ownStream);
+    }
     delete ctx;
 }
 
@@ -526,6 +530,7 @@ size_t rt_array_bytes(const rt_context* ctx, int what) {
             return ((w16 + 3) / 4) * ((h16 + 3) / 4) * 8;
         }
         case RT_ARR_RGBA8: return (size_t)ctx->screenW * ctx->screenH * 4;
+        case RT_ARR_PT_STATS: return P * 16;
         default: return 0;
     }
 }
@@ -566,6 +571,7 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
         case RT_ARR_COLOR16: src = ctx->fr.c16; break;
         case RT_ARR_COLOR64: src = ctx->fr.c64; break;
         case RT_ARR_RGBA8: src = ctx->fr.rgba; break;
+        case RT_ARR_PT_STATS: src = ctx->fr.ptStats; break;
         case RT_ARR_SUN_DIR: {
             if (bytes < 16) { ctx->err = "destination too small"; return RT_ERR_ARG; }
             float* o = (float*)dst;

@@ -46,6 +46,7 @@ struct FrameResources {
     uint16_t* depth = nullptr;
     uint32_t* motion = nullptr;
     uint32_t* rays = nullptr;
+    uint4* ptStats = nullptr;
     unsigned long long* rayCounter = nullptr;
     HistCamera hist{};
     bool histValid = false;
@@ -100,7 +101,8 @@ struct rt_context {
     uint32_t B = 0, nv = 0;
 
     // ---- device
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // stream every stage is enqueued on
+    hipStream_t ownStream = nullptr;   // the one rt_init created (destroyed by rt_destroy)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float* dVerts = nullptr;
     float* dNormals = nullptr;

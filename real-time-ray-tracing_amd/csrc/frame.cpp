@@ -189,6 +189,7 @@ int rt_frame_init(rt_context* ctx) {
     ALLOC(fr.depth, P * 2);
     ALLOC(fr.motion, P * 4);
     ALLOC(fr.rays, P * 4);
+    ALLOC(fr.ptStats, P * 16);
     ALLOC(fr.rayCounter, 64);
     ALLOC(fr.colorB, P * 8);
     ALLOC(fr.accum, P * 8);
@@ -230,6 +231,7 @@ int rt_frame_init(rt_context* ctx) {
     HIP_TRY(ctx, hipMemset(fr.depth, 0, P * 2));
     HIP_TRY(ctx, hipMemset(fr.motion, 0, P * 4));
     HIP_TRY(ctx, hipMemset(fr.rays, 0, P * 4));
+    HIP_TRY(ctx, hipMemset(fr.ptStats, 0, P * 16));
     HIP_TRY(ctx, hipMemset(fr.rayCounter, 0, 64));
     HIP_TRY(ctx, hipMemset(fr.colorB, 0, P * 8));
     HIP_TRY(ctx, hipMemset(fr.accum, 0, P * 8));
@@ -289,6 +291,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.depthOut = fr.depth;
     p.motionOut = fr.motion;
     p.raysOut = with_detail ? fr.rays : nullptr;
+    p.statsOut = with_detail ? fr.ptStats : nullptr;
     p.rayCounter = fr.rayCounter;
     HIP_TRY(ctx, rtk_launch_pathtrace(&p, ctx->stream));
     fr.renderColor = fr.color;
@@ -393,6 +396,36 @@ int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
         HIP_TRY(ctx, hipMemcpy(rgba8_out, ctx->fr.rgba, (size_t)ctx->screenW * ctx->screenH * 4, hipMemcpyDeviceToHost));
     if (hdr_out)
         HIP_TRY(ctx, hipMemcpy(hdr_out, ctx->fr.hdr, (size_t)ctx->renderW * ctx->renderH * 16, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_set_stream(rt_context* ctx, void* stream) {
+    if (!ctx) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_set_stream before rt_init"; return RT_ERR_STATE; }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->stream = stream ? (hipStream_t)stream : ctx->ownStream;
+    return RT_OK;
+}
+
+int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
+    if (!ctx || !device_ptr) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_bind_buffer before rt_init"; return RT_ERR_STATE; }
+    const size_t need = rt_buffer_bytes(ctx, name);
+    if (need == 0 || bytes < need) { ctx->err = "rt_bind_buffer: unknown buffer or too small"; return RT_ERR_ARG; }
+    if (((uintptr_t)device_ptr & 15u) != 0) { ctx->err = "rt_bind_buffer: pointer must be 16-byte aligned"; return RT_ERR_ARG; }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    FrameResources& fr = ctx->fr;
+    switch (name) {
+        case RT_BUF_RENDER_COLOR:
+            if (fr.renderColor == fr.color) fr.renderColor = (uint2*)device_ptr;
+            fr.color = (uint2*)device_ptr;
+            break;
+        case RT_BUF_NORMAL: fr.normal = (uint2*)device_ptr; break;
+        case RT_BUF_ALBEDO: fr.albedo = (uint2*)device_ptr; break;
+        case RT_BUF_DEPTH: fr.depth = (uint16_t*)device_ptr; break;
+        case RT_BUF_MOTION: fr.motion = (uint32_t*)device_ptr; break;
+        default: ctx->err = "rt_bind_buffer: only the path-trace G-buffers can be bound"; return RT_ERR_ARG;
+    }
     return RT_OK;
 }
 

@@ -76,6 +76,7 @@ struct PathTraceParams {
     uint16_t* depthOut;         // [W*H] half
     uint32_t* motionOut;        // [W*H] half2
     uint32_t* raysOut;          // optional [W*H] RaySceneIntersect calls that traced
+    uint4* statsOut;            // optional [W*H] rays, node visits, triangle tests, diffuse events
     unsigned long long* rayCounter;  // optional: total traced rays (one atomic per workgroup)
 };
 

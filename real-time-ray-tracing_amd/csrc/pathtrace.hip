@@ -28,7 +28,7 @@ struct Ctx {
     uint32_t* stkA;
     float* stkT;
     F3 sunDir;
-    uint32_t rays;
+    uint32_t rays, visits, tests, diffuse;
 };
 
 RT_DEV void update_material(const Ctx& c, RayState& rs) {
@@ -58,6 +58,8 @@ RT_DEV void scene_intersect(Ctx& c, RayState& rs) {
     ++c.rays;
     HitInfo h;
     intersect(c.sc, rs.orig, rs.dir, c.stkA, c.stkT, 256, h);
+    c.visits += h.visits;
+    c.tests += h.tests;
     rs.offset = h.offset;
     rs.objectIdx = h.objectIdx;
     rs.pos = h.pos;
@@ -124,6 +126,7 @@ RT_DEV void tri_plane(const PathTraceParams& P, F2 uv, float lod, F3 normal, F3 
 RT_DEV void diffuse(Ctx& c, int bounce, RayState& rs, F3& beta, const float r[4], const float r2[4]) {
     if (rs.hitLight || !rs.isDiffuse || rs.isOccluded) return;
     const PathTraceParams& P = c.P;
+    ++c.diffuse;
     rs.isDiffuseRay = true;
     rs.lightIdx = kDefaultLightId;
     rs.isHitProcessed = true;
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(256) void k_pathtrace(PathTraceParams P) {
     uint32_t rays = 0;
     if (active) {
         const int y = (int)P.y0 + yl;
-        Ctx c{P, SceneView{}, stkA + tid, stkT + tid, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), 0u};
+        Ctx c{P, SceneView{}, stkA + tid, stkT + tid, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), 0u, 0u, 0u, 0u};
         c.sc.triPos = P.triPos;
         c.sc.triNrm = P.triNrm;
         c.sc.nodes = (const Node*)P.nodes;
@@ -352,6 +355,7 @@ __global__ __launch_bounds__(256) void k_pathtrace(PathTraceParams P) {
         P.depthOut[p] = rt_f2h(s0.depth);
         P.motionOut[p] = (uint32_t)rt_f2h(s0.motion.x) | ((uint32_t)rt_f2h(s0.motion.y) << 16);
         if (P.raysOut) P.raysOut[p] = c.rays;
+        if (P.statsOut) P.statsOut[p] = make_uint4(c.rays, c.visits, c.tests, c.diffuse);
         rays = c.rays;
     }
     if (P.rayCounter) {

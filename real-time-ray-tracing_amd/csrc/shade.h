@@ -47,10 +47,10 @@ RT_DEV F4 load_u16x4(const uint2* tex, uint32_t texel) {
               (float)(q.y >> 16) / 65535.0f};
 }
 
-RT_DEV int wrap_repeat(int v, int size) {  // BoundaryFuncRepeat
+RT_DEV int wrap_repeat(int v, int size) {  // BoundaryFuncRepeat, then the surface read's clamp
     if (v >= size) v %= size;
-    if (v < 0) v = size - (-v) % size;
-    return v;
+    if (v < 0) v = size - (-v) % size;  // `size` for multiples of -size
+    return v < size ? v : size - 1;
 }
 
 // SampleBicubicSmoothStep<Load2DFuncUshort4<Float4>, Float4, BoundaryFuncRepeat> on one mip level
@@ -154,6 +154,7 @@ RT_DEV F3 bicubic_env(const float4* buf, F2 uv) {
         } else {
             if (x >= kSkyW) x %= kSkyW;
             if (x < 0) x = kSkyW - (-x) % kSkyW;
+            if (x >= kSkyW) x = kSkyW - 1;
             if (y >= kSkyH) y = kSkyH - 1;
             if (y < 0) y = 0;
             c = f3_4(buf[y * kSkyW + x]);

@@ -25,7 +25,7 @@ ARR = dict(VERTICES=0, INDICES=1, NORMALS=2, TRI_POS=3, AABBS=4, MORTON=5, REORD
            TLAS_MORTON=9, TLAS_REORDER=10, TLAS_NODES=11, TLAS_SCENE_AABB=12, BATCH_SCENE_AABBS=13, HITS=14,
            HIT_NORMALS=15, HIT_FAKE_NORMALS=16, HIT_STATS=17, TRI_NRM=18, RAYS=19, SKY_PDF=20, SKY_CDF=21,
            SUN_PDF=22, SUN_CDF=23, SUN_DIR=24, HISTOGRAM=25, EXPOSURE=26, COLOR4=27, COLOR16=28, COLOR64=29,
-           RGBA8=30)
+           RGBA8=30, PT_STATS=31)
 # rt_buffer_name (Buffer2DName, kernel.cuh:286-315)
 BUF = dict(RENDER_COLOR=0, ACCUMULATION=1, HISTORY_COLOR=2, SCALED_COLOR=3, NORMAL=10, DEPTH=11, HISTORY_DEPTH=12,
            MOTION=13, NOISE_LEVEL=14, NOISE_LEVEL16=15, SKY=16, SUN=17, ALBEDO=18)
@@ -101,6 +101,8 @@ SIGNATURES = {
     "rt_buffer_bytes": (C.c_size_t, [C.c_void_p, C.c_int]),
     "rt_path_trace": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "rt_denoise_post": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "rt_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "rt_bind_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     "rt_get_ray_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "rt_build_bvh": (C.c_int, [C.c_void_p]),
     "rt_trace_primary": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
@@ -224,6 +226,15 @@ class RayTracer:
 
     def denoise_post(self, frame_num: int, hdr: bool = False):
         self._check(self.lib.rt_denoise_post(self.h, frame_num, 1 if hdr else 0), "rt_denoise_post")
+
+    def set_stream(self, stream_ptr: int | None):
+        self._check(self.lib.rt_set_stream(self.h, stream_ptr), "rt_set_stream")
+
+    def bind_buffer(self, name: str, device_ptr: int, nbytes: int):
+        self._check(self.lib.rt_bind_buffer(self.h, BUF[name], device_ptr, nbytes), "rt_bind_buffer")
+
+    def buffer_bytes(self, name: str) -> int:
+        return self.lib.rt_buffer_bytes(self.h, BUF[name])
 
     def ray_count(self, reset: bool = False) -> int:
         v = C.c_uint64()

@@ -1,0 +1,86 @@
+"""Screen-strip split + all-gather (rtx/dist.py) on CPU with the gloo backend, world size 2 and 3.
+
+Each rank path traces its strip with the oracle (standing in for the GPU kernel, which is
+pinned bit-exact to the oracle by the gpu tests), writes it into its chunk of the flat
+G-buffer tensors, and all-gathers; every rank must then hold the full single-process frame.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from rtx.dist import GBUFFERS, StripGather, strip_rows
+
+W, H = 48, 30
+ORACLE_KEYS = dict(RENDER_COLOR="color", NORMAL="normal", ALBEDO="albedo", DEPTH="depth", MOTION="motion")
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def camera(O):
+    c = O.default_camera(W, H)
+    c.pos[:] = (8.0, 15.0, -6.0)
+    c.pitch = -0.7
+    return c
+
+
+def worker(rank, world, port, result_dir):
+    import torch
+    import torch.distributed as dist
+
+    from oracle import oracle as O
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        v, i, n = O.scene(1)
+        bvh = O.build_bvh(v, i, n, O.smooth_normals(v, i))
+        sg = StripGather(W, H, world, rank, torch.device("cpu"))
+        g = O.pathtrace(bvh, W, H, frame_num=2, cam=camera(O), y0=sg.y0, rows=sg.rows, threads=1)
+        for name, bpp in GBUFFERS:
+            a = np.ascontiguousarray(g[ORACLE_KEYS[name]]).view(np.uint8).reshape(-1)
+            lo, hi = sg.y0 * W * bpp, (sg.y0 + sg.rows) * W * bpp
+            sg.tensors[name][lo:hi] = torch.from_numpy(a[lo:hi].copy())
+        sg.gather()
+        out = {name: sg.tensors[name][:W * H * bpp].numpy().copy() for name, bpp in GBUFFERS}
+        np.savez(os.path.join(result_dir, "rank%d.npz" % rank), **out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_strip_allgather_matches_full_frame(tmp_path, world, oracle):
+    import torch.multiprocessing as mp
+
+    mp.spawn(worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    v, i, n = oracle.scene(1)
+    bvh = oracle.build_bvh(v, i, n, oracle.smooth_normals(v, i))
+    full = oracle.pathtrace(bvh, W, H, frame_num=2, cam=camera(oracle), threads=1)
+    for r in range(world):
+        got = np.load(os.path.join(str(tmp_path), "rank%d.npz" % r))
+        for name, _ in GBUFFERS:
+            ref = np.ascontiguousarray(full[ORACLE_KEYS[name]]).view(np.uint8).reshape(-1)
+            assert np.array_equal(got[name], ref), (r, name)
+
+
+@pytest.mark.parametrize("h,world", [(1080, 1), (1080, 2), (1080, 8), (1081, 8), (2160, 8), (30, 3)])
+def test_strip_rows_cover_frame(h, world):
+    covered = np.zeros(h, np.int32)
+    for r in range(world):
+        y0, rows, per = strip_rows(h, world, r)
+        assert rows >= 1 and rows <= per and y0 == r * per
+        covered[y0:y0 + rows] += 1
+    assert (covered == 1).all()
+
+
+def test_strip_rows_rejects_too_many_ranks():
+    with pytest.raises(ValueError):
+        strip_rows(10, 8, 7)

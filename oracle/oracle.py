@@ -213,6 +213,8 @@ def _bind_frame_api(L):
     L.orc_pathtrace.argtypes = [C.POINTER(Frame), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                 C.POINTER(GBuffer), C.c_int]
     L.orc_pathtrace.restype = None
+    L.orc_sky_radiance.argtypes = [C.POINTER(SkyTables), C.c_float, C.c_float, C.c_void_p, C.c_void_p]
+    L.orc_sky_radiance.restype = None
     L.orc_denoise_post.argtypes = [C.c_void_p]
     L.orc_denoise_post.restype = C.c_int
 
@@ -244,6 +246,16 @@ def sky(params: dict | None = None) -> dict:
     out["sun_dir"] = np.array(so.sunDir[:], np.float32)
     out["sun_area"] = np.float32(so.sunArea)
     out["cos_theta_max"] = np.float32(so.sunAngleCosThetaMax)
+    return out
+
+
+def sky_radiance(direction, time_of_day: float = 0.25, sun_axis_angle: float = 45.0) -> np.ndarray:
+    """GetSkyRadiance before skyScalar for one direction (sky.cuh:165-197)."""
+    t = sky_tables()
+    tabs = SkyTables(*[a.ctypes.data for a in t])
+    d = np.ascontiguousarray(direction, np.float32)
+    out = np.zeros(3, np.float32)
+    lib().orc_sky_radiance(C.byref(tabs), time_of_day, sun_axis_angle, d.ctypes.data, out.ctypes.data)
     return out
 
 

@@ -261,3 +261,22 @@ extern "C" void orc_sky(const OrcSkyTables* tables, const OrcSkyParams* params, 
     out->sunArea = rt_powf(rt_tanf(sunRadiusRadian), 2.0f) * kPi;
     out->sunAngleCosThetaMax = rt_cosf(sunRadiusRadian);
 }
+
+// Probe: GetSkyRadiance (unscaled) for one direction at the sun position of (timeOfDay,
+// sunAxisAngle) — pins the sky model against SURVEY.md §8c's reference run (zenith).
+extern "C" void orc_sky_radiance(const OrcSkyTables* tables, float timeOfDay, float sunAxisAngle, const float* dir,
+                                 float* out) {
+    F3 sunDir = sun_direction(timeOfDay, sunAxisAngle);
+    SkyState st;
+    sky_state(sunDir, *tables, st);
+    F3 c = sky_radiance(f3(dir[0], dir[1], dir[2]), sunDir, st);
+    out[0] = c.x; out[1] = c.y; out[2] = c.z;
+}
+
+extern "C" void orc_sky_radiance_sun(const OrcSkyTables* tables, const float* sun, const float* dir, float* out) {
+    F3 sunDir = f3(sun[0], sun[1], sun[2]);
+    SkyState st;
+    sky_state(sunDir, *tables, st);
+    F3 c = sky_radiance(f3(dir[0], dir[1], dir[2]), sunDir, st);
+    out[0] = c.x; out[1] = c.y; out[2] = c.z;
+}

@@ -228,6 +228,10 @@ enum rt_array_name {
     RT_ARR_COLOR16 = 28,         /* half4 [ceil(W/16) * ceil(H/16)] */
     RT_ARR_COLOR64 = 29,         /* half4 [ceil(W/64) * ceil(H/64)] */
     RT_ARR_RGBA8 = 30,           /* uint8[Ws*Hs][4] final output of the last rt_draw / rt_denoise_post */
+    RT_ARR_PT_QUEUE = 32,        /* uint32[64] path-trace wavefront counters of the last launch: [0] rays
+                                    deferred at step 3, [1] at step 4, [4] pixels resolved late,
+                                    [8]/[9] longest traversal (iterations) of the step-3/4 queues
+                                    (detail launches only) */
     RT_ARR_PT_STATS = 31         /* uint32[W*H][4] rays, node visits, triangle tests, diffuse events
                                     (rt_path_trace with_detail) */
 };

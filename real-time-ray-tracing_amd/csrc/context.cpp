@@ -531,6 +531,7 @@ size_t rt_array_bytes(const rt_context* ctx, int what) {
         }
         case RT_ARR_RGBA8: return (size_t)ctx->screenW * ctx->screenH * 4;
         case RT_ARR_PT_STATS: return P * 16;
+        case RT_ARR_PT_QUEUE: return 64 * 4;
         default: return 0;
     }
 }
@@ -572,6 +573,7 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
         case RT_ARR_COLOR64: src = ctx->fr.c64; break;
         case RT_ARR_RGBA8: src = ctx->fr.rgba; break;
         case RT_ARR_PT_STATS: src = ctx->fr.ptStats; break;
+        case RT_ARR_PT_QUEUE: src = ctx->fr.ws.counters; break;
         case RT_ARR_SUN_DIR: {
             if (bytes < 16) { ctx->err = "destination too small"; return RT_ERR_ARG; }
             float* o = (float*)dst;

@@ -48,6 +48,7 @@ struct FrameResources {
     uint32_t* rays = nullptr;
     uint4* ptStats = nullptr;
     unsigned long long* rayCounter = nullptr;
+    PtWorkspace ws{};              // wavefront queues of the path tracer (pathtrace.hip)
     HistCamera hist{};
     bool histValid = false;
     // denoise + post (denoising.cu, postprocessing.cu)

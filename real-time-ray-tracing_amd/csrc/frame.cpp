@@ -191,6 +191,30 @@ int rt_frame_init(rt_context* ctx) {
     ALLOC(fr.rays, P * 4);
     ALLOC(fr.ptStats, P * 16);
     ALLOC(fr.rayCounter, 64);
+    {  // wavefront workspace: one entry per traced sample of the strip
+        const size_t cap = (size_t)ctx->renderW * ctx->stripRows * ctx->spp;
+        if (cap >= (1ull << 31)) { ctx->err = "strip x spp too large for the path-trace queues"; return RT_ERR_ARG; }
+        PtWorkspace& ws = fr.ws;
+        ws.cap = (uint32_t)cap;
+        for (PtQueue* q : {&ws.q3, &ws.q4}) {
+            ALLOC(q->rayO, cap * 16);
+            ALLOC(q->rayD, cap * 16);
+            ALLOC(q->st0, cap * 16);
+            ALLOC(q->st1, cap * 16);
+            ALLOC(q->st2, cap * 16);
+        }
+        ALLOC(ws.hitRec, cap * 16);
+        ALLOC(ws.hitErr, cap * 4);
+        ALLOC(ws.pathL, cap * 16);
+        ALLOC(ws.pending, (size_t)ctx->renderW * ctx->stripRows * 4);
+        ALLOC(ws.counters, kWsCounterWords * 4);
+        ws.fetch = ws.counters + 64;
+        int dev = 0, cus = 0;
+        HIP_TRY(ctx, hipGetDevice(&dev));
+        HIP_TRY(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        const int perCu = rtk_trace_queue_blocks_per_cu();
+        ws.persistBlocks = (uint32_t)((cus > 0 ? cus : 256) * (perCu > 0 ? perCu : 4));
+    }
     ALLOC(fr.colorB, P * 8);
     ALLOC(fr.accum, P * 8);
     ALLOC(fr.histColor, P * 8);
@@ -293,6 +317,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.raysOut = with_detail ? fr.rays : nullptr;
     p.statsOut = with_detail ? fr.ptStats : nullptr;
     p.rayCounter = fr.rayCounter;
+    p.ws = fr.ws;
     HIP_TRY(ctx, rtk_launch_pathtrace(&p, ctx->stream));
     fr.renderColor = fr.color;
     fr.hist = hist_of(hc);  // HistoryCamera::Setup after PathTrace (kernel.cu:357)

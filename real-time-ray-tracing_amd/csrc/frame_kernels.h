@@ -46,6 +46,37 @@ struct SkyGenParams {
 
 struct HistCamera { float pos[3], left[3], up[3], dir[3]; };  // HistoryCamera (kernel.cuh:135-155)
 
+// One queue of deferred rays (wavefront path tracing).  Entry i is five float4
+// planes: the ray (orig + pixel index, dir + flags) that k_trace_queue reads, and the path
+// state the resume kernel needs after the hit.
+//   rayO  = orig.xyz, pixel index (bits)            rayD = dir.xyz, flags (bits, kQFlag*)
+//   st0   = albedo.xyz, rayConeWidth                 st1  = beta1.xyz, rayConeSpread
+//   st2   = beta0.xyz, 0
+struct PtQueue {
+    float4* rayO;
+    float4* rayD;
+    float4* st0;
+    float4* st1;
+    float4* st2;
+};
+
+// counters[] slots (zeroed before every path-trace launch sequence)
+enum PtCounter : int { kCntQ3 = 0, kCntQ4 = 1, kCntFetch3 = 2, kCntFetch4 = 3, kCntPending = 4, kCntResume3 = 5,
+                       kCntResume4 = 6, kCntResolve = 7, kCntMaxIter3 = 8, kCntMaxIter4 = 9, kCntSlots = 10 };
+constexpr int kWsCounterWords = 64 + 2 * 8 * 16;  // counters | fetch, zeroed together
+
+struct PtWorkspace {
+    PtQueue q3, q4;             // rays deferred at step 3 / step 4 of PathTrace's sequence
+    float4* hitRec;             // [cap] (t, triangle index bits, u, v) of the closest hit
+    float* hitErr;              // [cap] its errorT
+    float4* pathL;              // [rows*W*spp] per-sample radiance of pixels resolved late
+    uint32_t* pending;          // [rows*W] pixel (strip-local) | first deferred sample << 26
+    uint32_t* counters;         // [kCntSlots]
+    uint32_t* fetch;            // [2][8 parts x 16]: k_trace_queue fetch counters, 64 B apart
+    uint32_t cap;               // entries per queue (= rows * W * spp)
+    uint32_t persistBlocks;     // grid of the persistent queue kernels
+};
+
 struct PathTraceParams {
     TraceCamera cam;
     float tanHalfFov[2];
@@ -78,6 +109,7 @@ struct PathTraceParams {
     uint32_t* raysOut;          // optional [W*H] RaySceneIntersect calls that traced
     uint4* statsOut;            // optional [W*H] rays, node visits, triangle tests, diffuse events
     unsigned long long* rayCounter;  // optional: total traced rays (one atomic per workgroup)
+    PtWorkspace ws;
 };
 
 // TemporalSpatialDenoising + PostProcessing + CopyToOutput (denoise.hip)
@@ -121,3 +153,4 @@ extern "C" hipError_t rtk_launch_sky(const SkyGenParams* p, hipStream_t stream);
 extern "C" hipError_t rtk_launch_scan(const float* in, float* out, float* sums, int size, int blockSize,
                                       hipStream_t stream);
 extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream);
+extern "C" int rtk_trace_queue_blocks_per_cu();

@@ -1,11 +1,23 @@
-// pathtrace.hip — the per-pixel path tracer (PathTrace, pathtrace.cuh:11-128) for gfx950.
+// pathtrace.hip — the per-pixel path tracer (PathTrace, pathtrace.cuh:11-128) for gfx950,
+// run as a wavefront pipeline:
 //
-// One thread per pixel; a 256-thread workgroup covers 16x16 pixels and each wave64 an 8x8
-// tile so primary rays stay coherent.  The three RaySceneIntersect calls per path share one
-// 16-entry LDS stack column per thread (32 KB / workgroup).  With spp > 1 the thread loops
-// over its samples (frame index spp*(frameNum-1)+1+s) and averages demodulated colour and
-// albedo in fp32 before the half store; the other G-buffers come from sample 0.
-// Traced-ray totals are reduced per workgroup and added with one 64-bit atomic.
+//   k_pt_primary    one thread per pixel, looping over its samples: blue noise, GenerateRay,
+//                   the steps I0 G0 I1 G1 I2 G2 D0 of the reference's straight-line sequence
+//                   with the (coherent) primary traversal inline.  A sample whose next step is
+//                   an intersection (I3: the BSDF bounce or the shadow ray) is appended to
+//                   queue 3 with the state the rest of the path needs; every other sample is
+//                   finished here.
+//   k_trace_queue   (trace_queue.hip) traces a queue with persistent, refilling waves.
+//   k_pt_resume<3>  applies the I3 hit, runs G3 D1 and appends the I4 rays to queue 4.
+//   k_trace_queue   traces queue 4.
+//   k_pt_resume<4>  applies the I4 hit and finishes those samples.
+//   k_pt_resolve    averages the samples of the pixels that had a deferred sample.
+//
+// Every step runs the same code as the reference's sequence, in the same order per sample, so
+// the G-buffers are bit-identical to the single-kernel evaluation (and to the CPU oracle).
+// With spp > 1 sample s uses frame index spp*(frameNum-1)+1+s and the demodulated colour and
+// albedo are averaged in fp32, in sample order, before the half store;
+// the other G-buffers come from sample 0.
 #include "frame_kernels.h"
 #include "pt_common.h"
 #include "shade.h"
@@ -15,29 +27,47 @@ using namespace rtd;
 
 namespace {
 
+// queue-entry flags (PtQueue rayD.w)
+constexpr uint32_t kQShadow = 1u;          // isShadowRay
+constexpr int kQSampleShift = 1;           // sample index s (6 bits, spp <= 64)
+constexpr int kQLightShift = 16;           // lightIdx (16 bits: 7777 or 9999)
+
 struct RayState {
     F3 orig, dir, pos, normal, fakeNormal, albedo, centerRaydir;
     int matId, matType, lightIdx, objectIdx;
-    bool isRayIntoSurface, hitLight, hit, isDiffuseRay, isDiffuse, isHitProcessed, isOccluded, isShadowRay;
+    bool isRayIntoSurface, hitLight, hit, isDiffuse, isHitProcessed, isOccluded, isShadowRay;
     float offset, normalDotRayDir, depth, rayConeWidth, rayConeSpread;
 };
 
-struct Ctx {
+struct PathCtx {
     const PathTraceParams& P;
-    SceneView sc;
-    uint32_t* stkA;
-    float* stkT;
     F3 sunDir;
+    const uint32_t* sob;   // LDS copy of sobol dims 0..3
+    BnPixel bp;
+    int frameIdx;
     uint32_t rays, visits, tests, diffuse;
 };
 
-RT_DEV void update_material(const Ctx& c, RayState& rs) {
+// blue-noise sample (frameIdx * 4 + k, dim d) of this pixel (pathtrace.cuh:116-129)
+RT_DEV float rnd(const PathCtx& c, int k, int d) { return bn_value(c.sob, c.bp, c.frameIdx * 4 + k, d); }
+
+struct PathVars {
+    RayState rs;
+    F3 beta0, beta1;
+    // sample-0 G-buffer values, set by steps 0 and 2 (always run in k_pt_primary)
+    float outDepth;
+    uint32_t mask;
+    F2 mv, sampleUv;
+    F3 outNormal;
+};
+
+RT_DEV void update_material(const PathTraceParams& P, RayState& rs) {
     if (!rs.hit) {
         rs.matType = MAT_SKY;
         rs.matId = 99999;
     } else {
-        if (c.P.materialOverride >= 0) rs.matId = c.P.materialOverride;
-        else rs.matId = (rs.objectIdx >= 0 && rs.objectIdx < (int)c.P.triCount) ? 3 : 6;  // SAFE_LOAD(.., 6)
+        if (P.materialOverride >= 0) rs.matId = P.materialOverride;
+        else rs.matId = (rs.objectIdx >= 0 && rs.objectIdx < (int)P.triCount) ? 3 : 6;  // SAFE_LOAD(.., 6)
         rs.matType = (rs.matId >= 0 && rs.matId < 10) ? mat_type(rs.matId) : PERFECT_REFLECTION;
     }
     if (rs.isShadowRay) {
@@ -51,15 +81,12 @@ RT_DEV void update_material(const Ctx& c, RayState& rs) {
     rs.isDiffuse = (rs.matType == LAMBERTIAN) || (rs.matType == MICROFACET);
 }
 
-// RaySceneIntersect (traverse.cuh:64-225)
-RT_DEV void scene_intersect(Ctx& c, RayState& rs) {
-    if (rs.hitLight || !rs.isHitProcessed || rs.isOccluded) return;
+// RaySceneIntersect (traverse.cuh:64-225): does this step trace?
+RT_DEV bool needs_trace(const RayState& rs) { return !(rs.hitLight || !rs.isHitProcessed || rs.isOccluded); }
+
+// ... and what it does with the hit
+RT_DEV void apply_hit(const PathTraceParams& P, RayState& rs, const HitInfo& h) {
     rs.isHitProcessed = false;
-    ++c.rays;
-    HitInfo h;
-    intersect(c.sc, rs.orig, rs.dir, c.stkA, c.stkT, 256, h);
-    c.visits += h.visits;
-    c.tests += h.tests;
     rs.offset = h.offset;
     rs.objectIdx = h.objectIdx;
     rs.pos = h.pos;
@@ -70,11 +97,11 @@ RT_DEV void scene_intersect(Ctx& c, RayState& rs) {
     rs.hit = h.hit;
     rs.depth = h.t;
     if (rs.hit) rs.rayConeWidth += rs.rayConeSpread * h.t;
-    update_material(c, rs);
+    update_material(P, rs);
 }
 
-// GlossySurfaceInteraction (surfaceInteraction.cuh:11-34, bsdf.cuh:130-165)
-RT_DEV void glossy(RayState& rs, float rnd) {
+// GlossySurfaceInteraction (surfaceInteraction.cuh:11-34, bsdf.cuh:130-165); random number rn[0][k]
+RT_DEV void glossy(const PathCtx& c, RayState& rs, int k) {
     if (rs.hitLight || rs.isDiffuse || rs.isOccluded) return;
     rs.isHitProcessed = true;
     if (rs.matType == PERFECT_REFLECTION) {
@@ -97,7 +124,7 @@ RT_DEV void glossy(RayState& rs, float rnd) {
             const float R1 = etaT * cosI, R2 = etaI * cosT, R3 = etaI * cosI, R4 = etaT * cosT;
             const float Rparl = (R1 - R2) / (R1 + R2), Rperp = (R3 - R4) / (R3 + R4);
             const float fres = (Rparl * Rparl + Rperp * Rperp) / 2.0f;
-            if (rnd < fres) {
+            if (rnd(c, 0, k) < fres) {
                 next = rs.dir - rs.normal * ndr * 2.0f;
             } else {
                 next = eta * rs.dir + (eta * cosI - cosT) * rs.normal;
@@ -122,12 +149,12 @@ RT_DEV void tri_plane(const PathTraceParams& P, F2 uv, float lod, F3 normal, F3 
     nrm = normalize(u * n.x + v * n.y + normal * n.z);
 }
 
-// DiffuseSurfaceInteraction (surfaceInteraction.cuh:36-310)
-RT_DEV void diffuse(Ctx& c, int bounce, RayState& rs, F3& beta, const float r[4], const float r2[4]) {
+// DiffuseSurfaceInteraction (surfaceInteraction.cuh:36-310); random numbers rn[2*bounce] and
+// rn[2*bounce+1]
+RT_DEV void diffuse(PathCtx& c, int bounce, RayState& rs, F3& beta) {
     if (rs.hitLight || !rs.isDiffuse || rs.isOccluded) return;
     const PathTraceParams& P = c.P;
     ++c.diffuse;
-    rs.isDiffuseRay = true;
     rs.lightIdx = kDefaultLightId;
     rs.isHitProcessed = true;
     F3 normal = rs.fakeNormal;
@@ -156,6 +183,12 @@ RT_DEV void diffuse(Ctx& c, int bounce, RayState& rs, F3& beta, const float r[4]
         rs.fakeNormal = normal;
     }
     if (bounce == 0) rs.albedo = albedo * (1.0f + fabsf(dot(normal, rs.centerRaydir)));
+    float r[4], r2[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        r[d] = rnd(c, 2 * bounce, d);
+        r2[d] = rnd(c, 2 * bounce + 1, d);
+    }
     const F3 rayDir = rs.dir;
     F3 lDir;
     float lPdf = 1.0f;
@@ -218,159 +251,345 @@ RT_DEV float ray_cone_width(const PathTraceParams& P, int ix, int iy) {
     return af - an;
 }
 
-struct SampleOut {
-    F3 L2, albedo, normal;
-    float depth;
-    F2 motion;
-    uint32_t mask;
-};
-
-RT_DEV void path_sample(Ctx& c, int x, int y, int frameIdx, SampleOut& o) {
-    const PathTraceParams& P = c.P;
-    RayState rs;
-    F3 beta0 = f3(1.0f), beta1 = f3(1.0f);
-    rs.isDiffuseRay = false;
-    rs.hitLight = false;
-    rs.lightIdx = kDefaultLightId;
-    rs.isHitProcessed = true;
-    rs.isOccluded = false;
-    rs.isShadowRay = false;
-    rs.isDiffuse = false;
-    rs.hit = false;
-    rs.matType = MAT_SKY;
-    rs.matId = 0;
-    rs.objectIdx = -1;
-    rs.normal = f3(0.0f, -1.0f, 0.0f);
-    rs.fakeNormal = f3(0.0f);
-    rs.albedo = f3(1.0f);
-    rs.rayConeWidth = 0.0f;
-    rs.rayConeSpread = ray_cone_width(P, x, y);
-    float rn[4][4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int d = 0; d < 4; ++d) rn[k][d] = bluenoise(P.bluenoise, x, y, frameIdx * 4 + k, d);
-    F2 sampleUv;
-    generate_ray(P.cam, x, y, F2{rn[0][0], rn[0][1]}, F2{rn[0][2], rn[0][3]}, rs.orig, rs.dir, rs.centerRaydir,
-                 sampleUv);
-    // The reference's straight-line sequence (pathtrace.cuh:61-101)
-    //   I G0 I G1 I G2 D0 [normal] I G3 D1 I
-    // as one loop so traversal, glossy and diffuse each have a single call site.
-    float outDepth = 0.0f;
-    uint32_t mask = 0u;
-    F2 mv = {0.0f, 0.0f};
-    F3 outNormal = f3(0.0f);
+// Steps k0..4 of the reference's straight-line sequence (pathtrace.cuh:61-101)
+//   I G0 I G1 I G2 D0 [normal] I G3 D1 I
+// as one loop so traversal, glossy and diffuse each have a single call site.  With `hit`
+// set, step k0's intersection result is *hit (a deferred ray that came back from the queue
+// tracer).  An intersection at a step >= kDeferFrom is not traced here: the step is returned
+// and the caller queues the ray.  Returns 5 when the path is complete.
+template <int kDeferFrom>
+RT_DEV int run_path(PathCtx& c, PathVars& v, int k0, const HitInfo* hit, const SceneView& sc, uint32_t* stkA,
+                    float* stkT) {
+    RayState& rs = v.rs;
 #pragma unroll 1
-    for (int k = 0; k < 5; ++k) {
-        scene_intersect(c, rs);
+    for (int k = k0; k < 5; ++k) {
+        if (k == k0 && hit) {
+            apply_hit(c.P, rs, *hit);
+        } else if (needs_trace(rs)) {
+            if (k >= kDeferFrom) return k;
+            ++c.rays;
+            HitInfo h;
+            intersect(sc, rs.orig, rs.dir, stkA, stkT, 256, h);
+            c.visits += h.visits;
+            c.tests += h.tests;
+            apply_hit(c.P, rs, h);
+        }
         if (k == 0) {
-            outDepth = rs.depth;
-            mask = (uint32_t)rs.matId & 0xFFFFu;
+            v.outDepth = rs.depth;
+            v.mask = (uint32_t)rs.matId & 0xFFFFu;
+            F2 mv = {0.0f, 0.0f};
             if (rs.hit) {  // HistoryCamera::WorldToScreenSpace (kernel.cuh:144-151)
+                const PathTraceParams& P = c.P;
                 const F3 d = rs.pos - load3(P.hist.pos);
-                const F3 v = f3(dot(load3(P.hist.left), d), dot(load3(P.hist.up), d), dot(load3(P.hist.dir), d));
-                const F2 s = {v.x / v.z, v.y / v.z};
+                const F3 q = f3(dot(load3(P.hist.left), d), dot(load3(P.hist.up), d), dot(load3(P.hist.dir), d));
+                const F2 s = {q.x / q.z, q.y / q.z};
                 const F2 ndc = {s.x / P.tanHalfFov[0], s.y / P.tanHalfFov[1]};
-                mv = F2{(0.5f - ndc.x * 0.5f) - sampleUv.x, (0.5f - ndc.y * 0.5f) - sampleUv.y};
+                mv = F2{(0.5f - ndc.x * 0.5f) - v.sampleUv.x, (0.5f - ndc.y * 0.5f) - v.sampleUv.y};
             }
-            mv = F2{mv.x + 0.5f, mv.y + 0.5f};
+            v.mv = F2{mv.x + 0.5f, mv.y + 0.5f};
         }
         if (k == 4) break;
-        glossy(rs, k == 0 ? rn[0][0] : k == 1 ? rn[0][1] : k == 2 ? rn[0][2] : rn[0][3]);
+        glossy(c, rs, k);
         if (k >= 2) {
             const bool first = k == 2;
-            const float r[4] = {first ? rn[0][0] : rn[2][0], first ? rn[0][1] : rn[2][1], first ? rn[0][2] : rn[2][2],
-                                first ? rn[0][3] : rn[2][3]};
-            const float r2[4] = {first ? rn[1][0] : rn[3][0], first ? rn[1][1] : rn[3][1], first ? rn[1][2] : rn[3][2],
-                                 first ? rn[1][3] : rn[3][3]};
             F3 beta = f3(1.0f);
-            diffuse(c, first ? 0 : 1, rs, beta, r, r2);
+            diffuse(c, first ? 0 : 1, rs, beta);
             if (first) {
-                beta1 = beta;
-                outNormal = rs.fakeNormal;
+                v.beta1 = beta;
+                v.outNormal = rs.fakeNormal;
             } else {
-                beta0 = beta;
+                v.beta0 = beta;
             }
         }
     }
+    return 5;
+}
+
+// end of PathTrace (pathtrace.cuh:103-128): the sample's demodulated colour
+RT_DEV F3 finish(const PathCtx& c, const PathVars& v) {
+    const RayState& rs = v.rs;
     F3 L0 = f3(0.0f);
-    if (rs.hitLight && !rs.isOccluded && rs.matType == MAT_SKY) L0 = env_light(P, c.sunDir, rs.dir);
-    F3 L2 = L0 * beta0 * beta1;
+    if (rs.hitLight && !rs.isOccluded && rs.matType == MAT_SKY) L0 = env_light(c.P, c.sunDir, rs.dir);
+    F3 L2 = L0 * v.beta0 * v.beta1;
     if (isnan3(L2)) L2 = f3(0.0f);
-    if (isnan3(outNormal)) outNormal = f3(0.0f);
-    if (outDepth != outDepth) outDepth = 0.0f;
-    if (mv.x != mv.x || mv.y != mv.y) mv = F2{0.0f, 0.0f};
     L2 = f3(clampf(L2.x, 0.0f, 10.0f), clampf(L2.y, 0.0f, 10.0f), clampf(L2.z, 0.0f, 10.0f));
-    o.L2 = L2 / rs.albedo;
-    o.albedo = rs.albedo;
-    o.normal = outNormal;
-    o.depth = outDepth;
-    o.motion = mv;
-    o.mask = mask;
+    return L2 / rs.albedo;
 }
 
 RT_DEV uint2 pack_h4(float a, float b, float c, uint32_t d16) {
     return make_uint2((uint32_t)rt_f2h(a) | ((uint32_t)rt_f2h(b) << 16), (uint32_t)rt_f2h(c) | (d16 << 16));
 }
 
+// wave-aggregated append: one atomic per wave, slots in lane order
+RT_DEV uint32_t wave_append(bool want, uint32_t* counter) {
+    const unsigned long long m = __ballot(want);
+    if (m == 0ull) return 0u;
+    const int lane = (int)__lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0u;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+RT_DEV void enqueue(const PtQueue& q, uint32_t slot, const PathVars& v, uint32_t pixel, uint32_t s) {
+    const RayState& rs = v.rs;
+    const uint32_t flags = (rs.isShadowRay ? kQShadow : 0u) | (s << kQSampleShift) |
+                           ((uint32_t)rs.lightIdx << kQLightShift);
+    q.rayO[slot] = make_float4(rs.orig.x, rs.orig.y, rs.orig.z, __uint_as_float(pixel));
+    q.rayD[slot] = make_float4(rs.dir.x, rs.dir.y, rs.dir.z, __uint_as_float(flags));
+    q.st0[slot] = make_float4(rs.albedo.x, rs.albedo.y, rs.albedo.z, rs.rayConeWidth);
+    q.st1[slot] = make_float4(v.beta1.x, v.beta1.y, v.beta1.z, rs.rayConeSpread);
+    q.st2[slot] = make_float4(v.beta0.x, v.beta0.y, v.beta0.z, 0.0f);
+}
+
+RT_DEV SceneView scene_of(const PathTraceParams& P) {
+    SceneView sc;
+    sc.triPos = P.triPos;
+    sc.triNrm = P.triNrm;
+    sc.nodes = (const Node*)P.nodes;
+    sc.tlas = (const Node*)P.tlasNodes;
+    return sc;
+}
+
+// workgroup sum of traced rays into the frame counter (one atomic per workgroup)
+RT_DEV void add_rays(const PathTraceParams& P, unsigned long long* wgSlots, uint32_t rays) {
+    if (!P.rayCounter) return;
+    unsigned long long r = rays;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+    const int tid = threadIdx.x;
+    if ((tid & 63) == 0) wgSlots[tid >> 6] = r;
+    __syncthreads();
+    if (tid == 0) atomicAdd(P.rayCounter, wgSlots[0] + wgSlots[1] + wgSlots[2] + wgSlots[3]);
+}
+
 }  // namespace
 
-__global__ __launch_bounds__(256) void k_pathtrace(PathTraceParams P) {
+__global__ __launch_bounds__(256) void k_pt_primary(PathTraceParams P) {
     __shared__ uint32_t stkA[16 * 256];
     __shared__ float stkT[16 * 256];
+    __shared__ uint32_t sob[256];
     __shared__ unsigned long long wgRays[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    bn_stage_sobol(P.bluenoise, sob, tid, 256);
+    __syncthreads();
     const int x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
     const int yl = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
     const bool active = x < (int)P.width && yl < (int)P.rows;
-    uint32_t rays = 0;
-    if (active) {
-        const int y = (int)P.y0 + yl;
-        Ctx c{P, SceneView{}, stkA + tid, stkT + tid, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), 0u, 0u, 0u, 0u};
-        c.sc.triPos = P.triPos;
-        c.sc.triNrm = P.triNrm;
-        c.sc.nodes = (const Node*)P.nodes;
-        c.sc.tlas = (const Node*)P.tlasNodes;
-        SampleOut s0;
-        F3 L = f3(0.0f), A = f3(0.0f);
+    const int y = (int)P.y0 + yl;
+    const uint32_t p = (uint32_t)y * P.width + (uint32_t)x;   // frame pixel
+    const uint32_t pl = (uint32_t)yl * P.width + (uint32_t)x; // strip pixel
+    const SceneView sc = scene_of(P);
+    PathCtx c{P, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), sob, BnPixel{0u, 0u}, 0, 0u, 0u, 0u, 0u};
+    float coneSpread = 0.0f;
+    F3 centerDir = f3(0.0f);
+    if (active) {  // per-pixel invariants of the sample loop
+        c.bp = bn_pixel(P.bluenoise, x, y);
+        coneSpread = ray_cone_width(P, x, y);
+        centerDir = center_dir(P.cam, x, y);
+    }
+    F3 L = f3(0.0f), A = f3(0.0f), L0s = f3(0.0f), A0s = f3(0.0f), N0 = f3(0.0f);
+    float D0 = 0.0f;
+    F2 M0 = {0.0f, 0.0f};
+    uint32_t mask0 = 0u;
+    int sd = -1;  // first deferred sample
 #pragma unroll 1
-        for (uint32_t s = 0; s < P.spp; ++s) {  // fp32 running sums in sample order, one divide
-            SampleOut so;
-            path_sample(c, x, y, (int)P.spp * (P.frameNum - 1) + 1 + (int)s, so);
-            if (s == 0) s0 = so;
-            L = L + so.L2;
-            A = A + so.albedo;
+    for (uint32_t s = 0; s < P.spp; ++s) {  // uniform trip count: every lane reaches the appends
+        PathVars v;
+        int kd = 5;
+        if (active) {
+            c.frameIdx = (int)P.spp * (P.frameNum - 1) + 1 + (int)s;
+            RayState& rs = v.rs;
+            v.beta0 = f3(1.0f);
+            v.beta1 = f3(1.0f);
+            rs.hitLight = false;
+            rs.lightIdx = kDefaultLightId;
+            rs.isHitProcessed = true;
+            rs.isOccluded = false;
+            rs.isShadowRay = false;
+            rs.isDiffuse = false;
+            rs.hit = false;
+            rs.matType = MAT_SKY;
+            rs.matId = 0;
+            rs.objectIdx = -1;
+            rs.normal = f3(0.0f, -1.0f, 0.0f);
+            rs.fakeNormal = f3(0.0f);
+            rs.albedo = f3(1.0f);
+            rs.rayConeWidth = 0.0f;
+            rs.rayConeSpread = coneSpread;
+            rs.centerRaydir = centerDir;
+            generate_ray_jittered(P.cam, x, y, F2{rnd(c, 0, 0), rnd(c, 0, 1)}, F2{rnd(c, 0, 2), rnd(c, 0, 3)}, rs.orig,
+                                  rs.dir, v.sampleUv);
+            v.outDepth = 0.0f;
+            v.mask = 0u;
+            v.mv = F2{0.0f, 0.0f};
+            v.outNormal = f3(0.0f);
+            kd = run_path<3>(c, v, 0, nullptr, sc, stkA + tid, stkT + tid);
         }
+        const uint32_t slot3 = wave_append(kd == 3, &P.ws.counters[kCntQ3]);
+        const uint32_t slot4 = wave_append(kd == 4, &P.ws.counters[kCntQ4]);
+        if (active) {
+            A = A + v.rs.albedo;
+            if (s == 0) {
+                A0s = v.rs.albedo;
+                N0 = v.outNormal;
+                D0 = v.outDepth;
+                M0 = v.mv;
+                mask0 = v.mask;
+            }
+            if (kd < 5) {
+                ++c.rays;  // the deferred RaySceneIntersect
+                enqueue(kd == 3 ? P.ws.q3 : P.ws.q4, kd == 3 ? slot3 : slot4, v, p, s);
+                if (sd < 0) {
+                    sd = (int)s;
+                    if (s > 0) P.ws.pathL[(size_t)pl * P.spp + s - 1] = make_float4(L.x, L.y, L.z, 0.0f);
+                }
+            } else {
+                const F3 Ls = finish(c, v);
+                if (s == 0) L0s = Ls;
+                if (sd < 0) L = L + Ls;
+                else P.ws.pathL[(size_t)pl * P.spp + s] = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
+            }
+        }
+    }
+    const uint32_t pslot = wave_append(active && sd >= 0, &P.ws.counters[kCntPending]);
+    if (active) {
         if (P.spp == 1) {
-            L = s0.L2;
-            A = s0.albedo;
+            L = L0s;
+            A = A0s;
         } else {
             L = L / (float)P.spp;
             A = A / (float)P.spp;
         }
-        const size_t p = (size_t)y * P.width + x;
-        P.colorOut[p] = pack_h4(L.x, L.y, L.z, s0.mask);
-        P.normalOut[p] = pack_h4(s0.normal.x, s0.normal.y, s0.normal.z, 0u);
+        if (N0.x != N0.x || N0.y != N0.y || N0.z != N0.z) N0 = f3(0.0f);
+        if (D0 != D0) D0 = 0.0f;
+        if (M0.x != M0.x || M0.y != M0.y) M0 = F2{0.0f, 0.0f};
+        if (sd >= 0) {
+            P.ws.pending[pslot] = pl | ((uint32_t)sd << 26);
+            P.colorOut[p] = make_uint2(0u, mask0 << 16);  // colour resolved by k_pt_resolve
+        } else {
+            P.colorOut[p] = pack_h4(L.x, L.y, L.z, mask0);
+        }
+        P.normalOut[p] = pack_h4(N0.x, N0.y, N0.z, 0u);
         P.albedoOut[p] = pack_h4(A.x, A.y, A.z, 0u);
-        P.depthOut[p] = rt_f2h(s0.depth);
-        P.motionOut[p] = (uint32_t)rt_f2h(s0.motion.x) | ((uint32_t)rt_f2h(s0.motion.y) << 16);
+        P.depthOut[p] = rt_f2h(D0);
+        P.motionOut[p] = (uint32_t)rt_f2h(M0.x) | ((uint32_t)rt_f2h(M0.y) << 16);
         if (P.raysOut) P.raysOut[p] = c.rays;
         if (P.statsOut) P.statsOut[p] = make_uint4(c.rays, c.visits, c.tests, c.diffuse);
-        rays = c.rays;
     }
-    if (P.rayCounter) {
-        unsigned long long r = rays;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
-        if (lane == 0) wgRays[w] = r;
-        __syncthreads();
-        if (tid == 0) atomicAdd(P.rayCounter, wgRays[0] + wgRays[1] + wgRays[2] + wgRays[3]);
+    add_rays(P, wgRays, active ? c.rays : 0u);
+}
+
+// Resumes the samples of queue kStep (3 or 4) once k_trace_queue has written their hits.
+template <int kStep>
+__global__ __launch_bounds__(256) void k_pt_resume(PathTraceParams P) {
+    __shared__ uint32_t sob[256];
+    __shared__ unsigned long long wgRays[4];
+    const int tid = threadIdx.x;
+    bn_stage_sobol(P.bluenoise, sob, tid, 256);
+    __syncthreads();
+    const PtQueue& q = kStep == 3 ? P.ws.q3 : P.ws.q4;
+    const uint32_t n = P.ws.counters[kStep == 3 ? kCntQ3 : kCntQ4];
+    const SceneView sc = scene_of(P);
+    uint32_t rays = 0;
+#pragma unroll 1
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {  // block-uniform
+        const uint32_t i = base + (uint32_t)tid;
+        const bool active = i < n;
+        PathCtx c{P, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), sob, BnPixel{0u, 0u}, 0, 0u, 0u, 0u, 0u};
+        PathVars v;
+        int kd = 5;
+        uint32_t p = 0, s = 0;
+        if (active) {
+            const float4 o = q.rayO[i], d = q.rayD[i], s0 = q.st0[i], s1 = q.st1[i], s2 = q.st2[i];
+            const float4 hr = P.ws.hitRec[i];
+            const float herr = P.ws.hitErr[i];
+            p = __float_as_uint(o.w);
+            const uint32_t flags = __float_as_uint(d.w);
+            s = (flags >> kQSampleShift) & 63u;
+            const int x = (int)(p % P.width), y = (int)(p / P.width);
+            c.bp = bn_pixel(P.bluenoise, x, y);
+            c.frameIdx = (int)P.spp * (P.frameNum - 1) + 1 + (int)s;
+            RayState& rs = v.rs;
+            rs.orig = f3(o.x, o.y, o.z);
+            rs.dir = f3(d.x, d.y, d.z);
+            rs.isShadowRay = (flags & kQShadow) != 0u;
+            rs.lightIdx = (int)(flags >> kQLightShift);
+            rs.albedo = f3(s0.x, s0.y, s0.z);
+            rs.rayConeWidth = s0.w;
+            v.beta1 = f3(s1.x, s1.y, s1.z);
+            rs.rayConeSpread = s1.w;
+            v.beta0 = f3(s2.x, s2.y, s2.z);
+            rs.hitLight = false;  // a traced ray had neither flag set
+            rs.isOccluded = false;
+            rs.isHitProcessed = true;
+            rs.isDiffuse = false;
+            rs.centerRaydir = f3(0.0f);  // read by D0 only
+            rs.matId = 0;
+            rs.matType = MAT_SKY;
+            HitInfo h;
+            finalize_hit(sc, rs.orig, rs.dir, hr.x, (int)__float_as_uint(hr.y), hr.z, hr.w, herr, h);
+            kd = run_path<0>(c, v, kStep, &h, sc, nullptr, nullptr);
+        }
+        const uint32_t slot = wave_append(kd == 4, &P.ws.counters[kCntQ4]);
+        if (active) {
+            if (kd < 5) {  // kStep == 3 only: the I4 ray
+                ++c.rays;
+                enqueue(P.ws.q4, slot, v, p, s);
+            } else {
+                const F3 Ls = finish(c, v);
+                const uint32_t pl = p - P.y0 * P.width;
+                P.ws.pathL[(size_t)pl * P.spp + s] = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
+            }
+            if (P.raysOut && c.rays) atomicAdd(&P.raysOut[p], c.rays);
+            if (P.statsOut) {
+                if (c.rays) atomicAdd(&P.statsOut[p].x, c.rays);
+                if (c.diffuse) atomicAdd(&P.statsOut[p].w, c.diffuse);
+            }
+            rays += c.rays;
+        }
+    }
+    add_rays(P, wgRays, rays);
+}
+
+// colour of the pixels with a deferred sample: the fp32 sample average in sample order
+__global__ __launch_bounds__(256) void k_pt_resolve(PathTraceParams P) {
+    const uint32_t n = P.ws.counters[kCntPending];
+#pragma unroll 1
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint32_t e = P.ws.pending[i];
+        const uint32_t pl = e & 0x3FFFFFFu, sd = e >> 26;
+        const float4* ls = P.ws.pathL + (size_t)pl * P.spp;
+        F3 L;
+        if (P.spp == 1) {
+            L = f3(ls[0].x, ls[0].y, ls[0].z);
+        } else {
+            L = f3(0.0f);
+            if (sd > 0) L = f3(ls[sd - 1].x, ls[sd - 1].y, ls[sd - 1].z);  // prefix sum of samples < sd
+            for (uint32_t s = sd; s < P.spp; ++s) L = L + f3(ls[s].x, ls[s].y, ls[s].z);
+            L = L / (float)P.spp;
+        }
+        const uint32_t p = pl + P.y0 * P.width;
+        const uint32_t mask = P.colorOut[p].y >> 16;
+        P.colorOut[p] = pack_h4(L.x, L.y, L.z, mask);
     }
 }
 
+extern "C" hipError_t rtk_launch_trace_queue(const PathTraceParams* p, int step, hipStream_t stream);
+
 extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream) {
-    if (p->spp < 1) return hipErrorInvalidValue;
-    dim3 grid((p->width + 15) / 16, (p->rows + 15) / 16);
-    hipLaunchKernelGGL(k_pathtrace, grid, dim3(256), 0, stream, *p);
+    if (p->spp < 1 || p->spp > 64 || p->ws.persistBlocks < 1) return hipErrorInvalidValue;
+    if ((size_t)p->rows * p->width >= (1u << 26) || (size_t)p->rows * p->width * p->spp > p->ws.cap)
+        return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const dim3 grid((p->width + 15) / 16, (p->rows + 15) / 16);
+    hipLaunchKernelGGL(k_pt_primary, grid, dim3(256), 0, stream, *p);
+    if ((e = rtk_launch_trace_queue(p, 3, stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pt_resume<3>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
+    if ((e = rtk_launch_trace_queue(p, 4, stream)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pt_resume<4>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
+    hipLaunchKernelGGL(k_pt_resolve, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
     return hipGetLastError();
 }

@@ -30,6 +30,32 @@ RT_DEV float bluenoise(const uint8_t* tables, int px, int py, int sampleIdx, int
     return ((float)value + 0.5f) / 256.0f;
 }
 
+// The same lookup split into its per-pixel half (ranking + scrambling bytes of dims 0..3, one
+// dword each) and its per-sample half against an LDS copy of sobol dims 0..3 (row r at [r]).
+// bn_value(...) == bluenoise(...) for dim < 4.
+struct BnPixel {
+    uint32_t rnk, scr;
+};
+
+RT_DEV BnPixel bn_pixel(const uint8_t* tables, int px, int py) {
+    const uint8_t* scr = tables + 256 * 256;
+    const uint8_t* rnk = scr + 128 * 128 * 8;
+    const int cell = ((px & 127) + (py & 127) * 128) * 8;
+    return BnPixel{*(const uint32_t*)(rnk + cell), *(const uint32_t*)(scr + cell)};
+}
+
+RT_DEV float bn_value(const uint32_t* sobolRows, BnPixel b, int sampleIdx, int dim) {
+    const int sh = 8 * dim;
+    const int ranked = (sampleIdx & 255) ^ (int)((b.rnk >> sh) & 255u);
+    const int value = (int)((sobolRows[ranked] >> sh) & 255u) ^ (int)((b.scr >> sh) & 255u);
+    return ((float)value + 0.5f) / 256.0f;
+}
+
+// workgroup-cooperative copy of sobol dims 0..3 into LDS (caller syncs)
+RT_DEV void bn_stage_sobol(const uint8_t* tables, uint32_t* sobolRows, int tid, int nthreads) {
+    for (int r = tid; r < 256; r += nthreads) sobolRows[r] = *(const uint32_t*)(tables + r * 256);
+}
+
 RT_DEV F2 concentric_disk(F2 u) {
     const F2 o = {2.0f * u.x - 1.0f, 2.0f * u.y - 1.0f};
     if (fabsf(o.x) < 1e-10f && fabsf(o.y) < 1e-10f) return F2{0.0f, 0.0f};
@@ -47,6 +73,27 @@ RT_DEV F2 concentric_disk(F2 u) {
 }
 
 RT_DEV F3 load3(const float* a) { return f3(a[0], a[1], a[2]); }
+
+// the pixel-centre direction of GenerateRay (raygen.cuh:7-38): the same for every sample
+RT_DEV F3 center_dir(const TraceCamera& c, int ix, int iy) {
+    F2 uvc = {((float)ix + 0.5f) * c.invRes[0], ((float)iy + 0.5f) * c.invRes[1]};
+    uvc = F2{uvc.x * -2.0f + 1.0f, uvc.y * -2.0f + 1.0f};
+    const F3 pc = load3(c.adjustedFront) + load3(c.adjustedLeft) * uvc.x + load3(c.adjustedUp) * uvc.y;
+    return normalize(pc);
+}
+
+// GenerateRay without the centre direction
+RT_DEV void generate_ray_jittered(const TraceCamera& c, int ix, int iy, F2 pix, F2 ap, F3& orig, F3& dir,
+                                  F2& sampleUv) {
+    F2 uv = {((float)ix + pix.x) * c.invRes[0], ((float)iy + pix.y) * c.invRes[1]};
+    sampleUv = uv;
+    uv = F2{uv.x * -2.0f + 1.0f, uv.y * -2.0f + 1.0f};
+    const F3 p = load3(c.adjustedFront) + load3(c.adjustedLeft) * uv.x + load3(c.adjustedUp) * uv.y;
+    const F2 d = concentric_disk(ap);
+    const F3 pa = d.x * load3(c.apertureLeft) + d.y * load3(c.apertureUp);
+    orig = load3(c.pos) + pa;
+    dir = normalize(p - pa);
+}
 
 RT_DEV void generate_ray(const TraceCamera& c, int ix, int iy, F2 pix, F2 ap, F3& orig, F3& dir, F3& centerDir,
                          F2& sampleUv) {

@@ -1,0 +1,152 @@
+// trace_queue.hip — persistent tracer of a deferred-ray queue (wavefront path tracing,
+// DESIGN.md §4) for gfx950.
+//
+// The bounce and shadow rays leaving a surface are incoherent: inside one wave64 their
+// traversals differ in length by an order of magnitude, and the single-kernel path tracer
+// kept every lane of a wave waiting for its longest ray at 2 waves/SIMD.  Here a lean kernel
+// (traversal state only) runs at 5 waves/SIMD, and each wave refills its idle lanes from the
+// queue (one atomic per 64 rays, see Fetch) so lanes stay busy until the queue is drained
+// (Aila & Laine 2009, persistent threads with dynamic fetch).
+//
+// Each lane runs TraverseBvh (traverse.h:107-253) one iteration per trav_step call, so the
+// reference semantics — 16-entry LDS stack with dropped overflow pushes, nearer child first,
+// 1024-iteration cap — hold per ray exactly as in the inline traversal.
+//
+// Exit: a lane becomes `exhausted` once its reserve is empty and every part is drained; the
+// wave leaves the loop when no lane holds a ray, which every wave reaches because the fetch
+// counters only grow and every ray ends within 1024 iterations.
+#include "frame_kernels.h"
+#include "traverse.h"
+
+using namespace rtd;
+
+namespace {
+
+constexpr int kTraceBlock = 256;
+constexpr int kRefillMin = 16;  // idle lanes that trigger a refill
+constexpr int kParts = 8;       // fetch counters (one per XCD by blockIdx % 8): spreads the atomics
+
+// Work distribution.  Wave g first takes items [64 g, 64 g + 64) with no atomic: a short queue
+// (a sky-dominated frame) costs no atomics at all.  The rest, [64 * waves, n), is cut into
+// kParts contiguous parts; a wave tops up a 64-item reserve from its home part (one atomic per
+// 64 items), moving on to the next part when its home part is drained.  A same-address
+// device-scope atomic serialises at the memory side, so both the static first batch and the
+// per-part counters keep the queue of atomics on any one address short.
+struct Fetch {
+    uint32_t resLo, resHi;  // wave-uniform reserve [resLo, resHi)
+    uint32_t dynBase, partLen;
+    uint32_t drained;       // bit x: part x has no items left
+    int home;
+};
+
+RT_DEV void fetch_init(Fetch& f, uint32_t n, uint32_t wavesTotal, uint32_t gw) {
+    const uint32_t s0 = gw * 64u;
+    f.resLo = s0 < n ? s0 : n;
+    f.resHi = s0 + 64u < n ? s0 + 64u : n;
+    f.dynBase = wavesTotal * 64u;
+    const uint32_t dyn = n > f.dynBase ? n - f.dynBase : 0u;
+    f.partLen = (dyn + kParts - 1) / kParts;
+    f.drained = dyn == 0u ? (1u << kParts) - 1u : 0u;
+    f.home = (int)(blockIdx.x % kParts);
+}
+
+// refill an empty reserve from the first part that still has items (wave-uniform call)
+RT_DEV void fetch_topup(Fetch& f, uint32_t n, uint32_t* counters, int lane) {
+    while (f.resLo == f.resHi && f.drained != (1u << kParts) - 1u) {
+        int part = f.home;
+        while (f.drained & (1u << part)) part = (part + 1) % kParts;
+        uint32_t got = 0u;
+        if (lane == 0) got = atomicAdd(&counters[part * 16], 64u);  // counters 64 B apart
+        got = __shfl(got, 0);
+        const uint32_t lo = f.dynBase + part * f.partLen + got;
+        uint32_t hi = f.dynBase + part * f.partLen + (got + 64u < f.partLen ? got + 64u : f.partLen);
+        if (hi > n) hi = n;
+        if (got >= f.partLen || lo >= hi) {
+            f.drained |= 1u << part;
+            continue;
+        }
+        f.resLo = lo;
+        f.resHi = hi;
+    }
+}
+
+template <int kStep>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) {
+    __shared__ uint32_t stkA[16 * kTraceBlock];
+    __shared__ float stkT[16 * kTraceBlock];
+    const int tid = threadIdx.x;
+    const int lane = (int)__lane_id();
+    const PtQueue& q = kStep == 3 ? P.ws.q3 : P.ws.q4;
+    const uint32_t n = P.ws.counters[kStep == 3 ? kCntQ3 : kCntQ4];
+    uint32_t* fetchCounters = P.ws.fetch + (kStep == 3 ? 0 : kParts * 16);
+    SceneView sc;
+    sc.triPos = P.triPos;
+    sc.triNrm = P.triNrm;
+    sc.nodes = (const Node*)P.nodes;
+    sc.tlas = (const Node*)P.tlasNodes;
+
+    const uint32_t wavesPerBlock = kTraceBlock / 64;
+    Fetch f;
+    fetch_init(f, n, gridDim.x * wavesPerBlock, blockIdx.x * wavesPerBlock + (uint32_t)(tid >> 6));
+
+    bool active = false, exhausted = false;
+    uint32_t idx = 0;
+    TravRay r;
+    TravState s;
+    r.org = f3(0.0f);
+    trav_init(s);
+#pragma unroll 1
+    while (true) {
+        const unsigned long long need = __ballot(!active && !exhausted);
+        const unsigned long long busy = __ballot(active);
+        if (need != 0ull && (__popcll(need) >= kRefillMin || busy == 0ull)) {
+            const uint32_t k = (uint32_t)__popcll(need);
+            fetch_topup(f, n, fetchCounters, lane);
+            const uint32_t avail = f.resHi - f.resLo;
+            const bool none = avail == 0u && f.drained == (1u << kParts) - 1u;
+            if (!active && !exhausted) {
+                const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+                if (rank < avail) {
+                    idx = f.resLo + rank;
+                    const float4 o = q.rayO[idx], d = q.rayD[idx];
+                    trav_setup(sc, f3(o.x, o.y, o.z), f3(d.x, d.y, d.z), r);
+                    trav_init(s);
+                    active = true;
+                } else if (none) {
+                    exhausted = true;
+                }
+            }
+            f.resLo += k < avail ? k : avail;
+        }
+        if (__ballot(active) == 0ull) break;
+        if (active) {
+            const bool done = trav_step(sc, r, s, stkA + tid, stkT + tid, kTraceBlock) || s.iters >= 1024u;
+            if (done) {
+                P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);
+                P.ws.hitErr[idx] = s.hitErrT;
+                if (P.statsOut) {
+                    const uint32_t p = __float_as_uint(q.rayO[idx].w);
+                    atomicAdd(&P.statsOut[p].y, s.visits);
+                    atomicAdd(&P.statsOut[p].z, s.tests);
+                    atomicMax(&P.ws.counters[kStep == 3 ? kCntMaxIter3 : kCntMaxIter4], s.iters);
+                }
+                active = false;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int rtk_trace_queue_blocks_per_cu() {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_trace_queue<3>, kTraceBlock, 0) != hipSuccess) return 0;
+    return b;
+}
+
+extern "C" hipError_t rtk_launch_trace_queue(const PathTraceParams* p, int step, hipStream_t stream) {
+    const dim3 grid(p->ws.persistBlocks);
+    if (step == 3) hipLaunchKernelGGL(k_trace_queue<3>, grid, dim3(kTraceBlock), 0, stream, *p);
+    else hipLaunchKernelGGL(k_trace_queue<4>, grid, dim3(kTraceBlock), 0, stream, *p);
+    return hipGetLastError();
+}

@@ -176,92 +176,121 @@ RT_DEV F3 f3_of(float4 a) { return f3(a.x, a.y, a.z); }
 
 // stack entry: idx (15) | blasOffset (15) << 15 | isBlas << 30 | isLeaf << 31  + float t
 // stkA / stkT point at this thread's column: element k lives at [k * stride].
-RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint32_t* stkA, float* stkT, int stride, HitInfo& out) {
+//
+// The traversal is split into setup / one loop iteration / hit finalisation so that the
+// inline callers (primary rays, intersect()) and the persistent queue tracer (trace_queue.hip)
+// run the same per-iteration code: one call of trav_step == one iteration of TraverseBvh's
+// loop (traverse.h:120-160), which keeps the 1024-iteration cap exact per ray.
+struct TravRay {
+    F3 org;
+    RayBox h;
+    TriRay tr;
+};
+
+struct TravState {
+    float t;
+    int hitIdx;
+    float hitU, hitV, hitErrT;   // of the closest hit
+    float u, v, errT;            // of the last successful triangle test (HitInfo.u/.v)
+    int top;
+    uint32_t cIdx, cOff;
+    bool cBlas, cLeaf;
+    float cT;
+    uint32_t visits, tests, dropped, iters;
+};
+
+RT_DEV void trav_setup(const SceneView& sc, F3 org, F3 dir, TravRay& r) {
     const F3 inv = f3(safe_divide(1.0f, dir.x), safe_divide(1.0f, dir.y), safe_divide(1.0f, dir.z));
-    float t = kRayMax;
-    int objectIdx = -1;
-    float u = 0.0f, v = 0.0f, errorT = 1e-7f;
-    int hitIdx = -1;
-    float hitU = 0.0f, hitV = 0.0f, hitErrT = 1e-7f;
-    uint32_t visits = 0, tests = 0, dropped = 0, iters = 0;
-
     const Box sceneBox = node_merged(sc.tlas[0]);
-    const RayBox h = make_raybox(org, dir, sceneBox, inv);
-    const TriRay tr = make_triray(dir);
+    r.org = org;
+    r.h = make_raybox(org, dir, sceneBox, inv);
+    r.tr = make_triray(dir);
+}
 
-    int top = -1;
-    uint32_t cIdx = 0, cOff = 0;
-    bool cBlas = false, cLeaf = false;
-    float cT = -kFltMax;
+RT_DEV void trav_init(TravState& s) {
+    s.t = kRayMax;
+    s.hitIdx = -1;
+    s.hitU = 0.0f; s.hitV = 0.0f; s.hitErrT = 1e-7f;
+    s.u = 0.0f; s.v = 0.0f; s.errT = 1e-7f;
+    s.top = -1;
+    s.cIdx = 0; s.cOff = 0;
+    s.cBlas = false; s.cLeaf = false;
+    s.cT = -kFltMax;
+    s.visits = 0; s.tests = 0; s.dropped = 0; s.iters = 0;
+}
 
-    for (int it = 0; it < 1024; ++it) {
-        ++iters;
-        bool pop = false;
-        if (cLeaf) {
-            if (cBlas) {
-                const uint32_t li = cOff * 1024u + cIdx;
-                const float4 p0 = sc.triPos[3 * li], p1 = sc.triPos[3 * li + 1], p2 = sc.triPos[3 * li + 2];
-                ++tests;
-                float tt;
-                if (watertight(tr, org, f3_of(p0), f3_of(p1), f3_of(p2), t, tt, u, v, errorT) && tt < t) {
-                    t = tt;
-                    objectIdx = (int)li;
-                    hitIdx = (int)li;
-                    hitU = u; hitV = v; hitErrT = errorT;
-                }
-                pop = true;
+// One loop iteration; returns true when the stack ran empty (TestForFinish, traverse.h:88-105).
+// The caller stops at 1024 iterations as well.
+//
+// Written for a short dependent chain per iteration (a lone wave's traversal latency sets the
+// tail of the queue tracer): the node visit picks the next node and the pushed sibling with
+// selects instead of the reference's four-way branch, and there is a single branch for the push.
+RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint32_t* stkA, float* stkT, int stride) {
+    ++s.iters;
+    bool pop;
+    if (!s.cLeaf) {
+        const Node nd = s.cBlas ? sc.nodes[s.cOff * 1024u + s.cIdx] : sc.tlas[s.cIdx];
+        ++s.visits;
+        float t1, t2;
+        const bool i1 = box_test(r.h, nd.q0.x, nd.q0.y, nd.q0.z, nd.q0.w, nd.q1.x, nd.q1.y, t1);
+        const bool i2 = box_test(r.h, nd.q1.z, nd.q1.w, nd.q2.x, nd.q2.y, nd.q2.z, nd.q2.w, t2);
+        // one child hit: go there; both: nearer first (tie -> right), push the other
+        const bool both = i1 && i2;
+        const bool goLeft = both ? (t1 < t2) : i1;
+        if (both) {
+            if (s.top >= 15) {
+                ++s.dropped;
             } else {
-                cLeaf = false;
-                cBlas = true;
-                cOff = cIdx;
-                cIdx = 0;
-            }
-        } else {
-            const Node nd = cBlas ? sc.nodes[cOff * 1024u + cIdx] : sc.tlas[cIdx];
-            ++visits;
-            float t1, t2;
-            const bool i1 = box_test(h, nd.q0.x, nd.q0.y, nd.q0.z, nd.q0.w, nd.q1.x, nd.q1.y, t1);
-            const bool i2 = box_test(h, nd.q1.z, nd.q1.w, nd.q2.x, nd.q2.y, nd.q2.z, nd.q2.w, t2);
-            if (!i1 && !i2) {
-                pop = true;
-            } else if (i1 && !i2) {
-                cIdx = nd.q3.x; cLeaf = nd.q3.z != 0u; cT = t1;
-            } else if (!i1 && i2) {
-                cIdx = nd.q3.y; cLeaf = nd.q3.w != 0u; cT = t2;
-            } else {
-                const bool leftFirst = t1 < t2;
-                const uint32_t pIdx = leftFirst ? nd.q3.y : nd.q3.x;
-                const uint32_t pLeaf = leftFirst ? nd.q3.w : nd.q3.z;
-                const float pT = leftFirst ? t2 : t1;
-                if (top >= 15) {
-                    ++dropped;
-                } else {
-                    ++top;
-                    stkA[top * stride] = (pIdx & 0x7FFFu) | ((cOff & 0x7FFFu) << 15) | ((cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31);
-                    stkT[top * stride] = pT;
-                }
-                cIdx = leftFirst ? nd.q3.x : nd.q3.y;
-                cLeaf = (leftFirst ? nd.q3.z : nd.q3.w) != 0u;
-                cT = leftFirst ? t1 : t2;
+                ++s.top;
+                const uint32_t pIdx = goLeft ? nd.q3.y : nd.q3.x;
+                const uint32_t pLeaf = goLeft ? nd.q3.w : nd.q3.z;
+                stkA[s.top * stride] = (pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) | ((s.cBlas ? 1u : 0u) << 30) |
+                                       ((pLeaf ? 1u : 0u) << 31);
+                stkT[s.top * stride] = goLeft ? t2 : t1;
             }
         }
-        if (pop) {  // TestForFinish (traverse.h:88-105)
-            bool finished = false;
-            do {
-                if (top < 0) { finished = true; break; }
-                const uint32_t a = stkA[top * stride];
-                cT = stkT[top * stride];
-                --top;
-                cIdx = a & 0x7FFFu;
-                cOff = (a >> 15) & 0x7FFFu;
-                cBlas = (a >> 30) & 1u;
-                cLeaf = (a >> 31) & 1u;
-            } while (cT > t);
-            if (finished) break;
+        pop = !i1 && !i2;
+        if (!pop) {
+            s.cIdx = goLeft ? nd.q3.x : nd.q3.y;
+            s.cLeaf = (goLeft ? nd.q3.z : nd.q3.w) != 0u;
+            s.cT = goLeft ? t1 : t2;
         }
+    } else if (s.cBlas) {
+        const uint32_t li = s.cOff * 1024u + s.cIdx;
+        const float4 p0 = sc.triPos[3 * li], p1 = sc.triPos[3 * li + 1], p2 = sc.triPos[3 * li + 2];
+        ++s.tests;
+        float tt;
+        if (watertight(r.tr, r.org, f3_of(p0), f3_of(p1), f3_of(p2), s.t, tt, s.u, s.v, s.errT) && tt < s.t) {
+            s.t = tt;
+            s.hitIdx = (int)li;
+            s.hitU = s.u; s.hitV = s.v; s.hitErrT = s.errT;
+        }
+        pop = true;
+    } else {  // TLAS leaf: continue at the root of that batch's BLAS
+        s.cLeaf = false;
+        s.cBlas = true;
+        s.cOff = s.cIdx;
+        s.cIdx = 0;
+        pop = false;
     }
+    if (pop) {  // TestForFinish (traverse.h:88-105)
+        do {
+            if (s.top < 0) return true;
+            const uint32_t a = stkA[s.top * stride];
+            s.cT = stkT[s.top * stride];
+            --s.top;
+            s.cIdx = a & 0x7FFFu;
+            s.cOff = (a >> 15) & 0x7FFFu;
+            s.cBlas = (a >> 30) & 1u;
+            s.cLeaf = (a >> 31) & 1u;
+        } while (s.cT > s.t);
+    }
+    return false;
+}
 
-    // hit finalisation (traverse.h:161-174, traverse.cuh:192-217), once for the closest hit
+// hit finalisation (traverse.h:161-174, traverse.cuh:192-217), once for the closest hit
+RT_DEV void finalize_hit(const SceneView& sc, F3 org, F3 dir, float t, int hitIdx, float hitU, float hitV,
+                         float hitErrT, HitInfo& out) {
     F3 nrm = f3(0.0f), pos = f3(kRayMax), fake = f3(0.0f);
     float offset = 1e-7f;
     if (hitIdx >= 0) {
@@ -285,9 +314,7 @@ RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint32_t* stkA, float
     const bool hit = t < kRayMax;
     if (!hit) { nrm = f3(0.0f, -1.0f, 0.0f); fake = f3(0.0f, -1.0f, 0.0f); }
     out.t = t;
-    out.objectIdx = objectIdx;
-    out.u = u;
-    out.v = v;
+    out.objectIdx = hitIdx;
     out.normal = nrm;
     out.fakeNormal = fake;
     out.pos = pos;
@@ -295,7 +322,19 @@ RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint32_t* stkA, float
     out.ndr = ndr;
     out.into = into;
     out.hit = hit;
-    out.visits = visits; out.tests = tests; out.dropped = dropped; out.iters = iters;
+}
+
+RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint32_t* stkA, float* stkT, int stride, HitInfo& out) {
+    TravRay r;
+    trav_setup(sc, org, dir, r);
+    TravState s;
+    trav_init(s);
+    for (int it = 0; it < 1024; ++it)
+        if (trav_step(sc, r, s, stkA, stkT, stride)) break;
+    finalize_hit(sc, org, dir, s.t, s.hitIdx, s.hitU, s.hitV, s.hitErrT, out);
+    out.u = s.u;
+    out.v = s.v;
+    out.visits = s.visits; out.tests = s.tests; out.dropped = s.dropped; out.iters = s.iters;
 }
 
 }  // namespace rtd

@@ -25,7 +25,7 @@ ARR = dict(VERTICES=0, INDICES=1, NORMALS=2, TRI_POS=3, AABBS=4, MORTON=5, REORD
            TLAS_MORTON=9, TLAS_REORDER=10, TLAS_NODES=11, TLAS_SCENE_AABB=12, BATCH_SCENE_AABBS=13, HITS=14,
            HIT_NORMALS=15, HIT_FAKE_NORMALS=16, HIT_STATS=17, TRI_NRM=18, RAYS=19, SKY_PDF=20, SKY_CDF=21,
            SUN_PDF=22, SUN_CDF=23, SUN_DIR=24, HISTOGRAM=25, EXPOSURE=26, COLOR4=27, COLOR16=28, COLOR64=29,
-           RGBA8=30, PT_STATS=31)
+           RGBA8=30, PT_STATS=31, PT_QUEUE=32)
 # rt_buffer_name (Buffer2DName, kernel.cuh:286-315)
 BUF = dict(RENDER_COLOR=0, ACCUMULATION=1, HISTORY_COLOR=2, SCALED_COLOR=3, NORMAL=10, DEPTH=11, HISTORY_DEPTH=12,
            MOTION=13, NOISE_LEVEL=14, NOISE_LEVEL16=15, SKY=16, SUN=17, ALBEDO=18)

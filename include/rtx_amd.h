@@ -231,7 +231,8 @@ enum rt_array_name {
     RT_ARR_PT_QUEUE = 32,        /* uint32[64] path-trace wavefront counters of the last launch: [0] rays
                                     deferred at step 3, [1] at step 4, [4] pixels resolved late,
                                     [8]/[9] longest traversal (iterations) of the step-3/4 queues
-                                    (detail launches only) */
+                                    (detail launches only), [10] internal errors (must be 0),
+                                    [11] pixels with a sample that hit geometry */
     RT_ARR_PT_STATS = 31         /* uint32[W*H][4] rays, node visits, triangle tests, diffuse events
                                     (rt_path_trace with_detail) */
 };

@@ -196,6 +196,8 @@ int rt_frame_init(rt_context* ctx) {
         if (cap >= (1ull << 31)) { ctx->err = "strip x spp too large for the path-trace queues"; return RT_ERR_ARG; }
         PtWorkspace& ws = fr.ws;
         ws.cap = (uint32_t)cap;
+        ALLOC(ws.hit0Rec, cap * 16);
+        ALLOC(ws.hit0Err, cap * 4);
         for (PtQueue* q : {&ws.q3, &ws.q4}) {
             ALLOC(q->rayO, cap * 16);
             ALLOC(q->rayD, cap * 16);
@@ -207,6 +209,7 @@ int rt_frame_init(rt_context* ctx) {
         ALLOC(ws.hitErr, cap * 4);
         ALLOC(ws.pathL, cap * 16);
         ALLOC(ws.pending, (size_t)ctx->renderW * ctx->stripRows * 4);
+        ALLOC(ws.surface, (size_t)ctx->renderW * ctx->stripRows * 4);
         ALLOC(ws.counters, kWsCounterWords * 4);
         ws.fetch = ws.counters + 64;
         int dev = 0, cus = 0;
@@ -318,6 +321,14 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.statsOut = with_detail ? fr.ptStats : nullptr;
     p.rayCounter = fr.rayCounter;
     p.ws = fr.ws;
+    {  // material table (init.cu:215-251): only mirror / glass ids make steps 1-2 trace
+        const int m = ctx->materialOverride;
+        p.ws.glossy = m >= 0 && (m == 1 || m == 5 || m >= 10);
+    }
+    if (with_detail) {
+        HIP_TRY(ctx, hipMemsetAsync(fr.rays, 0, (size_t)ctx->renderW * ctx->renderH * 4, ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(fr.ptStats, 0, (size_t)ctx->renderW * ctx->renderH * 16, ctx->stream));
+    }
     HIP_TRY(ctx, rtk_launch_pathtrace(&p, ctx->stream));
     fr.renderColor = fr.color;
     fr.hist = hist_of(hc);  // HistoryCamera::Setup after PathTrace (kernel.cu:357)

@@ -62,19 +62,24 @@ struct PtQueue {
 
 // counters[] slots (zeroed before every path-trace launch sequence)
 enum PtCounter : int { kCntQ3 = 0, kCntQ4 = 1, kCntFetch3 = 2, kCntFetch4 = 3, kCntPending = 4, kCntResume3 = 5,
-                       kCntResume4 = 6, kCntResolve = 7, kCntMaxIter3 = 8, kCntMaxIter4 = 9, kCntSlots = 10 };
+                       kCntResume4 = 6, kCntResolve = 7, kCntMaxIter3 = 8, kCntMaxIter4 = 9, kCntError = 10,
+                       kCntSurface = 11, kCntSlots = 12 };
 constexpr int kWsCounterWords = 64 + 2 * 8 * 16;  // counters | fetch, zeroed together
 
 struct PtWorkspace {
+    float4* hit0Rec;            // [spp][rows*W] camera-ray hits (t, triangle index bits, u, v)
+    float* hit0Err;             // [spp][rows*W] their errorT
     PtQueue q3, q4;             // rays deferred at step 3 / step 4 of PathTrace's sequence
     float4* hitRec;             // [cap] (t, triangle index bits, u, v) of the closest hit
     float* hitErr;              // [cap] its errorT
     float4* pathL;              // [rows*W*spp] per-sample radiance of pixels resolved late
     uint32_t* pending;          // [rows*W] pixel (strip-local) | first deferred sample << 26
+    uint32_t* surface;          // [rows*W] strip-local pixels with a sample that hit geometry
     uint32_t* counters;         // [kCntSlots]
     uint32_t* fetch;            // [2][8 parts x 16]: k_trace_queue fetch counters, 64 B apart
     uint32_t cap;               // entries per queue (= rows * W * spp)
     uint32_t persistBlocks;     // grid of the persistent queue kernels
+    int glossy;                 // materials can be glossy: steps 1-2 may trace (materialOverride)
 };
 
 struct PathTraceParams {

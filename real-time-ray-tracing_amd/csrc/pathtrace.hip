@@ -1,12 +1,15 @@
 // pathtrace.hip — the per-pixel path tracer (PathTrace, pathtrace.cuh:11-128) for gfx950,
 // run as a wavefront pipeline:
 //
-//   k_pt_primary    one thread per pixel, looping over its samples: blue noise, GenerateRay,
-//                   the steps I0 G0 I1 G1 I2 G2 D0 of the reference's straight-line sequence
-//                   with the (coherent) primary traversal inline.  A sample whose next step is
-//                   an intersection (I3: the BSDF bounce or the shadow ray) is appended to
-//                   queue 3 with the state the rest of the path needs; every other sample is
-//                   finished here.
+//   k_pt_camera     one thread per (pixel, sample): blue noise, GenerateRay and the step-0
+//                   RaySceneIntersect; a lean kernel (traversal state only) so the coherent
+//                   camera rays trace at 4 waves/SIMD.  Writes the closest-hit record.
+//   k_pt_shade0     one thread per pixel, looping over its samples: regenerates the camera
+//                   ray, applies its hit and runs G0 I1 G1 I2 G2 D0 of the reference's
+//                   straight-line sequence (I1/I2 trace inline only when the material table
+//                   holds mirror or glass).  A sample whose next step is an intersection (I3:
+//                   the BSDF bounce or the shadow ray) is appended to queue 3 with the state
+//                   the rest of the path needs; every other sample is finished here.
 //   k_trace_queue   (trace_queue.hip) traces a queue with persistent, refilling waves.
 //   k_pt_resume<3>  applies the I3 hit, runs G3 D1 and appends the I4 rays to queue 4.
 //   k_trace_queue   traces queue 4.
@@ -54,7 +57,7 @@ RT_DEV float rnd(const PathCtx& c, int k, int d) { return bn_value(c.sob, c.bp, 
 struct PathVars {
     RayState rs;
     F3 beta0, beta1;
-    // sample-0 G-buffer values, set by steps 0 and 2 (always run in k_pt_primary)
+    // sample-0 G-buffer values, set by steps 0 and 2 (always run in k_pt_shade0)
     float outDepth;
     uint32_t mask;
     F2 mv, sampleUv;
@@ -364,121 +367,280 @@ RT_DEV void add_rays(const PathTraceParams& P, unsigned long long* wgSlots, uint
     if (tid == 0) atomicAdd(P.rayCounter, wgSlots[0] + wgSlots[1] + wgSlots[2] + wgSlots[3]);
 }
 
+// per-sample init of PathTrace (pathtrace.cuh:20-60) and GenerateRay (raygen.cuh:7-38)
+RT_DEV void start_sample(PathCtx& c, PathVars& v, int x, int y, float coneSpread, F3 centerDir) {
+    RayState& rs = v.rs;
+    v.beta0 = f3(1.0f);
+    v.beta1 = f3(1.0f);
+    rs.hitLight = false;
+    rs.lightIdx = kDefaultLightId;
+    rs.isHitProcessed = true;
+    rs.isOccluded = false;
+    rs.isShadowRay = false;
+    rs.isDiffuse = false;
+    rs.hit = false;
+    rs.matType = MAT_SKY;
+    rs.matId = 0;
+    rs.objectIdx = -1;
+    rs.normal = f3(0.0f, -1.0f, 0.0f);
+    rs.fakeNormal = f3(0.0f);
+    rs.albedo = f3(1.0f);
+    rs.rayConeWidth = 0.0f;
+    rs.rayConeSpread = coneSpread;
+    rs.centerRaydir = centerDir;
+    generate_ray_jittered(c.P.cam, x, y, F2{rnd(c, 0, 0), rnd(c, 0, 1)}, F2{rnd(c, 0, 2), rnd(c, 0, 3)}, rs.orig,
+                          rs.dir, v.sampleUv);
+    v.outDepth = 0.0f;
+    v.mask = 0u;
+    v.mv = F2{0.0f, 0.0f};
+    v.outNormal = f3(0.0f);
+}
+
 }  // namespace
 
-__global__ __launch_bounds__(256) void k_pt_primary(PathTraceParams P) {
+// Pixel block of one k_pt_camera workgroup: four waves = (4 / nSW) 8x8 tiles x nSW sample
+// lanes, nSW = min(spp, 4) rounded down to 1, 2 or 4.
+__host__ __device__ inline int cam_sample_waves(uint32_t spp) { return spp >= 4 ? 4 : (spp >= 2 ? 2 : 1); }
+
+// Step 0 of every sample: the camera ray's RaySceneIntersect.  A sample that misses is complete
+// right here (its path is GenerateRay -> miss -> EnvLight2, pathtrace.cuh:61-128, with every
+// other step a no-op), so a pixel whose samples all miss — the sky, most of the default view —
+// gets its G-buffer texels from this kernel and never reaches the shading kernels.  The other
+// pixels keep their samples' hit records and are appended to the surface list for k_pt_shade0.
+__global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
     __shared__ uint32_t stkA[16 * 256];
     __shared__ float stkT[16 * 256];
     __shared__ uint32_t sob[256];
+    __shared__ float4 fold[4][64];   // this round's samples: sky colour xyz, w = 1 when it hit
+    __shared__ uint32_t surf[4][64]; // pixel has a sample that hit (set by its folding thread)
     __shared__ unsigned long long wgRays[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     bn_stage_sobol(P.bluenoise, sob, tid, 256);
     __syncthreads();
-    const int x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
-    const int yl = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
+    const int nSW = cam_sample_waves(P.spp);
+    const int sw = w % nSW, g = w / nSW, tilesX = nSW == 4 ? 1 : 2;
+    const int BW = 8 * tilesX, BH = nSW == 1 ? 16 : 8;
+    const int x = blockIdx.x * BW + (g % tilesX) * 8 + (lane & 7);
+    const int yl = blockIdx.y * BH + (g / tilesX) * 8 + (lane >> 3);
     const bool active = x < (int)P.width && yl < (int)P.rows;
     const int y = (int)P.y0 + yl;
-    const uint32_t p = (uint32_t)y * P.width + (uint32_t)x;   // frame pixel
-    const uint32_t pl = (uint32_t)yl * P.width + (uint32_t)x; // strip pixel
+    const uint32_t p = (uint32_t)y * P.width + (uint32_t)x;
+    const uint32_t pl = (uint32_t)yl * P.width + (uint32_t)x;
+    const size_t plane = (size_t)P.rows * P.width;
     const SceneView sc = scene_of(P);
     PathCtx c{P, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), sob, BnPixel{0u, 0u}, 0, 0u, 0u, 0u, 0u};
-    float coneSpread = 0.0f;
-    F3 centerDir = f3(0.0f);
-    if (active) {  // per-pixel invariants of the sample loop
-        c.bp = bn_pixel(P.bluenoise, x, y);
-        coneSpread = ray_cone_width(P, x, y);
-        centerDir = center_dir(P.cam, x, y);
-    }
-    F3 L = f3(0.0f), A = f3(0.0f), L0s = f3(0.0f), A0s = f3(0.0f), N0 = f3(0.0f);
-    float D0 = 0.0f;
-    F2 M0 = {0.0f, 0.0f};
-    uint32_t mask0 = 0u;
-    int sd = -1;  // first deferred sample
+    if (active) c.bp = bn_pixel(P.bluenoise, x, y);
+    const int rounds = ((int)P.spp + nSW - 1) / nSW;
+    F3 L = f3(0.0f), A = f3(0.0f);  // folding thread (sw == 0): running sums of an all-sky pixel
+    bool anyHit = false;
+    float4 rec = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float recErr = 0.0f;
+    uint32_t rays = 0;
 #pragma unroll 1
-    for (uint32_t s = 0; s < P.spp; ++s) {  // uniform trip count: every lane reaches the appends
-        PathVars v;
-        int kd = 5;
-        if (active) {
-            c.frameIdx = (int)P.spp * (P.frameNum - 1) + 1 + (int)s;
-            RayState& rs = v.rs;
-            v.beta0 = f3(1.0f);
-            v.beta1 = f3(1.0f);
-            rs.hitLight = false;
-            rs.lightIdx = kDefaultLightId;
-            rs.isHitProcessed = true;
-            rs.isOccluded = false;
-            rs.isShadowRay = false;
-            rs.isDiffuse = false;
-            rs.hit = false;
-            rs.matType = MAT_SKY;
-            rs.matId = 0;
-            rs.objectIdx = -1;
-            rs.normal = f3(0.0f, -1.0f, 0.0f);
-            rs.fakeNormal = f3(0.0f);
-            rs.albedo = f3(1.0f);
-            rs.rayConeWidth = 0.0f;
-            rs.rayConeSpread = coneSpread;
-            rs.centerRaydir = centerDir;
-            generate_ray_jittered(P.cam, x, y, F2{rnd(c, 0, 0), rnd(c, 0, 1)}, F2{rnd(c, 0, 2), rnd(c, 0, 3)}, rs.orig,
-                                  rs.dir, v.sampleUv);
-            v.outDepth = 0.0f;
-            v.mask = 0u;
-            v.mv = F2{0.0f, 0.0f};
-            v.outNormal = f3(0.0f);
-            kd = run_path<3>(c, v, 0, nullptr, sc, stkA + tid, stkT + tid);
-        }
-        const uint32_t slot3 = wave_append(kd == 3, &P.ws.counters[kCntQ3]);
-        const uint32_t slot4 = wave_append(kd == 4, &P.ws.counters[kCntQ4]);
-        if (active) {
-            A = A + v.rs.albedo;
-            if (s == 0) {
-                A0s = v.rs.albedo;
-                N0 = v.outNormal;
-                D0 = v.outDepth;
-                M0 = v.mv;
-                mask0 = v.mask;
+    for (int r = 0; r < rounds; ++r) {  // uniform trip count: every thread reaches the barriers
+        const int s = r * nSW + sw;
+        float4 out = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (active && s < (int)P.spp) {
+            c.frameIdx = (int)P.spp * (P.frameNum - 1) + 1 + s;
+            F3 org, dir;
+            F2 uv;
+            generate_ray_jittered(P.cam, x, y, F2{rnd(c, 0, 0), rnd(c, 0, 1)}, F2{rnd(c, 0, 2), rnd(c, 0, 3)}, org,
+                                  dir, uv);
+            TravRay tr;
+            trav_setup(sc, org, dir, tr);
+            TravState st;
+            trav_init(st);
+            for (int it = 0; it < 1024; ++it)
+                if (trav_step(sc, tr, st, stkA + tid, stkT + tid, 256)) break;
+            ++rays;
+            if (P.statsOut) {
+                atomicAdd(&P.statsOut[p].y, st.visits);
+                atomicAdd(&P.statsOut[p].z, st.tests);
             }
-            if (kd < 5) {
-                ++c.rays;  // the deferred RaySceneIntersect
-                enqueue(kd == 3 ? P.ws.q3 : P.ws.q4, kd == 3 ? slot3 : slot4, v, p, s);
-                if (sd < 0) {
-                    sd = (int)s;
-                    if (s > 0) P.ws.pathL[(size_t)pl * P.spp + s - 1] = make_float4(L.x, L.y, L.z, 0.0f);
-                }
-            } else {
+            rec = make_float4(st.t, __uint_as_float((uint32_t)st.hitIdx), st.hitU, st.hitV);
+            recErr = st.hitErrT;
+            if (rounds > 1) {  // several rounds: the pixel's status is not known yet
+                P.ws.hit0Rec[(size_t)s * plane + pl] = rec;
+                P.ws.hit0Err[(size_t)s * plane + pl] = recErr;
+            }
+            if (st.t < kRayMax) {
+                out.w = 1.0f;
+            } else {  // the whole path: finish() of a miss (beta 1, albedo 1)
+                PathVars v;
+                v.rs.dir = dir;
+                v.rs.hitLight = true;
+                v.rs.isOccluded = false;
+                v.rs.matType = MAT_SKY;
+                v.rs.albedo = f3(1.0f);
+                v.beta0 = f3(1.0f);
+                v.beta1 = f3(1.0f);
                 const F3 Ls = finish(c, v);
-                if (s == 0) L0s = Ls;
-                if (sd < 0) L = L + Ls;
-                else P.ws.pathL[(size_t)pl * P.spp + s] = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
+                out = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
             }
         }
-    }
-    const uint32_t pslot = wave_append(active && sd >= 0, &P.ws.counters[kCntPending]);
-    if (active) {
-        if (P.spp == 1) {
-            L = L0s;
-            A = A0s;
-        } else {
-            L = L / (float)P.spp;
-            A = A / (float)P.spp;
+        fold[w][lane] = out;
+        __syncthreads();
+        if (sw == 0 && active) {
+#pragma unroll 1
+            for (int k = 0; k < nSW; ++k) {  // fold this round's samples in sample order
+                const int sk = r * nSW + k;
+                if (sk >= (int)P.spp) break;
+                const float4 o = fold[g * nSW + k][lane];
+                anyHit = anyHit || o.w != 0.0f;
+                if (P.spp == 1) {
+                    L = f3(o.x, o.y, o.z);
+                    A = f3(1.0f);
+                } else {
+                    L = L + f3(o.x, o.y, o.z);
+                    A = A + f3(1.0f);
+                }
+            }
         }
-        if (N0.x != N0.x || N0.y != N0.y || N0.z != N0.z) N0 = f3(0.0f);
-        if (D0 != D0) D0 = 0.0f;
-        if (M0.x != M0.x || M0.y != M0.y) M0 = F2{0.0f, 0.0f};
-        if (sd >= 0) {
-            P.ws.pending[pslot] = pl | ((uint32_t)sd << 26);
-            P.colorOut[p] = make_uint2(0u, mask0 << 16);  // colour resolved by k_pt_resolve
-        } else {
-            P.colorOut[p] = pack_h4(L.x, L.y, L.z, mask0);
-        }
-        P.normalOut[p] = pack_h4(N0.x, N0.y, N0.z, 0u);
-        P.albedoOut[p] = pack_h4(A.x, A.y, A.z, 0u);
-        P.depthOut[p] = rt_f2h(D0);
-        P.motionOut[p] = (uint32_t)rt_f2h(M0.x) | ((uint32_t)rt_f2h(M0.y) << 16);
-        if (P.raysOut) P.raysOut[p] = c.rays;
-        if (P.statsOut) P.statsOut[p] = make_uint4(c.rays, c.visits, c.tests, c.diffuse);
+        __syncthreads();
     }
-    add_rays(P, wgRays, active ? c.rays : 0u);
+    if (sw == 0) surf[g][lane] = (active && anyHit) ? 1u : 0u;
+    __syncthreads();
+    const bool surface = active && surf[g][lane] != 0u;
+    if (surface && rounds == 1 && sw < (int)P.spp) {
+        P.ws.hit0Rec[(size_t)sw * plane + pl] = rec;
+        P.ws.hit0Err[(size_t)sw * plane + pl] = recErr;
+    }
+    if (active && rays) {
+        if (P.raysOut) atomicAdd(&P.raysOut[p], rays);
+        if (P.statsOut) atomicAdd(&P.statsOut[p].x, rays);
+    }
+    const uint32_t slot = wave_append(sw == 0 && surface, &P.ws.counters[kCntSurface]);
+    if (sw == 0 && active) {
+        if (surface) {
+            P.ws.surface[slot] = pl;
+        } else {  // G-buffer of an all-sky pixel: sample 0 missed (matId 99999, miss normal/depth)
+            if (P.spp > 1) {
+                L = L / (float)P.spp;
+                A = A / (float)P.spp;
+            }
+            P.colorOut[p] = pack_h4(L.x, L.y, L.z, 99999u & 0xFFFFu);
+            P.normalOut[p] = pack_h4(0.0f, -1.0f, 0.0f, 0u);
+            P.albedoOut[p] = pack_h4(A.x, A.y, A.z, 0u);
+            P.depthOut[p] = rt_f2h(kRayMax);
+            P.motionOut[p] = (uint32_t)rt_f2h(0.5f) | ((uint32_t)rt_f2h(0.5f) << 16);
+        }
+    }
+    add_rays(P, wgRays, rays);
+}
+
+// Steps 0 (hit from k_pt_camera) .. 3 of every sample of the surface pixels.  kGlossy: the
+// material table holds mirror/glass, so steps 1 and 2 may trace (inline, LDS stack).
+template <bool kGlossy>
+__global__ __launch_bounds__(256) void k_pt_shade0(PathTraceParams P) {
+    __shared__ uint32_t stkA[kGlossy ? 16 * 256 : 1];
+    __shared__ float stkT[kGlossy ? 16 * 256 : 1];
+    __shared__ uint32_t sob[256];
+    __shared__ unsigned long long wgRays[4];
+    const int tid = threadIdx.x;
+    bn_stage_sobol(P.bluenoise, sob, tid, 256);
+    __syncthreads();
+    const uint32_t n = P.ws.counters[kCntSurface];
+    const SceneView sc = scene_of(P);
+    const size_t plane = (size_t)P.rows * P.width;
+    uint32_t raysWg = 0;
+#pragma unroll 1
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {  // block-uniform
+        const uint32_t i = base + (uint32_t)tid;
+        const bool active = i < n;
+        const uint32_t pl = active ? P.ws.surface[i] : 0u;
+        const int x = (int)(pl % P.width), yl = (int)(pl / P.width);
+        const int y = (int)P.y0 + yl;
+        const uint32_t p = (uint32_t)y * P.width + (uint32_t)x;
+        PathCtx c{P, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), sob, BnPixel{0u, 0u}, 0, 0u, 0u, 0u, 0u};
+        float coneSpread = 0.0f;
+        F3 centerDir = f3(0.0f);
+        if (active) {  // per-pixel invariants of the sample loop
+            c.bp = bn_pixel(P.bluenoise, x, y);
+            coneSpread = ray_cone_width(P, x, y);
+            centerDir = center_dir(P.cam, x, y);
+        }
+        F3 L = f3(0.0f), A = f3(0.0f), L0s = f3(0.0f), A0s = f3(0.0f), N0 = f3(0.0f);
+        float D0 = 0.0f;
+        F2 M0 = {0.0f, 0.0f};
+        uint32_t mask0 = 0u;
+        int sd = -1;  // first deferred sample
+#pragma unroll 1
+        for (uint32_t s = 0; s < P.spp; ++s) {  // uniform trip count: every lane reaches the appends
+            PathVars v;
+            int kd = 5;
+            if (active) {
+                c.frameIdx = (int)P.spp * (P.frameNum - 1) + 1 + (int)s;
+                start_sample(c, v, x, y, coneSpread, centerDir);
+                const size_t q = (size_t)s * plane + pl;
+                const float4 hr = P.ws.hit0Rec[q];
+                HitInfo h;
+                finalize_hit(sc, v.rs.orig, v.rs.dir, hr.x, (int)__float_as_uint(hr.y), hr.z, hr.w, P.ws.hit0Err[q],
+                             h);
+                kd = run_path<kGlossy ? 3 : 1>(c, v, 0, &h, sc, stkA + (kGlossy ? tid : 0), stkT + (kGlossy ? tid : 0));
+                if (kd < 3) {  // cannot happen without mirror/glass materials: flag it, finish the sample
+                    atomicAdd(&P.ws.counters[kCntError], 1u);
+                    kd = 5;
+                }
+            }
+            const uint32_t slot3 = wave_append(kd == 3, &P.ws.counters[kCntQ3]);
+            const uint32_t slot4 = wave_append(kd == 4, &P.ws.counters[kCntQ4]);
+            if (active) {
+                A = A + v.rs.albedo;
+                if (s == 0) {
+                    A0s = v.rs.albedo;
+                    N0 = v.outNormal;
+                    D0 = v.outDepth;
+                    M0 = v.mv;
+                    mask0 = v.mask;
+                }
+                if (kd < 5) {
+                    ++c.rays;  // the deferred RaySceneIntersect
+                    enqueue(kd == 3 ? P.ws.q3 : P.ws.q4, kd == 3 ? slot3 : slot4, v, p, s);
+                    if (sd < 0) {
+                        sd = (int)s;
+                        if (s > 0) P.ws.pathL[(size_t)pl * P.spp + s - 1] = make_float4(L.x, L.y, L.z, 0.0f);
+                    }
+                } else {
+                    const F3 Ls = finish(c, v);
+                    if (s == 0) L0s = Ls;
+                    if (sd < 0) L = L + Ls;
+                    else P.ws.pathL[(size_t)pl * P.spp + s] = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
+                }
+            }
+        }
+        const uint32_t pslot = wave_append(active && sd >= 0, &P.ws.counters[kCntPending]);
+        if (active) {
+            if (P.spp == 1) {
+                L = L0s;
+                A = A0s;
+            } else {
+                L = L / (float)P.spp;
+                A = A / (float)P.spp;
+            }
+            if (N0.x != N0.x || N0.y != N0.y || N0.z != N0.z) N0 = f3(0.0f);
+            if (D0 != D0) D0 = 0.0f;
+            if (M0.x != M0.x || M0.y != M0.y) M0 = F2{0.0f, 0.0f};
+            if (sd >= 0) {
+                P.ws.pending[pslot] = pl | ((uint32_t)sd << 26);
+                P.colorOut[p] = make_uint2(0u, mask0 << 16);  // colour resolved by k_pt_resolve
+            } else {
+                P.colorOut[p] = pack_h4(L.x, L.y, L.z, mask0);
+            }
+            P.normalOut[p] = pack_h4(N0.x, N0.y, N0.z, 0u);
+            P.albedoOut[p] = pack_h4(A.x, A.y, A.z, 0u);
+            P.depthOut[p] = rt_f2h(D0);
+            P.motionOut[p] = (uint32_t)rt_f2h(M0.x) | ((uint32_t)rt_f2h(M0.y) << 16);
+            if (P.raysOut && c.rays) atomicAdd(&P.raysOut[p], c.rays);
+            if (P.statsOut) {
+                if (c.rays) atomicAdd(&P.statsOut[p].x, c.rays);
+                if (c.visits) atomicAdd(&P.statsOut[p].y, c.visits);
+                if (c.tests) atomicAdd(&P.statsOut[p].z, c.tests);
+                if (c.diffuse) atomicAdd(&P.statsOut[p].w, c.diffuse);
+            }
+            raysWg += c.rays;
+        }
+    }
+    add_rays(P, wgRays, raysWg);
 }
 
 // Resumes the samples of queue kStep (3 or 4) once k_trace_queue has written their hits.
@@ -584,8 +746,12 @@ extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t
         return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    const dim3 grid((p->width + 15) / 16, (p->rows + 15) / 16);
-    hipLaunchKernelGGL(k_pt_primary, grid, dim3(256), 0, stream, *p);
+    const int nSW = cam_sample_waves(p->spp);
+    const int BW = nSW == 4 ? 8 : 16, BH = nSW == 1 ? 16 : 8;
+    const dim3 grid((p->width + BW - 1) / BW, (p->rows + BH - 1) / BH);
+    hipLaunchKernelGGL(k_pt_camera, grid, dim3(256), 0, stream, *p);
+    if (p->ws.glossy) hipLaunchKernelGGL(k_pt_shade0<true>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
+    else hipLaunchKernelGGL(k_pt_shade0<false>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
     if ((e = rtk_launch_trace_queue(p, 3, stream)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_pt_resume<3>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
     if ((e = rtk_launch_trace_queue(p, 4, stream)) != hipSuccess) return e;

@@ -4,12 +4,13 @@ import csv
 import glob
 import sys
 
-names = ['k_pt_primary', 'k_trace_queue<3>', 'k_pt_resume<3>', 'k_trace_queue<4>', 'k_pt_resume<4>', 'k_pt_resolve']
+names = ['k_pt_camera', 'k_pt_shade0', 'k_trace_queue<3>', 'k_pt_resume<3>', 'k_trace_queue<4>', 'k_pt_resume<4>', 'k_pt_resolve']
 f = glob.glob(sys.argv[1] + '/*kernel_trace.csv')[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r['Start_Timestamp']))
 seq = [(k, (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3, int(r['Start_Timestamp']),
         int(r['End_Timestamp'])) for r in rows for k in names if k in r['Kernel_Name']]
-frames = [seq[i:i + 6] for i in range(0, len(seq), 6)]
+N = len(names)
+frames = [seq[i:i + N] for i in range(0, len(seq), N)]
 per = len(frames) // 3
 for ci, cam in enumerate(('default', 'down', 'up')):
     fr = frames[ci * per + 4]

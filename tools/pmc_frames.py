@@ -5,7 +5,7 @@ import csv
 import glob
 import sys
 
-names = ['k_pt_primary', 'k_trace_queue<3>', 'k_pt_resume<3>', 'k_trace_queue<4>', 'k_pt_resume<4>', 'k_pt_resolve']
+names = ['k_pt_camera', 'k_pt_shade0', 'k_trace_queue<3>', 'k_pt_resume<3>', 'k_trace_queue<4>', 'k_pt_resume<4>', 'k_pt_resolve']
 for d in sys.argv[1:]:
     f = glob.glob(d + '/*counter_collection.csv')[0]
     disp = collections.OrderedDict()
@@ -16,7 +16,8 @@ for d in sys.argv[1:]:
         key = int(r['Dispatch_Id'])
         disp.setdefault(key, [k, {}])[1][r['Counter_Name']] = float(r['Counter_Value'])
     seq = [disp[k] for k in sorted(disp)]
-    frames = [seq[i:i + 6] for i in range(0, len(seq), 6)]
+    N = len(names)
+    frames = [seq[i:i + N] for i in range(0, len(seq), N)]
     per_cam = len(frames) // 3
     for ci, cam in enumerate(('default', 'down', 'up')):
         fr = frames[ci * per_cam + 2]

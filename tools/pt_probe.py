@@ -20,16 +20,23 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--lib", default=None, help="alternative librtx.so (ablation builds)")
+    ap.add_argument("--torch-stream", action="store_true", help="run on torch's current stream, as bench.py does")
+    ap.add_argument("--only-default", action="store_true")
     a = ap.parse_args()
     if a.lib:
         rtx.load_library(a.lib)
     d = tempfile.mkdtemp()
     rt = rtx.RayTracer(a.width, a.height, rtx.write_config(os.path.join(d, "p.toml"), a.width, a.height, spp=4)).init()
     rt.set_delta_time(16.667)
+    if a.torch_stream:
+        import torch
+        torch.cuda.set_device(0)
+        rt.set_stream(torch.cuda.current_stream().cuda_stream)
     rt.build_bvh()
     out = {}
     base = rt.camera
-    for name, pitch in (("default", None), ("down", -1.2), ("up", 0.9)):
+    cams = (("default", None),) if a.only_default else (("default", None), ("down", -1.2), ("up", 0.9))
+    for name, pitch in cams:
         c = rtx.Camera.from_buffer_copy(base)
         if pitch is not None:
             c.pos[1] = 12.0 if name == "down" else base.pos[1]

@@ -275,7 +275,17 @@ RT_HD float rt_powf(float xf, float yf) {
 }
 
 // IEEE float -> binary16, round to nearest even (matches __float2half_rn / v_cvt_f16_f32)
+//
+// On gfx950 both conversions are the hardware v_cvt_f16_f32 / v_cvt_f32_f16 (round to nearest
+// even, half denormals preserved in the default float mode): the same bits as the integer
+// restatement below for every non-NaN input; NaNs are canonicalised to sign | 0x7E00 after
+// the hardware conversion so the two stay identical there too.
 RT_HD uint16_t rt_f2h(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (f != f) return (uint16_t)(((rtm::float_to_bits(f) >> 16) & 0x8000u) | 0x7E00u);
+    const _Float16 hv = (_Float16)f;
+    return __builtin_bit_cast(uint16_t, hv);
+#endif
     uint32_t x = rtm::float_to_bits(f);
     uint32_t sign = (x >> 16) & 0x8000u;
     uint32_t ax = x & 0x7FFFFFFFu;
@@ -298,6 +308,9 @@ RT_HD uint16_t rt_f2h(float f) {
 }
 
 RT_HD float rt_h2f(uint16_t h) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if ((h & 0x7C00u) != 0x7C00u) return (float)__builtin_bit_cast(_Float16, h);  // exact
+#endif
     uint32_t sign = ((uint32_t)h & 0x8000u) << 16;
     uint32_t e = ((uint32_t)h >> 10) & 0x1Fu;
     uint32_t m = (uint32_t)h & 0x3FFu;

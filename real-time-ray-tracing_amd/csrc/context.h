@@ -54,7 +54,8 @@ struct FrameResources {
     // denoise + post (denoising.cu, postprocessing.cu)
     uint2* colorB = nullptr;       // ping-pong partner of color
     uint2* accum = nullptr;        // AccumulationColorBuffer
-    uint2* histColor = nullptr;    // HistoryColorBuffer
+    uint2* histColor = nullptr;    // HistoryColorBuffer (latest)
+    uint2* histColorAlt = nullptr; // its partner: TemporalFilter2 writes here, then they swap
     uint16_t* histDepth = nullptr; // HistoryDepthBuffer
     uint16_t* noise8 = nullptr;
     uint16_t* noise16 = nullptr;

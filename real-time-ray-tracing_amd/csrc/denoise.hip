@@ -100,11 +100,84 @@ RT_DEV F3 bicubic_smooth(const View2& im, F2 uv) {
     return o / sw;
 }
 
+template <typename T>
+RT_DEV T tree_sum32(T v) {
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) v = v + __shfl_down(v, off, 32);
+    return v;
+}
+
+// TileNoiseLevel8x8 + TileNoiseLevel8x8to16x16 (denoising.cu:73-99) over the 16x16 output tile
+// the calling workgroup just produced (sOut, in LDS): threads 0..127 are four 32-lane groups,
+// one per 8x8 tile, with k_tile_noise's lane layout and shuffle-tree order; thread 0 then
+// averages the four half-rounded tile values into the 16x16 noise level.  Reads outside the
+// image clamp to its edge, which always lands inside this workgroup's tile.
+RT_DEV void noise_epilogue(const DenoisePostParams& P, const uint2* sOut, uint16_t* sN8) {
+    const int W = (int)P.W, H = (int)P.H;
+    const int W8 = (W + 7) / 8, H8 = (H + 7) / 8, W16 = (W + 15) / 16, H16 = (H + 15) / 16;
+    const int tid = threadIdx.x;
+    const int x0 = blockIdx.x * 16, y0 = blockIdx.y * 16;
+    if (tid < 128) {
+        const int t = tid >> 5, lane = tid & 31;
+        const int tx8 = 2 * blockIdx.x + (t & 1), ty8 = 2 * blockIdx.y + (t >> 1);
+        const bool valid = tx8 < W8 && ty8 < H8;
+        const int x = clampi((valid ? tx8 : 2 * (int)blockIdx.x) * 8 + (lane & 7), 0, W - 1);
+        const int ya = clampi((valid ? ty8 : 2 * (int)blockIdx.y) * 8 + 2 * (lane >> 3), 0, H - 1);
+        const int yb = clampi((valid ? ty8 : 2 * (int)blockIdx.y) * 8 + 2 * (lane >> 3) + 1, 0, H - 1);
+        const F3 ca = rgb_of(sOut[(ya - y0) * 16 + (x - x0)]), cb = rgb_of(sOut[(yb - y0) * 16 + (x - x0)]);
+        const uint32_t bg = (h2f(P.depth[(size_t)ya * W + x]) >= kRayMaxF ? 1u : 0u);
+        const uint32_t bg2 = (h2f(P.depth[(size_t)yb * W + x]) >= kRayMaxF ? 1u : 0u);
+        const float l1 = fmaxf(fmaxf(ca.x, ca.y), ca.z), l2 = fmaxf(fmaxf(cb.x, cb.y), cb.z);
+        const uint32_t b1s = tree_sum32(bg), b2s = tree_sum32(bg2);
+        const float s1 = tree_sum32(l1), s12 = tree_sum32(l1 * l1), s2 = tree_sum32(l2), s22 = tree_sum32(l2 * l2);
+        if (lane == 0) {
+            uint16_t h = 0;
+            if (valid) {
+                const float notSky = 1.0f - (float)(b1s + b2s) / 64.0f;
+                const float lumAve = (s1 + s2) / 64.0f;
+                const float lumAveSq = lumAve * lumAve;
+                const float lumSqAve = (s12 + s22) / 64.0f;
+                const float var = fmaxf(1e-20f, lumSqAve - lumAveSq);
+                float noise = var / fmaxf(lumAveSq, 1e-20f);
+                noise *= notSky;
+                h = (uint16_t)f2h(noise);
+                P.noise8[ty8 * W8 + tx8] = h;
+            }
+            sN8[t] = h;
+        }
+    }
+    __syncthreads();
+    if (tid == 0 && (int)blockIdx.x < W16 && (int)blockIdx.y < H16) {
+        // n8.at(2x + i, 2y + j) clamped to the tile grid: tile i/j falls back to 0 past its edge
+        const int i1 = 2 * (int)blockIdx.x + 1 < W8 ? 1 : 0, j1 = 2 * (int)blockIdx.y + 1 < H8 ? 2 : 0;
+        const float v1 = h2f(sN8[0]), v2 = h2f(sN8[i1]), v3 = h2f(sN8[j1]), v4 = h2f(sN8[i1 + j1]);
+        P.noise16[blockIdx.y * W16 + blockIdx.x] = (uint16_t)f2h((v1 + v2 + v3 + v4) / 4);
+    }
+}
+
 // ------------------------------------------------------------------ TemporalFilter
+RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, int y);
+
+// kNoise: also the tile noise levels of the output (noise_epilogue)
+template <bool kNoise>
 __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uint2* in, uint2* out) {
+    __shared__ uint2 sOut[kNoise ? 256 : 1];
+    __shared__ uint16_t sN8[4];
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
     const int W = (int)P.W, H = (int)P.H;
-    if (x >= W || y >= H) return;
+    if (x < W && y < H) {
+        const uint2 res = temporal_pixel(P, in, x, y);
+        out[(size_t)y * W + x] = res;
+        if (kNoise) sOut[threadIdx.x] = res;
+    }
+    if (kNoise) {
+        __syncthreads();
+        noise_epilogue(P, sOut, sN8);
+    }
+}
+
+RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, int y) {
+    const int W = (int)P.W, H = (int)P.H;
     const View2 col{in, W, H}, nrm{P.normal, W, H}, acc{P.accum, W, H};
     const View1 dep{P.depth, W, H};
     const size_t p = (size_t)y * W + x;
@@ -176,18 +249,12 @@ __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uin
             res = pack_color(o, mV);
         }
     }
-    out[p] = res;
+    return res;
 }
 
 // ------------------------------------------------------------------ tile noise level
 // One 32-lane group per 8x8 tile (two per wave64): lane L = tx + 8*ty covers rows 2ty, 2ty+1.
 // Sums use the reference's __shfl_down tree (offsets 16..1) so lane 0 gets its exact order.
-template <typename T>
-RT_DEV T tree_sum32(T v) {
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) v = v + __shfl_down(v, off, 32);
-    return v;
-}
 
 __global__ __launch_bounds__(256) void k_tile_noise(DenoisePostParams P, const uint2* color) {
     const int W = (int)P.W, H = (int)P.H;
@@ -245,10 +312,16 @@ __global__ __launch_bounds__(256) void k_noise_visualize(DenoisePostParams P, ui
 // 16x16 tile + 3-pixel apron staged in LDS (22 x 22 entries of colour, normal, depth).
 struct Tap7 { uint2 c; uint2 n; float d; };
 
+RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD, int tx,
+                            int ty);
+
+template <bool kNoise>
 __global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uint2* in, uint2* out) {
     __shared__ uint2 sC[22 * 22];
     __shared__ uint2 sN[22 * 22];
     __shared__ float sD[22 * 22];
+    __shared__ uint2 sOut[kNoise ? 256 : 1];
+    __shared__ uint16_t sN8[4];
     const int W = (int)P.W, H = (int)P.H;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const int x = blockIdx.x * 16 + tx, y = blockIdx.y * 16 + ty;
@@ -265,9 +338,20 @@ __global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uin
         }
     }
     __syncthreads();
-    if (x >= W || y >= H) return;
-    const size_t p = (size_t)y * W + x;
-    if (gated) { out[p] = in[p]; return; }
+    if (x < W && y < H) {
+        const size_t p = (size_t)y * W + x;
+        const uint2 res = gated ? in[p] : spatial7_pixel(P, sC, sN, sD, tx, ty);
+        out[p] = res;
+        if (kNoise) sOut[threadIdx.x] = res;
+    }
+    if (kNoise) {
+        __syncthreads();
+        noise_epilogue(P, sOut, sN8);
+    }
+}
+
+RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD, int tx,
+                            int ty) {
     const int ci = (tx + 3) + (ty + 3) * 22;
     const uint2 c0 = sC[ci];
     uint2 res = c0;
@@ -307,11 +391,12 @@ __global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uin
         if (isnan3(fin)) fin = f3(0.0f);
         res = pack_color(fin, mV);
     }
-    out[p] = res;
+    return res;
 }
 
 // ------------------------------------------------------------------ SpatialFilterGlobal5x5<S>
-template <int S>
+// kAlbedo: ApplyAlbedo (denoising.cu:160-171) fused into the store of the last wide pass
+template <int S, bool kAlbedo>
 __global__ __launch_bounds__(256) void k_spatial5(DenoisePostParams P, const uint2* in, uint2* out) {
     const int W = (int)P.W, H = (int)P.H;
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
@@ -358,16 +443,17 @@ __global__ __launch_bounds__(256) void k_spatial5(DenoisePostParams P, const uin
             res = pack_color(fin, mV);
         }
     }
+    if (kAlbedo) res = pack_color(rgb_of(res) * rgb_of(P.albedo[p]), 0x3C00u);  // w = half(1.0)
     out[p] = res;
 }
 
 // ------------------------------------------------------------------ ApplyAlbedo (in place, pointwise)
-__global__ __launch_bounds__(256) void k_apply_albedo(DenoisePostParams P, uint2* color) {
+__global__ __launch_bounds__(256) void k_apply_albedo(DenoisePostParams P, const uint2* in, uint2* out) {
     const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= (size_t)P.W * P.H) return;
-    const F3 c = rgb_of(color[p]);
+    const F3 c = rgb_of(in[p]);
     const F3 a = rgb_of(P.albedo[p]);
-    color[p] = pack_color(c * a, 0x3C00u);  // w = half(1.0)
+    out[p] = pack_color(c * a, 0x3C00u);  // w = half(1.0)
 }
 
 // ------------------------------------------------------------------ TemporalFilter2
@@ -531,10 +617,18 @@ __global__ void k_auto_exposure(float* e, const uint32_t* hist, float area, floa
 }
 
 // BicubicScale with SampleBicubicCatmullRom (16 taps, clamped)
-__global__ __launch_bounds__(256) void k_bicubic_scale(const uint2* in, int W, int H, uint2* out, int Ws, int Hs) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= Ws || y >= Hs) return;
-    const View2 im{in, W, H};
+// BicubicScale's source column / row of output pixel x (t1 of the 16-tap Catmull-Rom footprint)
+RT_DEV int scale_t1(int x, int Ws, int W) { return (int)floorf((float)x / Ws * (float)W - 0.5f); }
+
+// clamped reads of a W x H image staged in LDS: rows [Y0, Y0 + TH), columns [X0, X0 + TW)
+struct LdsImage {
+    const uint2* s;
+    int X0, Y0, TW, W, H;
+    RT_DEV uint2 at(int x, int y) const { return s[(clampi(y, 0, H - 1) - Y0) * TW + (clampi(x, 0, W - 1) - X0)]; }
+};
+
+template <class Img>
+RT_DEV uint2 bicubic_scale_px(const Img& im, int W, int H, int x, int y, int Ws, int Hs) {
     const F2 uv = {(float)x / Ws, (float)y / Hs};
     const F2 UV = {uv.x * (float)W, uv.y * (float)H};
     const float fx0 = floorf(UV.x - 0.5f), fy0 = floorf(UV.y - 0.5f);
@@ -558,19 +652,50 @@ __global__ __launch_bounds__(256) void k_bicubic_scale(const uint2* in, int W, i
             o = o + rgb_of(im.at(t1x - 1 + i, t1y - 1 + j)) * w;
         }
     o = o / sw;
-    out[(size_t)y * Ws + x] = pack_color(o, 0x3C00u);
+    return pack_color(o, 0x3C00u);
 }
 
-// SharpeningFilter (FidelityFX CAS), then the selected tone mapper and CopyToOutput's dither,
-// fused: the sharpened and tone-mapped values are rounded to half in between, as the
-// reference's separate passes store and reload them.
-__global__ __launch_bounds__(256) void k_sharpen_tonemap_output(DenoisePostParams P, const uint2* in, uint2* out) {
-    const int Ws = (int)P.Ws, Hs = (int)P.Hs;
+// BicubicScale, SharpeningFilter (FidelityFX CAS), the selected tone mapper and CopyToOutput's
+// dither in one pass.  Each workgroup evaluates the scaled image over its 16x16 screen tile and
+// a 1-pixel apron into LDS, rounded to half exactly as the reference stores ScaledColorBuffer;
+// the sharpened and tone-mapped values are rounded to half in between too, as the reference's
+// separate passes store and reload them.
+constexpr int kScaleLds = 48 * 48;  // render texels staged per workgroup (scale factors up to ~2.5)
+
+__global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const uint2* render) {
+    __shared__ uint2 sIn[kScaleLds];
+    __shared__ uint2 sS[18 * 18];
+    const int W = (int)P.W, H = (int)P.H, Ws = (int)P.Ws, Hs = (int)P.Hs;
+    const int X0 = blockIdx.x * 16 - 1, Y0 = blockIdx.y * 16 - 1;
+    // render texels the 18x18 output apron reads (t1 is monotone in x and y)
+    const int ix0 = clampi(scale_t1(clampi(X0, 0, Ws - 1), Ws, W) - 1, 0, W - 1);
+    const int ix1 = clampi(scale_t1(clampi(X0 + 17, 0, Ws - 1), Ws, W) + 2, 0, W - 1);
+    const int iy0 = clampi(scale_t1(clampi(Y0, 0, Hs - 1), Hs, H) - 1, 0, H - 1);
+    const int iy1 = clampi(scale_t1(clampi(Y0 + 17, 0, Hs - 1), Hs, H) + 2, 0, H - 1);
+    const int TW = ix1 - ix0 + 1, TH = iy1 - iy0 + 1;
+    const bool staged = TW * TH <= kScaleLds;
+    if (staged) {
+        for (int i = threadIdx.x; i < TW * TH; i += 256) sIn[i] = render[(size_t)(iy0 + i / TW) * W + ix0 + i % TW];
+        __syncthreads();
+    }
+    const LdsImage li{sIn, ix0, iy0, TW, W, H};
+    const View2 gi{render, W, H};
+    for (int i = threadIdx.x; i < 18 * 18; i += 256) {
+        const int sx = clampi(X0 + i % 18, 0, Ws - 1), sy = clampi(Y0 + i / 18, 0, Hs - 1);
+        sS[i] = staged ? bicubic_scale_px(li, W, H, sx, sy, Ws, Hs) : bicubic_scale_px(gi, W, H, sx, sy, Ws, Hs);
+    }
+    __syncthreads();
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= Ws || y >= Hs) return;
     const size_t p = (size_t)y * Ws + x;
-    const View2 im{in, Ws, Hs};
-    uint2 cur = in[p];
+    struct {  // clamped reads of the scaled image, from the LDS tile
+        const uint2* s;
+        int X0, Y0, Ws, Hs;
+        RT_DEV uint2 at(int xx, int yy) const {
+            return s[(clampi(yy, 0, Hs - 1) - Y0) * 18 + (clampi(xx, 0, Ws - 1) - X0)];
+        }
+    } im{sS, X0, Y0, Ws, Hs};
+    uint2 cur = im.at(x, y);
     if (P.sharpen) {
         F3 c[3][3];
 #pragma unroll
@@ -606,7 +731,7 @@ __global__ __launch_bounds__(256) void k_sharpen_tonemap_output(DenoisePostParam
         c = clamp3(f3(rt_powf(c.x, g), rt_powf(c.y, g), rt_powf(c.z, g)), f3(0.0f), f3(1.0f));
         cur = pack_color(c, 0x3C00u);
     }
-    out[p] = cur;
+    P.scaledB[p] = cur;
     // CopyToOutput (kernel.cu:26-59): blue-noise dither (bn/256; the -1/512 is integer 0)
     const int s = P.frameNum;
     F3 c = rgb_of(cur) + f3(bluenoise(P.bluenoise, x, y, s, 0) / 256, bluenoise(P.bluenoise, x, y, s, 1) / 256,
@@ -636,16 +761,16 @@ extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
     const int W = (int)P->W, H = (int)P->H, Ws = (int)P->Ws, Hs = (int)P->Hs;
     const size_t Pn = (size_t)W * H;
     const dim3 g16((W + 15) / 16, (H + 15) / 16), b256(256);
+    // Buffer plan: the path-trace colour (colorA) and colorB ping-pong; SpatialFilter7x7 writes
+    // AccumulationColorBuffer directly and TemporalFilter2 the next history buffer, so neither
+    // needs the reference's copy (denoising.cu:110-112, 178-183).  The tile noise levels are
+    // computed in the epilogue of the pass that produces their input when the debug
+    // visualisation is off.
     uint2* cur = P->colorA;
-    uint2* alt = P->colorB;
-    auto swap = [&]() { uint2* t = cur; cur = alt; alt = t; };
+    uint2* spare = P->colorB;
+    auto next_from = [&](uint2* dst) { if (cur == P->colorA || cur == P->colorB) spare = cur; cur = dst; };
     const int W8 = (W + 7) / 8, H8 = (H + 7) / 8, W16 = (W + 15) / 16, H16 = (H + 15) / 16;
-    // ---- TemporalSpatialDenoising (denoising.cu:51-188)
-    if (P->temporal && P->frameNum != 1) {
-        hipLaunchKernelGGL(k_temporal, g16, b256, 0, s, *P, (const uint2*)cur, alt);
-        LAUNCH_CHECK();
-        swap();
-    }
+    hipError_t e;
     auto noise = [&](int level) -> hipError_t {
         hipLaunchKernelGGL(k_tile_noise, dim3((W8 * H8 + 7) / 8), b256, 0, s, *P, (const uint2*)cur);
         LAUNCH_CHECK();
@@ -657,37 +782,59 @@ extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
         }
         return hipSuccess;
     };
-    hipError_t e;
-    if (P->localSpatial) {
-        if ((e = noise(1)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_spatial7, g16, b256, 0, s, *P, (const uint2*)cur, alt);
+    // ---- TemporalSpatialDenoising (denoising.cu:51-188)
+    bool noise1 = false;
+    if (P->temporal && P->frameNum != 1) {
+        noise1 = P->localSpatial && !P->visualize;
+        uint2* dst = spare;
+        if (noise1) hipLaunchKernelGGL(k_temporal<true>, g16, b256, 0, s, *P, (const uint2*)cur, dst);
+        else hipLaunchKernelGGL(k_temporal<false>, g16, b256, 0, s, *P, (const uint2*)cur, dst);
         LAUNCH_CHECK();
-        swap();
+        next_from(dst);
     }
-    if (P->temporal) {
+    bool noise2 = false;
+    if (P->localSpatial) {
+        if (!noise1 && (e = noise(1)) != hipSuccess) return e;
+        noise2 = P->wideSpatial && !P->visualize;
+        uint2* dst = P->temporal ? P->accum : spare;
+        if (noise2) hipLaunchKernelGGL(k_spatial7<true>, g16, b256, 0, s, *P, (const uint2*)cur, dst);
+        else hipLaunchKernelGGL(k_spatial7<false>, g16, b256, 0, s, *P, (const uint2*)cur, dst);
+        LAUNCH_CHECK();
+        next_from(dst);
+    } else if (P->temporal) {
         if ((e = hipMemcpyAsync(P->accum, cur, Pn * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
     }
     if (P->wideSpatial) {
-        if ((e = noise(2)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_spatial5<3>, g16, b256, 0, s, *P, (const uint2*)cur, alt);
+        if (P->visualize && cur == P->accum) {  // the debug outlines must not land in the history
+            if ((e = hipMemcpyAsync(spare, cur, Pn * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+            next_from(spare);
+        }
+        if (!noise2 && (e = noise(2)) != hipSuccess) return e;
+        // a: a colour buffer other than the one being read; b: the other colour buffer
+        uint2* a = cur == P->colorA ? P->colorB : cur == P->colorB ? P->colorA : spare;
+        uint2* b = a == P->colorA ? P->colorB : P->colorA;
+        hipLaunchKernelGGL((k_spatial5<3, false>), g16, b256, 0, s, *P, (const uint2*)cur, a);
         LAUNCH_CHECK();
-        swap();
-        hipLaunchKernelGGL(k_spatial5<6>, g16, b256, 0, s, *P, (const uint2*)cur, alt);
+        hipLaunchKernelGGL((k_spatial5<6, false>), g16, b256, 0, s, *P, (const uint2*)a, b);
         LAUNCH_CHECK();
-        swap();
-        hipLaunchKernelGGL(k_spatial5<12>, g16, b256, 0, s, *P, (const uint2*)cur, alt);
+        hipLaunchKernelGGL((k_spatial5<12, true>), g16, b256, 0, s, *P, (const uint2*)b, a);
         LAUNCH_CHECK();
-        swap();
+        cur = a;
+        spare = b;
+    } else {  // out of place when cur is the accumulation buffer (the next frame's history)
+        uint2* dst = cur == P->accum ? spare : cur;
+        hipLaunchKernelGGL(k_apply_albedo, dim3((unsigned)((Pn + 255) / 256)), b256, 0, s, *P, (const uint2*)cur, dst);
+        LAUNCH_CHECK();
+        cur = dst;
     }
-    hipLaunchKernelGGL(k_apply_albedo, dim3((unsigned)((Pn + 255) / 256)), b256, 0, s, *P, cur);
-    LAUNCH_CHECK();
     if (P->temporal2) {
         if (P->frameNum != 1) {
-            hipLaunchKernelGGL(k_temporal2, g16, b256, 0, s, *P, (const uint2*)cur, alt);
+            hipLaunchKernelGGL(k_temporal2, g16, b256, 0, s, *P, (const uint2*)cur, P->histColorOut);
             LAUNCH_CHECK();
-            swap();
+        } else if ((e = hipMemcpyAsync(P->histColorOut, cur, Pn * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) {
+            return e;
         }
-        if ((e = hipMemcpyAsync(P->histColor, cur, Pn * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+        cur = P->histColorOut;
         if ((e = hipMemcpyAsync(P->histDepth, P->depth, Pn * 2, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
     }
     P->finalColor = cur;
@@ -719,13 +866,10 @@ extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
                            (float)(W64 * H64), P->deltaTime, P->gain, P->autoExposure, P->fixedExposure);
         LAUNCH_CHECK();
     }
-    const dim3 gs((Ws + 15) / 16, (Hs + 15) / 16);
-    hipLaunchKernelGGL(k_bicubic_scale, gs, b256, 0, s, (const uint2*)cur, W, H, P->scaledA, Ws, Hs);
-    LAUNCH_CHECK();
     DenoisePostParams Q = *P;
     Q.sharpen = P->postProcess && P->sharpen;
     Q.tonemap = P->postProcess && P->tonemap;
-    hipLaunchKernelGGL(k_sharpen_tonemap_output, gs, b256, 0, s, Q, (const uint2*)P->scaledA, P->scaledB);
+    hipLaunchKernelGGL(k_scale_post, dim3((Ws + 15) / 16, (Hs + 15) / 16), b256, 0, s, Q, (const uint2*)cur);
     LAUNCH_CHECK();
     P->finalScaled = P->scaledB;
     return hipSuccess;

@@ -11,6 +11,7 @@
 
 #include <chrono>
 #include <fstream>
+#include <utility>
 #include <vector>
 
 #include "context.h"
@@ -221,6 +222,7 @@ int rt_frame_init(rt_context* ctx) {
     ALLOC(fr.colorB, P * 8);
     ALLOC(fr.accum, P * 8);
     ALLOC(fr.histColor, P * 8);
+    ALLOC(fr.histColorAlt, P * 8);
     ALLOC(fr.histDepth, P * 2);
     const size_t W = (size_t)ctx->renderW, H = (size_t)ctx->renderH;
     const size_t W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16 = (W4 + 3) / 4, H16 = (H4 + 3) / 4;
@@ -263,6 +265,7 @@ int rt_frame_init(rt_context* ctx) {
     HIP_TRY(ctx, hipMemset(fr.colorB, 0, P * 8));
     HIP_TRY(ctx, hipMemset(fr.accum, 0, P * 8));
     HIP_TRY(ctx, hipMemset(fr.histColor, 0, P * 8));
+    HIP_TRY(ctx, hipMemset(fr.histColorAlt, 0, P * 8));
     HIP_TRY(ctx, hipMemset(fr.histDepth, 0, P * 2));
     HIP_TRY(ctx, hipMemset(fr.histogram, 0, 256));
     const float exposure0[4] = {1.0f, 1.0f, 1.0f, 1.0f};  // init.cu:331-333
@@ -399,6 +402,7 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.motion = fr.motion;
     p.accum = fr.accum;
     p.histColor = fr.histColor;
+    p.histColorOut = fr.histColorAlt;
     p.histDepth = fr.histDepth;
     p.noise8 = fr.noise8;
     p.noise16 = fr.noise16;
@@ -413,6 +417,7 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.bluenoise = ctx->dBlueNoise;
     p.hdrOut = with_hdr ? fr.hdr : nullptr;
     HIP_TRY(ctx, rtk_denoise_post(&p, ctx->stream));
+    if (p.temporal2) std::swap(fr.histColor, fr.histColorAlt);
     fr.renderColor = p.finalColor;
     fr.scaledColor = p.finalScaled;
     return RT_OK;

@@ -134,7 +134,8 @@ struct DenoisePostParams {
     uint16_t* depth;            // written only by the noise-visualize debug pass
     const uint32_t* motion;
     uint2* accum;               // AccumulationColorBuffer
-    uint2* histColor;           // HistoryColorBuffer
+    uint2* histColor;           // HistoryColorBuffer of the previous frame (read by TemporalFilter2)
+    uint2* histColorOut;        // HistoryColorBuffer written this frame (the other of the pair)
     uint16_t* histDepth;        // HistoryDepthBuffer
     uint16_t* noise8;
     uint16_t* noise16;

@@ -221,10 +221,131 @@ RT_HD double atan2d(double y, double x) {
 }  // namespace rtm
 
 // ------------------------------------------------------------------ float API
-RT_HD float rt_expf(float x) { return (float)rtm::expd((double)x); }
-RT_HD float rt_exp2f(float x) { return (float)rtm::exp2d((double)x); }
-RT_HD float rt_logf(float x) { return (float)rtm::logd((double)x); }
-RT_HD float rt_log2f(float x) { return (float)rtm::log2d((double)x); }
+// ---- float cores of exp / log / pow (the denoiser's per-tap weights, texture gamma, LOD).
+// Single-precision arithmetic with explicit fmaf (v_fma_f32 on gfx950, the correctly rounded
+// fmaf of libm on the host) and correctly rounded division: the same bits on both sides at
+// about a quarter of the double path's latency.  log2 is carried as a float pair
+// (hi + lo, ~2^-40 relative) so that pow stays within about one ulp even for large exponents.
+namespace rtm {
+RT_HD float f_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
+// 2^f for |f| <= 0.5 + 2^-20: Taylor series of e^(f ln2) to degree 8 (truncation < 2e-10)
+RT_HD float exp2_core(float f) {
+    float p = 1.5252733804059840e-05f;  // ln2^7/7!
+    p = f_fma(p, f, 1.5403530393381609e-04f);
+    p = f_fma(p, f, 1.3333558146428443e-03f);
+    p = f_fma(p, f, 9.6181291076284772e-03f);
+    p = f_fma(p, f, 5.5504108664821580e-02f);
+    p = f_fma(p, f, 2.4022650695910071e-01f);
+    p = f_fma(p, f, 6.9314718055994531e-01f);
+    return f_fma(p, f, 1.0f);
+}
+
+// p * 2^n for p in [0.7, 1.5], n in [-151, 128], one rounding (into the subnormal range too)
+RT_HD float scale2(float p, int n) {
+    if (n > 127) return p * 2.0f * bits_to_float((uint32_t)(n - 1 + 127) << 23);
+    if (n >= -126) return p * bits_to_float((uint32_t)(n + 127) << 23);
+    return (p * bits_to_float((uint32_t)(n + 64 + 127) << 23)) * bits_to_float((uint32_t)(-64 + 127) << 23);
+}
+
+// 2^(hi + lo), |lo| <= ulp(hi)
+RT_HD float exp2_pair(float hi, float lo) {
+    if (hi >= 128.0f) return bits_to_float(0x7F800000u);
+    if (hi < -152.0f) return 0.0f;
+    const float n = __builtin_rintf(hi);
+    const float f = (hi - n) + lo;  // hi - n is exact
+    return scale2(exp2_core(f), (int)n);
+}
+
+// log2(x) = hi + lo for finite x > 0
+RT_HD void log2_pair(float x, float& hi, float& lo) {
+    uint32_t b = float_to_bits(x);
+    int e = 0;
+    if (b < 0x00800000u) {  // subnormal: scale by 2^23
+        x *= 8388608.0f;
+        b = float_to_bits(x);
+        e = -23;
+    }
+    e += (int)(b >> 23) - 127;
+    float m = bits_to_float((b & 0x007FFFFFu) | 0x3F800000u);  // [1, 2)
+    if (m > 1.41421354f) { m *= 0.5f; e += 1; }
+    const float r = m - 1.0f;  // exact
+    // ln(1 + r) = 2 atanh(s), s = r / (2 + r), s carried as s_hi + s_lo
+    const float d = 2.0f + r, dl = r - (d - 2.0f);  // 2 + r exactly as d + dl
+    const float s = r / d;
+    const float sl = (f_fma(-s, d, r) - s * dl) / d;
+    const float s2 = s * s;
+    float q = 1.0f / 13.0f;
+    q = f_fma(q, s2, 1.0f / 11.0f);
+    q = f_fma(q, s2, 1.0f / 9.0f);
+    q = f_fma(q, s2, 1.0f / 7.0f);
+    q = f_fma(q, s2, 1.0f / 5.0f);
+    q = f_fma(q, s2, 1.0f / 3.0f);
+    const float lnh = 2.0f * s;                       // exact
+    const float lnl = 2.0f * sl + (2.0f * s) * (s2 * q);
+    // times log2(e) = Lh + Ll, plus the exponent
+    const float Lh = 1.44269502162933349609f, Ll = 1.9259629911783e-08f;
+    const float ph = lnh * Lh;
+    const float pl = f_fma(lnh, Lh, -ph) + (f_fma(lnh, Ll, lnl * Lh));
+    const float fe = (float)e;
+    const float sh = fe + ph;
+    const float err = (fe - sh) + ph;  // |fe| >= 1 > |ph| or fe == 0: exact two-sum
+    hi = sh;
+    lo = err + pl;
+    const float t = hi + lo;  // renormalise
+    lo = lo - (t - hi);
+    hi = t;
+}
+}  // namespace rtm
+
+RT_HD float rt_exp2f(float x) {
+    if (x != x) return x;
+    return rtm::exp2_pair(x, 0.0f);
+}
+
+RT_HD float rt_expf(float x) {
+    if (x != x) return x;
+    if (x > 89.0f) return rtm::bits_to_float(0x7F800000u);
+    if (x < -104.0f) return 0.0f;
+    // Cody-Waite: x = n ln2 + r, ln2 = 0.693145752 (16 bits) + 1.42860677e-06
+    const float n = __builtin_rintf(x * 1.44269502162933349609f);
+    float r = rtm::f_fma(-n, 0.693145751953125f, x);
+    r = rtm::f_fma(-n, 1.428606765330187e-06f, r);
+    // e^r, |r| <= 0.35: Taylor to degree 8
+    float p = 2.4801587301587302e-05f;
+    p = rtm::f_fma(p, r, 1.9841269841269841e-04f);
+    p = rtm::f_fma(p, r, 1.3888888888888889e-03f);
+    p = rtm::f_fma(p, r, 8.3333333333333333e-03f);
+    p = rtm::f_fma(p, r, 4.1666666666666667e-02f);
+    p = rtm::f_fma(p, r, 1.6666666666666667e-01f);
+    p = rtm::f_fma(p, r, 0.5f);
+    p = rtm::f_fma(p, r, 1.0f);
+    p = rtm::f_fma(p, r, 1.0f);
+    return rtm::scale2(p, (int)n);
+}
+
+RT_HD float rt_log2f(float x) {
+    if (x != x) return x;
+    if (x < 0.0f) return rtm::bits_to_float(0x7FC00000u);
+    if (x == 0.0f) return rtm::bits_to_float(0xFF800000u);
+    if (x == rtm::bits_to_float(0x7F800000u)) return x;
+    float h, l;
+    rtm::log2_pair(x, h, l);
+    return h + l;
+}
+
+RT_HD float rt_logf(float x) {
+    if (x != x) return x;
+    if (x < 0.0f) return rtm::bits_to_float(0x7FC00000u);
+    if (x == 0.0f) return rtm::bits_to_float(0xFF800000u);
+    if (x == rtm::bits_to_float(0x7F800000u)) return x;
+    float h, l;
+    rtm::log2_pair(x, h, l);
+    // times ln2 = 0.693147182 + -1.90465421e-09
+    const float Nh = 0.693147182464599609375f, Nl = -1.904654212125e-09f;
+    const float ph = h * Nh;
+    return ph + (rtm::f_fma(h, Nh, -ph) + rtm::f_fma(h, Nl, l * Nh));
+}
 RT_HD float rt_log10f(float x) { return (float)(rtm::logd((double)x) * 0.43429448190325182765); }
 RT_HD float rt_sinf(float x) { double s, c; rtm::sincosd((double)x, s, c); return (float)s; }
 RT_HD float rt_cosf(float x) { double s, c; rtm::sincosd((double)x, s, c); return (float)c; }
@@ -271,7 +392,13 @@ RT_HD float rt_powf(float xf, float yf) {
         x = -x;
     }
     if (x == rtm::d_inf()) return (float)(sign * (y > 0 ? rtm::d_inf() : 0.0));
-    return (float)(sign * rtm::exp2d(y * rtm::log2d(x)));
+    // exp2(y log2 x) with log2 x as a float pair and the product's rounding error kept
+    float lh, ll;
+    rtm::log2_pair((float)x, lh, ll);
+    const float th = yf * lh;
+    const float tl = rtm::f_fma(yf, lh, -th) + yf * ll;
+    const float r = rtm::exp2_pair(th, tl);
+    return sign < 0.0 ? -r : r;
 }
 
 // IEEE float -> binary16, round to nearest even (matches __float2half_rn / v_cvt_f16_f32)

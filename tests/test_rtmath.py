@@ -55,3 +55,22 @@ def test_rtmath_special_cases(oracle):
     assert oracle.rtmath("log2", 8.0) == 3.0
     assert math.isinf(oracle.rtmath("log", 0.0)) and oracle.rtmath("log", 0.0) < 0
     assert oracle.rtmath("atan2", 0.0, -1.0) == np.float32(np.pi)
+
+
+def test_rtmath_float_pow_large_exponent(oracle):
+    """powf(x, 100) (the denoiser's normal weight): float-pair log2 keeps it within 2 ulp."""
+    rng = np.random.default_rng(11)
+    worst = 0
+    for x in rng.uniform(0, 1, 3000).astype(np.float32):
+        worst = max(worst, ulp_err(oracle.rtmath("pow", float(x), 100.0), np.float64(x) ** 100.0))
+    assert worst <= 2, worst
+
+
+def test_rtmath_subnormal_range(oracle):
+    rng = np.random.default_rng(5)
+    worst = 0
+    for x in rng.uniform(-149, -126, 2000).astype(np.float32):
+        worst = max(worst, ulp_err(oracle.rtmath("exp2", float(x)), np.exp2(np.float64(x))))
+    for x in (np.float32(2.0) ** rng.uniform(-149, -126, 2000)).astype(np.float32):
+        worst = max(worst, ulp_err(oracle.rtmath("log2", float(x)), np.log2(np.float64(x))))
+    assert worst <= 1, worst

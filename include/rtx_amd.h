@@ -109,6 +109,21 @@ typedef struct rt_camera {
 int rt_get_camera(const rt_context* ctx, rt_camera* out); /* RayTracer::GetCamera */
 int rt_set_camera(rt_context* ctx, const rt_camera* in);
 
+/* RayTracer::SaveCameraToFile / LoadCameraFromFile (inputControl.cu:115-149): the reference's
+ * 176-byte binary Camera record (kernel.cuh:78-100, derived fields included).  Loading takes
+ * pos, pitch, yaw, focal, aperture and fov.x from the record; the derived fields are recomputed
+ * by Camera::update every frame, as in the reference.  rt_init loads [file] inputCameraFileName
+ * when loadCameraAtInit is true (init.cu:433-435). */
+int rt_save_camera(const rt_context* ctx, const char* path);
+int rt_load_camera(rt_context* ctx, const char* path);
+
+/* Offscreen presentation (replaces the Vulkan swapchain blit, main.cu:1295-1310): the last
+ * frame's RGBA8 output as a binary PPM (P6, screen size), or the denoised pre-tone-map HDR
+ * colour as a PFM (PF, render size, bottom row first as the format prescribes). */
+#define RT_IMAGE_PPM_RGBA8 0
+#define RT_IMAGE_PFM_HDR 1
+int rt_save_image(rt_context* ctx, const char* path, int kind);
+
 /* Determinism hooks the reference lacks: the frame counter is a function static
  * (kernel.cu:64) and AutoExposure reads wall-clock deltaTime (postprocessing.cu:46-51). */
 int rt_set_frame_index(rt_context* ctx, int frame_num); /* next rt_draw renders this frameNum */

@@ -17,6 +17,10 @@
 //   BicubicScale                postprocessing.cuh:785-802 (SampleBicubicCatmullRom sampler.cuh:446-496)
 //   SharpeningFilter            postprocessing.cuh:726-783
 //   ToneMappingReinhardExtended postprocessing.cuh:542-564 (+ :488-516, luminance linearMath.h:746-749)
+//   ToneMappingACES / ACES2 / Uncharted postprocessing.cuh:566-708 (ACESFitted, ACESFilm, Mat3 *)
+//   BloomGuassian / Bloom       postprocessing.cuh:348-408
+//   LensFlare(Pred)             postprocessing.cuh:414-487, sunPos/sunUv kernel.cu:126-127,
+//                               predicate postprocessing.cu:88-94
 //   CopyToOutput                kernel.cu:26-59
 // Gaussian kernels gaussian.cuh:12-47; RgbToYcocg/YcocgToRgb temporalDenoising.cuh:10-21.
 //
@@ -566,18 +570,174 @@ void sharpen(const uint16_t* in, uint16_t* out, int W, int H) {
 
 float luminance(F3 v) { return dot(v, f3(0.2126f, 0.7152f, 0.0722f)); }
 
-void tonemap_reinhard_ext(uint16_t* buf, int W, int H, float exposure, const rt_post_process_params& pp) {
-    for (size_t p = 0; p < (size_t)W * H; ++p) {
-        F3 c = f3(h2f(buf[4 * p]), h2f(buf[4 * p + 1]), h2f(buf[4 * p + 2]));
-        c = c * exposure;
+// ToneMappingReinhardExtended / ACES (ACESFitted) / ACES2 (ACESFilm) / Uncharted, each
+// followed by the clamp3f(pow3f(color, 1 / gamma)) gamma step (postprocessing.cuh:488-708)
+F3 mat3_mul(const float m[9], F3 v) {  // Mat3 * Float3: rows (m00 m01 m02) ... via InnerProduct
+    return f3(inner3(m[0], v.x, m[1], v.y, m[2], v.z), inner3(m[3], v.x, m[4], v.y, m[5], v.z),
+              inner3(m[6], v.x, m[7], v.y, m[8], v.z));
+}
+
+F3 tonemap_color(F3 c, int type, const rt_post_process_params& pp) {
+    if (type == 3) {  // ReinhardExtendedLuminance
         const float lo = luminance(c);
         const float num = lo * (1.0f + (lo / (pp.maxWhite * pp.maxWhite)));
         const float ln = num / (1.0f + lo);
         c = c * (ln / luminance(c));
-        const float g = 1.0f / pp.gamma;
-        c = clamp3(f3(rt_powf(c.x, g), rt_powf(c.y, g), rt_powf(c.z, g)), f3(0.0f), f3(1.0f));
+    } else if (type == 1) {  // ACESFitted
+        const float in[9] = {(float)0.59719, (float)0.35458, (float)0.04823, (float)0.07600, (float)0.90834,
+                             (float)0.01566, (float)0.02840, (float)0.13383, (float)0.83777};
+        const float out[9] = {(float)1.60475, (float)-0.53108, (float)-0.07367, (float)-0.10208, (float)1.10813,
+                              (float)-0.00605, (float)-0.00327, (float)-0.07276, (float)1.07602};
+        c = mat3_mul(in, c);
+        const float lum = luminance(c);  // RRTAndODTFitLuminance
+        const float a = lum * (lum + 0.0245786f) - 0.000090537f;
+        const float b = lum * (0.983729f * lum + 0.4329510f) + 0.238081f;
+        c = c * ((a / b) / luminance(c));
+        c = mat3_mul(out, c);
+        c = clamp3(c, f3(0.0f), f3(1.0f));
+    } else if (type == 2) {  // ACESFilm
+        const float a = 2.51f, b = 0.03f, cc = 2.43f, d = 0.59f, e = 0.14f;
+        const F3 num = c * (c * a + b);
+        const F3 den = c * (c * cc + d) + e;
+        c = clamp3(num / den, f3(0.0f), f3(1.0f));
+    } else {  // Uncharted: Uncharted2Tonemap returns 0, so the white scale is 1/0
+        const F3 curr = f3(0.0f);
+        const F3 whiteScale = f3(1.0f / 0.0f);
+        c = curr * whiteScale;
+    }
+    const float g = 1.0f / pp.gamma;
+    return clamp3(f3(rt_powf(c.x, g), rt_powf(c.y, g), rt_powf(c.z, g)), f3(0.0f), f3(1.0f));
+}
+
+void tonemap(uint16_t* buf, int W, int H, float exposure, int type, const rt_post_process_params& pp) {
+    for (size_t p = 0; p < (size_t)W * H; ++p) {
+        F3 c = f3(h2f(buf[4 * p]), h2f(buf[4 * p + 1]), h2f(buf[4 * p + 2]));
+        c = tonemap_color(c * exposure, type, pp);
         buf[4 * p] = f2h(c.x); buf[4 * p + 1] = f2h(c.y); buf[4 * p + 2] = f2h(c.z); buf[4 * p + 3] = f2h(1.0f);
     }
+}
+
+// BloomGuassian: brightness key max(sqrt(lum^2 - brightLum), 0) (a NaN square root keys to 0),
+// then the 5x5 gaussian over the keyed texels, clamped reads
+void bloom_gauss(const uint16_t* in, int W, int H, uint16_t* out, float brightLum) {
+    std::vector<F3> keyed((size_t)W * H);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const H4 v = load_h4(in, W, H, x, y);
+            F3 c = f3(v.x, v.y, v.z);
+            const float lum = fmx(fmx(c.x, c.y), c.z);
+            const float s = sqrtf(lum * lum - brightLum);
+            c = c * (s > 0.0f ? s : 0.0f);
+            keyed[(size_t)y * W + x] = c;
+        }
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            F3 o = f3(0.0f);
+            float wsum = 0.0f;
+            for (int i = 0; i < 25; ++i) {
+                const int sx = clampi(x + i % 5 - 2, 0, W - 1), sy = clampi(y + i / 5 - 2, 0, H - 1);
+                const float g = (float)kG5[i];
+                o = o + keyed[(size_t)sy * W + sx] * g;
+                wsum += g;
+            }
+            o = o / wsum;
+            if (isnan3(o)) o = f3(0.0f);
+            uint16_t* q = out + ((size_t)y * W + x) * 4;
+            q[0] = f2h(o.x); q[1] = f2h(o.y); q[2] = f2h(o.z); q[3] = f2h(1.0f);
+        }
+}
+
+// SampleBicubicCatmullRom<Load2DFuncHalf4<Float3>> (sampler.cuh:446-496), clamped reads
+F3 catmull_rom(const uint16_t* in, int W, int H, F2 uv) {
+    const F2 UV = {uv.x * (float)W, uv.y * (float)H};
+    const float fx0 = floorf(UV.x - 0.5f), fy0 = floorf(UV.y - 0.5f);
+    const F2 f = {UV.x - (fx0 + 0.5f), UV.y - (fy0 + 0.5f)};
+    const F2 f2 = {f.x * f.x, f.y * f.y};
+    const F2 f3v = {f2.x * f.x, f2.y * f.y};
+    const F2 w0 = {f2.x - 0.5f * (f3v.x + f.x), f2.y - 0.5f * (f3v.y + f.y)};
+    const F2 w1 = {1.5f * f3v.x - 2.5f * f2.x + 1.0f, 1.5f * f3v.y - 2.5f * f2.y + 1.0f};
+    const F2 w3 = {0.5f * (f3v.x - f2.x), 0.5f * (f3v.y - f2.y)};
+    const F2 w2 = {1.0f - w0.x - w1.x - w3.x, 1.0f - w0.y - w1.y - w3.y};
+    const int t1x = (int)fx0, t1y = (int)fy0;
+    const float wx[4] = {w0.x, w1.x, w2.x, w3.x}, wy[4] = {w0.y, w1.y, w2.y, w3.y};
+    F3 o = f3(0.0f);
+    float sw = 0.0f;
+    for (int j = 0; j < 4; ++j)
+        for (int i = 0; i < 4; ++i) {
+            const float w = wx[i] * wy[j];
+            sw += w;
+            const H4 v = load_h4(in, W, H, t1x - 1 + i, t1y - 1 + j);
+            o = o + f3(v.x, v.y, v.z) * w;
+        }
+    return o / sw;
+}
+
+// Bloom: colour += (bloom4 + bloom16 sampled bicubically) * 0.05, alpha 1
+void bloom_apply(uint16_t* color, int W, int H, const uint16_t* b4, int W4, int H4, const uint16_t* b16, int W16,
+                 int H16) {
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            const F2 uv = {(float)x / W, (float)y / H};
+            const F3 s4 = catmull_rom(b4, W4, H4, uv), s16 = catmull_rom(b16, W16, H16, uv);
+            uint16_t* q = color + ((size_t)y * W + x) * 4;
+            F3 c = f3(h2f(q[0]), h2f(q[1]), h2f(q[2]));
+            c = c + (s4 + s16) * 0.05f;
+            if (isnan3(c)) c = f3(0.0f);
+            q[0] = f2h(c.x); q[1] = f2h(c.y); q[2] = f2h(c.z); q[3] = f2h(1.0f);
+        }
+}
+
+// ---- LensFlare (postprocessing.cuh:414-480)
+float lf_fract(float x) { return x - truncf(x); }  // modff: the signed fractional part
+float lf_rand(float w) { return lf_fract(rt_sinf(w) * 1000.0f); }
+float lf_len(F2 p) { return sqrtf(p.x * p.x + p.y * p.y); }
+float smoothstep1f(float a, float b, float w) { return a + (w * w * (3.0f - 2.0f * w)) * (b - a); }
+
+float lf_reg_shape(F2 p, int N) {
+    const float a = rt_atan2f(p.x, p.y) + 0.2f;
+    const float b = kTwoPi / float(N);
+    return smoothstep1f(0.5f, 0.51f, rt_cosf(floorf(0.5f + a / b) * b - a) * lf_len(p));
+}
+
+F3 lf_circle(F2 p, float size, float dist, F2 m) {
+    const float d4 = (float)((double)dist * 4.0);
+    const float l = lf_len(F2{p.x + m.x * d4, p.y + m.y * d4}) + size / 2.0f;
+    const float c = fmx(0.01f - rt_powf(lf_len(F2{p.x + m.x * dist, p.y + m.y * dist}), size * 1.4f), 0.0f) * 30.0f;
+    const float c1 = fmx(0.001f - rt_powf(l - 0.3f, 1.0f / 40.0f) + rt_sinf(l * 30.0f), 0.0f) * 3.0f;
+    const F2 md = {m.x * dist / 2.0f, m.y * dist / 2.0f};
+    const F2 q = {(p.x - md.x) + 0.09f, (p.y - md.y) + 0.09f};
+    const float c2 = fmx(0.04f / rt_powf(lf_len(q) * 1.0f, 1.0f), 0.0f) / 20.0f;
+    const F2 rp = {(p.x * 5.0f + (m.x * dist) * 5.0f) + 0.9f, (p.y * 5.0f + (m.y * dist) * 5.0f) + 0.9f};
+    const float sh = fmx(0.01f - rt_powf(lf_reg_shape(rp, 6), 1.0f), 0.0f) * 6.0f;
+    const F3 a = f3(0.44f * 8.0f + dist * 4.0f, 0.24f * 8.0f + dist * 4.0f, 0.2f * 8.0f + dist * 4.0f);
+    const F3 color = f3(rt_cosf(a.x) * 0.5f + 0.5f, rt_cosf(a.y) * 0.5f + 0.5f, rt_cosf(a.z) * 0.5f + 0.5f);
+    F3 f = color * c;
+    f = f + color * c1;
+    f = f + color * c2;
+    f = f + color * sh;
+    return f - 0.01f;
+}
+
+void lens_flare(uint16_t* color, int W, int H, F2 sunPos) {
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            F2 uv = {(float)x / (float)W, (float)y / (float)H};
+            uv = F2{uv.x - 0.5f, uv.y - 0.5f};
+            uv.x *= (float)W / (float)H;
+            const F2 vec = {uv.x - sunPos.x, uv.y - sunPos.y};
+            const float len = lf_len(vec);
+            uint16_t* q = color + ((size_t)y * W + x) * 4;
+            F3 c = f3(h2f(q[0]), h2f(q[1]), h2f(q[2]));
+            for (int i = 0; i < 2; ++i)
+                c = c + lf_circle(uv, rt_powf(lf_rand(i * 2000.0f) * 1.8f, 2.0f) + 1.41f,
+                                  lf_rand(i * 20.0f) * 3.0f + 0.2f - 0.5f, sunPos);
+            const float angle = rt_atan2f(vec.y, vec.x);
+            c = c + fmx(0.1f / fmx(rt_powf(len * 10.0f, 5.0f), 0.0001f), 0.0f) *
+                        fabsf(rt_sinf(angle * 5.0f + rt_cosf(angle * 9.0f))) / 20.0f;
+            c = c + (fmx(0.1f / rt_powf(len * 10.0f, 1.0f / 20.0f), 0.0f) +
+                     fabsf(rt_sinf(angle * 3.0f + rt_cosf(angle * 9.0f))) / 16.0f * fabsf(rt_sinf(angle * 9.0f)));
+            q[0] = f2h(c.x); q[1] = f2h(c.y); q[2] = f2h(c.z); q[3] = f2h(1.0f);
+        }
 }
 
 void copy_to_output(const uint16_t* scaled, int W, int H, int frameNum, const uint8_t* bn, uint8_t* rgba) {
@@ -606,8 +766,7 @@ extern "C" int orc_denoise_post(const OrcDrawIO* io) {
     const size_t P = (size_t)W * H;
     const rt_params& prm = *io->params;
     const rt_render_pass_settings& ps = prm.pass;
-    if (ps.enableBloomEffect || ps.enableLensFlare) return -1;
-    if (ps.enableToneMapping && prm.post.toneMappingType != 3) return -1;
+    if (ps.enableToneMapping && (prm.post.toneMappingType < 0 || prm.post.toneMappingType > 3)) return -1;
     Ctx c{W, H, io->frameNum, io->params, io->normal, io->albedo, io->depth, io->motion};
     OrcPostState& st = *io->state;
     std::vector<uint16_t> tmp(P * 4);
@@ -670,6 +829,18 @@ extern "C" int orc_denoise_post(const OrcDrawIO* io) {
             st.exposure[0] = prm.post.exposure;
             st.exposure[1] = st.exposure[2] = st.exposure[3] = 1.0f;
         }
+        if (ps.enableBloomEffect) {
+            std::vector<uint16_t> b4s((size_t)W4 * H4 * 4), b16s((size_t)W16 * H16 * 4);
+            uint16_t* b4 = io->bloom4 ? io->bloom4 : b4s.data();
+            uint16_t* b16 = io->bloom16 ? io->bloom16 : b16s.data();
+            bloom_gauss(io->c4, W4, H4, b4, st.exposure[2]);
+            bloom_gauss(io->c16, W16, H16, b16, st.exposure[2]);
+            bloom_apply(cur, W, H, b4, W4, H4, b16, W16, H16);
+        }
+        if (ps.enableLensFlare && io->lensFlare) {
+            const float d = h2f(io->depth[(size_t)io->sunUv[1] * W + io->sunUv[0]]);  // LensFlarePred
+            if (!(d < kRayMaxF)) lens_flare(cur, W, H, F2{io->sunPos[0], io->sunPos[1]});
+        }
     }
     bicubic_scale(cur, W, H, io->scaled, Ws, Hs);
     if (ps.enablePostProcess) {
@@ -678,8 +849,30 @@ extern "C" int orc_denoise_post(const OrcDrawIO* io) {
             sharpen(io->scaled, s2.data(), Ws, Hs);
             memcpy(io->scaled, s2.data(), s2.size() * 2);
         }
-        if (ps.enableToneMapping) tonemap_reinhard_ext(io->scaled, Ws, Hs, st.exposure[0], prm.post);
+        if (ps.enableToneMapping) tonemap(io->scaled, Ws, Hs, st.exposure[0], prm.post.toneMappingType, prm.post);
     }
     if (io->rgba) copy_to_output(io->scaled, Ws, Hs, io->frameNum, io->bluenoise, io->rgba);
     return 0;
+}
+
+extern "C" int orc_lens_flare_setup(const OrcCamera* cam, const float* sunDir, uint32_t W, uint32_t H, float* sunPos,
+                                    int* sunUv) {
+    Camera c;
+    camera_update(*cam, c);
+    const F3 sd = f3(sunDir[0], sunDir[1], sunDir[2]);
+    // Camera::WorldToScreenSpace(pos + sunDir) (kernel.cuh:123-131): rows of the transposed view
+    // matrix are left, up, dir
+    const F3 d = (c.pos + sd) - c.pos;
+    const F3 v = f3(dot(c.left, d), dot(c.up, d), dot(c.dir, d));
+    const F2 s = {v.x / v.z, v.y / v.z};
+    const F2 ndc = {s.x / c.tanHalfFov.x, s.y / c.tanHalfFov.y};
+    F2 sp = {0.5f - ndc.x * 0.5f, 0.5f - ndc.y * 0.5f};
+    sunUv[0] = (int)floorf(sp.x * (float)W);
+    sunUv[1] = (int)floorf(sp.y * (float)H);
+    const int on = sp.x > 0 && sp.x < 1 && sp.y > 0 && sp.y < 1 && sd.y > -0.0f && dot(sd, c.dir) > 0;
+    sp = F2{sp.x - 0.5f, sp.y - 0.5f};
+    sp.x *= (float)W / (float)H;
+    sunPos[0] = sp.x;
+    sunPos[1] = sp.y;
+    return on;
 }

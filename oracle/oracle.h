@@ -172,7 +172,17 @@ typedef struct OrcDrawIO {
     uint16_t* scaled;       // out [Ws*Hs][4] half (ScaledColorBuffer, tone mapped)
     uint8_t* rgba;          // out [Ws*Hs][4] (may be NULL)
     OrcPostState* state;
+    uint16_t* bloom4;       // out [ceil(W/4) * ceil(H/4)][4] half (BloomBuffer4; NULL: scratch)
+    uint16_t* bloom16;      // out [ceil(W/16) * ceil(H/16)][4] half (BloomBuffer16; NULL: scratch)
+    int lensFlare;          // the host-side lens-flare predicate held (orc_lens_flare_setup)
+    float sunPos[2];        // LensFlare's sun position (already centred and aspect-scaled)
+    int sunUv[2];           // render texel of the sun (LensFlarePred's depth test)
 } OrcDrawIO;
+
+// UpdateFrame's sunPos / sunUv (kernel.cu:126-127) and PostProcessing's lens-flare predicate
+// (postprocessing.cu:88-94).  Returns 1 when the lens flare pass is launched.
+int orc_lens_flare_setup(const OrcCamera* cam, const float* sunDir, uint32_t W, uint32_t H, float* sunPos,
+                         int* sunUv);
 
 // TemporalSpatialDenoising + PostProcessing + CopyToOutput; returns < 0 for unsupported settings
 int orc_denoise_post(const OrcDrawIO* io);

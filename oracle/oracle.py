@@ -217,6 +217,9 @@ def _bind_frame_api(L):
     L.orc_sky_radiance.restype = None
     L.orc_denoise_post.argtypes = [C.c_void_p]
     L.orc_denoise_post.restype = C.c_int
+    L.orc_lens_flare_setup.argtypes = [C.POINTER(CameraIn), C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p,
+                                       C.c_void_p]
+    L.orc_lens_flare_setup.restype = C.c_int
 
 
 def sky_tables() -> list:
@@ -348,7 +351,8 @@ class DrawIO(C.Structure):
                 ("color", C.c_void_p), ("normal", C.c_void_p), ("albedo", C.c_void_p), ("depth", C.c_void_p),
                 ("motion", C.c_void_p), ("noise8", C.c_void_p), ("noise16", C.c_void_p), ("c4", C.c_void_p),
                 ("c16", C.c_void_p), ("c64", C.c_void_p), ("histogram", C.c_void_p), ("scaled", C.c_void_p),
-                ("rgba", C.c_void_p), ("state", C.c_void_p)]
+                ("rgba", C.c_void_p), ("state", C.c_void_p), ("bloom4", C.c_void_p), ("bloom16", C.c_void_p),
+                ("lensFlare", C.c_int), ("sunPos", C.c_float * 2), ("sunUv", C.c_int * 2)]
 
 
 class Denoiser:
@@ -365,7 +369,9 @@ class Denoiser:
                                (C.c_float * 4)(1.0, 1.0, 1.0, 1.0))
         self.bn = bluenoise_tables()
 
-    def draw(self, g: dict, frame_num: int, params=None, delta_time: float = 1000.0 / 60.0) -> dict:
+    def draw(self, g: dict, frame_num: int, params=None, delta_time: float = 1000.0 / 60.0,
+             cam: CameraIn | None = None, sun_dir=None) -> dict:
+        """cam / sun_dir: the frame's camera and sun direction, needed only for the lens flare."""
         params = params if params is not None else default_params()
         W, H, Ws, Hs = self.W, self.H, self.Ws, self.Hs
         d = lambda n: (n + 3) // 4
@@ -385,7 +391,19 @@ class Denoiser:
                     out["noise16"].ctypes.data, out["c4"].ctypes.data, out["c16"].ctypes.data,
                     out["c64"].ctypes.data, out["histogram"].ctypes.data, out["scaled"].ctypes.data,
                     out["rgba"].ctypes.data, C.addressof(self.state))
+        out["bloom4"] = np.zeros((W4 * H4, 4), np.uint16)
+        out["bloom16"] = np.zeros((W16 * H16, 4), np.uint16)
+        io.bloom4, io.bloom16 = out["bloom4"].ctypes.data, out["bloom16"].ctypes.data
+        if params.enableLensFlare and cam is not None and sun_dir is not None:
+            sd = np.ascontiguousarray(sun_dir, np.float32)
+            sp, su = np.zeros(2, np.float32), np.zeros(2, np.int32)
+            io.lensFlare = lib().orc_lens_flare_setup(C.byref(cam), sd.ctypes.data, W, H, sp.ctypes.data,
+                                                      su.ctypes.data)
+            io.sunPos[:] = sp.tolist()
+            io.sunUv[:] = su.tolist()
         rc = lib().orc_denoise_post(C.byref(io))
+        out["lens_flare"] = int(io.lensFlare)
+        out["sun_uv"] = (int(io.sunUv[0]), int(io.sunUv[1]))
         if rc < 0:
             raise RuntimeError("orc_denoise_post: unsupported settings")
         out["exposure"] = np.array(self.state.exposure[:], np.float32)

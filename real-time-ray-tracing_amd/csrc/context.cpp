@@ -342,6 +342,10 @@ int rt_init(rt_context* ctx) {
     if ((rc = rt_frame_init(ctx)) != RT_OK) return rc;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     ctx->inited = true;
+    // CameraSetup (init.cu:433-435): a missing or short file leaves the default camera, and the
+    // reference only prints its error, so this is not an rt_init failure either
+    if (ctx->loadCameraAtInit && rt_load_camera(ctx, ctx->inputCameraFileName.c_str()) != RT_OK)
+        fprintf(stderr, "librtx: %s (default camera kept)\n", ctx->err.c_str());
     return RT_OK;
 }
 

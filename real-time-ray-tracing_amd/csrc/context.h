@@ -62,6 +62,8 @@ struct FrameResources {
     uint2* c4 = nullptr;
     uint2* c16 = nullptr;
     uint2* c64 = nullptr;
+    uint2* bloom4 = nullptr;       // BloomBuffer4 / BloomBuffer16 (postprocessing.cu:73-88)
+    uint2* bloom16 = nullptr;
     uint32_t* histogram = nullptr;
     float* exposure = nullptr;
     uint2* scaledA = nullptr;

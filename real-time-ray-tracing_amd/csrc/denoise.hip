@@ -655,6 +655,170 @@ RT_DEV uint2 bicubic_scale_px(const Img& im, int W, int H, int x, int y, int Ws,
     return pack_color(o, 0x3C00u);
 }
 
+// ---- tone mappers (postprocessing.cuh:488-708), each followed by the gamma step
+RT_DEV float luminance(F3 v) { return dot(v, f3(0.2126f, 0.7152f, 0.0722f)); }  // linearMath.h:746-749
+
+RT_DEV F3 mat3_mul(const float* m, F3 v) {  // Mat3 * Float3 (linearMath.h:533-538), rows via InnerProduct
+    return f3(inner3(m[0], v.x, m[1], v.y, m[2], v.z), inner3(m[3], v.x, m[4], v.y, m[5], v.z),
+              inner3(m[6], v.x, m[7], v.y, m[8], v.z));
+}
+
+__constant__ float cAcesIn[9] = {(float)0.59719, (float)0.35458, (float)0.04823, (float)0.07600, (float)0.90834,
+                                 (float)0.01566, (float)0.02840, (float)0.13383, (float)0.83777};
+__constant__ float cAcesOut[9] = {(float)1.60475, (float)-0.53108, (float)-0.07367, (float)-0.10208, (float)1.10813,
+                                  (float)-0.00605, (float)-0.00327, (float)-0.07276, (float)1.07602};
+
+RT_DEV F3 tonemap_color(F3 c, int type, float maxWhite, float gamma) {
+    if (type == 3) {  // ToneMappingReinhardExtended: ReinhardExtendedLuminance
+        const float lo = luminance(c);
+        const float num = lo * (1.0f + (lo / (maxWhite * maxWhite)));
+        const float ln = num / (1.0f + lo);
+        c = c * (ln / luminance(c));
+    } else if (type == 1) {  // ToneMappingACES: ACESFitted with RRTAndODTFitLuminance
+        c = mat3_mul(cAcesIn, c);
+        const float lum = luminance(c);
+        const float a = lum * (lum + 0.0245786f) - 0.000090537f;
+        const float b = lum * (0.983729f * lum + 0.4329510f) + 0.238081f;
+        c = c * ((a / b) / luminance(c));
+        c = mat3_mul(cAcesOut, c);
+        c = clamp3(c, f3(0.0f), f3(1.0f));
+    } else if (type == 2) {  // ToneMappingACES2: ACESFilm
+        const F3 num = c * (c * 2.51f + 0.03f);
+        const F3 den = c * (c * 2.43f + 0.59f) + 0.14f;
+        c = clamp3(num / den, f3(0.0f), f3(1.0f));
+    } else {  // ToneMappingUncharted: Uncharted2Tonemap returns 0, white scale 1/0
+        c = f3(0.0f) * f3(__builtin_inff());
+    }
+    const float g = 1.0f / gamma;
+    return clamp3(f3(rt_powf(c.x, g), rt_powf(c.y, g), rt_powf(c.z, g)), f3(0.0f), f3(1.0f));
+}
+
+// ---- BloomGuassian (postprocessing.cuh:348-388): a 16x16 workgroup keys a 16x16 tile
+// (2-texel apron, clamped reads) into LDS and its inner 12x12 threads take the 5x5 gaussian.
+__global__ __launch_bounds__(256) void k_bloom_gauss(const uint2* in, int W, int H, uint2* out, const float* exposure) {
+    __shared__ F3 sh[16][16];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int x = blockIdx.x * 12 + tx - 2, y = blockIdx.y * 12 + ty - 2;
+    const View2 im{in, W, H};
+    F3 c = rgb_of(im.at(x, y));
+    const float lum = fmx(fmx(c.x, c.y), c.z);
+    const float sq = __builtin_sqrtf(lum * lum - exposure[2]);
+    c = c * (sq > 0.0f ? sq : 0.0f);  // max(sqrtf(.), 0.0): a NaN root keys to 0
+    sh[tx][ty] = c;
+    __syncthreads();
+    if (tx < 2 || ty < 2 || tx > 13 || ty > 13 || x >= W || y >= H) return;
+    F3 o = f3(0.0f);
+    float wsum = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 25; ++i) {
+        o = o + sh[tx + i % 5 - 2][ty + i / 5 - 2] * cG5[i];
+        wsum += cG5[i];
+    }
+    o = o / wsum;
+    if (isnan3(o)) o = f3(0.0f);
+    out[(size_t)y * W + x] = pack_color(o, 0x3C00u);
+}
+
+// SampleBicubicCatmullRom<Load2DFuncHalf4<Float3>> (sampler.cuh:446-496)
+RT_DEV F3 catmull_rom(const View2& im, F2 uv) {
+    const F2 UV = {uv.x * (float)im.W, uv.y * (float)im.H};
+    const float fx0 = floorf(UV.x - 0.5f), fy0 = floorf(UV.y - 0.5f);
+    const F2 f = {UV.x - (fx0 + 0.5f), UV.y - (fy0 + 0.5f)};
+    const F2 f2 = {f.x * f.x, f.y * f.y};
+    const F2 f3v = {f2.x * f.x, f2.y * f.y};
+    const F2 w0 = {f2.x - 0.5f * (f3v.x + f.x), f2.y - 0.5f * (f3v.y + f.y)};
+    const F2 w1 = {1.5f * f3v.x - 2.5f * f2.x + 1.0f, 1.5f * f3v.y - 2.5f * f2.y + 1.0f};
+    const F2 w3 = {0.5f * (f3v.x - f2.x), 0.5f * (f3v.y - f2.y)};
+    const F2 w2 = {1.0f - w0.x - w1.x - w3.x, 1.0f - w0.y - w1.y - w3.y};
+    const int t1x = (int)fx0, t1y = (int)fy0;
+    const float wx[4] = {w0.x, w1.x, w2.x, w3.x}, wy[4] = {w0.y, w1.y, w2.y, w3.y};
+    F3 o = f3(0.0f);
+    float sw = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float w = wx[i] * wy[j];
+            sw += w;
+            o = o + rgb_of(im.at(t1x - 1 + i, t1y - 1 + j)) * w;
+        }
+    return o / sw;
+}
+
+// Bloom (postprocessing.cuh:390-408), out of place: `in` may be the next frame's history
+__global__ __launch_bounds__(256) void k_bloom_apply(DenoisePostParams P, const uint2* in, uint2* out) {
+    const int W = (int)P.W, H = (int)P.H;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const int W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16 = (W4 + 3) / 4, H16 = (H4 + 3) / 4;
+    const F2 uv = {(float)x / W, (float)y / H};
+    const F3 s4 = catmull_rom(View2{P.bloom4, W4, H4}, uv), s16 = catmull_rom(View2{P.bloom16, W16, H16}, uv);
+    const size_t p = (size_t)y * W + x;
+    F3 c = rgb_of(in[p]);
+    c = c + (s4 + s16) * 0.05f;
+    if (isnan3(c)) c = f3(0.0f);
+    out[p] = pack_color(c, 0x3C00u);
+}
+
+// ---- LensFlare (postprocessing.cuh:414-480); LensFlarePred's depth test runs per thread
+RT_DEV float lf_len(F2 p) { return __builtin_sqrtf(p.x * p.x + p.y * p.y); }
+RT_DEV float lf_rand(float w) {  // fract(sinf(w) * 1000) with modff: the signed fractional part
+    const float v = rt_sinf(w) * 1000.0f;
+    return v - truncf(v);
+}
+RT_DEV float lf_reg_shape(F2 p, int N) {
+    const float a = rt_atan2f(p.x, p.y) + 0.2f;
+    const float b = kTwoPi / float(N);
+    const float w = rt_cosf(floorf(0.5f + a / b) * b - a) * lf_len(p);
+    return 0.5f + (w * w * (3.0f - 2.0f * w)) * (0.51f - 0.5f);  // smoothstep1f (linearMath.h:494)
+}
+RT_DEV F3 lf_circle(F2 p, float size, float dist, F2 m) {
+    const float d4 = (float)((double)dist * 4.0);
+    const float l = lf_len(F2{p.x + m.x * d4, p.y + m.y * d4}) + size / 2.0f;
+    const float c = fmx(0.01f - rt_powf(lf_len(F2{p.x + m.x * dist, p.y + m.y * dist}), size * 1.4f), 0.0f) * 30.0f;
+    const float c1 = fmx(0.001f - rt_powf(l - 0.3f, 1.0f / 40.0f) + rt_sinf(l * 30.0f), 0.0f) * 3.0f;
+    const F2 md = {m.x * dist / 2.0f, m.y * dist / 2.0f};
+    const float c2 = fmx(0.04f / rt_powf(lf_len(F2{(p.x - md.x) + 0.09f, (p.y - md.y) + 0.09f}) * 1.0f, 1.0f), 0.0f) / 20.0f;
+    const F2 rp = {(p.x * 5.0f + (m.x * dist) * 5.0f) + 0.9f, (p.y * 5.0f + (m.y * dist) * 5.0f) + 0.9f};
+    const float sh = fmx(0.01f - rt_powf(lf_reg_shape(rp, 6), 1.0f), 0.0f) * 6.0f;
+    const F3 a = f3(0.44f * 8.0f + dist * 4.0f, 0.24f * 8.0f + dist * 4.0f, 0.2f * 8.0f + dist * 4.0f);
+    const F3 color = f3(rt_cosf(a.x) * 0.5f + 0.5f, rt_cosf(a.y) * 0.5f + 0.5f, rt_cosf(a.z) * 0.5f + 0.5f);
+    F3 f = color * c;
+    f = f + color * c1;
+    f = f + color * c2;
+    f = f + color * sh;
+    return f - 0.01f;
+}
+
+__global__ __launch_bounds__(256) void k_lens_flare(DenoisePostParams P, const uint2* in, uint2* out) {
+    const int W = (int)P.W, H = (int)P.H;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const size_t p = (size_t)y * W + x;
+    const float sunDepth = h2f(P.depth[(size_t)P.sunUv[1] * W + P.sunUv[0]]);
+    if (sunDepth < kRayMaxF) {  // the sun is behind geometry: LensFlarePred launches nothing
+        if (in != out) out[p] = in[p];
+        return;
+    }
+    const F2 sunPos = {P.sunPos[0], P.sunPos[1]};
+    F2 uv = {(float)x / (float)W, (float)y / (float)H};
+    uv = F2{uv.x - 0.5f, uv.y - 0.5f};
+    uv.x *= (float)W / (float)H;
+    const F2 vec = {uv.x - sunPos.x, uv.y - sunPos.y};
+    const float len = lf_len(vec);
+    F3 c = rgb_of(in[p]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+        c = c + lf_circle(uv, rt_powf(lf_rand(i * 2000.0f) * 1.8f, 2.0f) + 1.41f, lf_rand(i * 20.0f) * 3.0f + 0.2f - 0.5f,
+                          sunPos);
+    const float angle = rt_atan2f(vec.y, vec.x);
+    c = c + fmx(0.1f / fmx(rt_powf(len * 10.0f, 5.0f), 0.0001f), 0.0f) *
+                fabsf(rt_sinf(angle * 5.0f + rt_cosf(angle * 9.0f))) / 20.0f;
+    c = c + (fmx(0.1f / rt_powf(len * 10.0f, 1.0f / 20.0f), 0.0f) +
+             fabsf(rt_sinf(angle * 3.0f + rt_cosf(angle * 9.0f))) / 16.0f * fabsf(rt_sinf(angle * 9.0f)));
+    out[p] = pack_color(c, 0x3C00u);
+}
+
 // BicubicScale, SharpeningFilter (FidelityFX CAS), the selected tone mapper and CopyToOutput's
 // dither in one pass.  Each workgroup evaluates the scaled image over its 16x16 screen tile and
 // a 1-pixel apron into LDS, rounded to half exactly as the reference stores ScaledColorBuffer;
@@ -720,15 +884,8 @@ __global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const u
         o = o / (f3(1.0f) + f3(4.0f) * w);
         cur = pack_color(o, 0x3C00u);
     }
-    if (P.tonemap) {  // ToneMappingReinhardExtended
-        F3 c = rgb_of(cur) * P.exposure[0];
-        const F3 wl = f3(0.2126f, 0.7152f, 0.0722f);
-        const float lo = dot(c, wl);
-        const float num = lo * (1.0f + (lo / (P.maxWhite * P.maxWhite)));
-        const float ln = num / (1.0f + lo);
-        c = c * (ln / dot(c, wl));
-        const float g = 1.0f / P.gamma;
-        c = clamp3(f3(rt_powf(c.x, g), rt_powf(c.y, g), rt_powf(c.z, g)), f3(0.0f), f3(1.0f));
+    if (P.tonemap) {
+        const F3 c = tonemap_color(rgb_of(cur) * P.exposure[0], P.toneMappingType, P.maxWhite, P.gamma);
         cur = pack_color(c, 0x3C00u);
     }
     P.scaledB[p] = cur;
@@ -865,6 +1022,26 @@ extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
         hipLaunchKernelGGL(k_auto_exposure, dim3(1), dim3(64), 0, s, P->exposure, (const uint32_t*)P->histogram,
                            (float)(W64 * H64), P->deltaTime, P->gain, P->autoExposure, P->fixedExposure);
         LAUNCH_CHECK();
+        // Bloom and LensFlare modify RenderColorBuffer, which here may be the next frame's
+        // history (TemporalFilter2's output): both write a colour buffer instead.
+        uint2* post = cur == P->colorA ? P->colorB : P->colorA;
+        if (P->bloom) {
+            hipLaunchKernelGGL(k_bloom_gauss, dim3((W4 + 11) / 12, (H4 + 11) / 12), b256, 0, s, (const uint2*)P->c4, W4,
+                               H4, P->bloom4, (const float*)P->exposure);
+            LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_bloom_gauss, dim3((W16b + 11) / 12, (H16b + 11) / 12), b256, 0, s,
+                               (const uint2*)P->c16, W16b, H16b, P->bloom16, (const float*)P->exposure);
+            LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_bloom_apply, g16, b256, 0, s, *P, (const uint2*)cur, post);
+            LAUNCH_CHECK();
+            cur = post;
+        }
+        if (P->lensFlare) {
+            hipLaunchKernelGGL(k_lens_flare, g16, b256, 0, s, *P, (const uint2*)cur, post);
+            LAUNCH_CHECK();
+            cur = post;
+        }
+        P->finalColor = cur;
     }
     DenoisePostParams Q = *P;
     Q.sharpen = P->postProcess && P->sharpen;

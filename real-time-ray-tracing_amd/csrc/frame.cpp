@@ -231,6 +231,8 @@ int rt_frame_init(rt_context* ctx) {
     ALLOC(fr.c4, W4 * H4 * 8);
     ALLOC(fr.c16, W16 * H16 * 8);
     ALLOC(fr.c64, ((W16 + 3) / 4) * ((H16 + 3) / 4) * 8);
+    ALLOC(fr.bloom4, W4 * H4 * 8);
+    ALLOC(fr.bloom16, W16 * H16 * 8);
     ALLOC(fr.histogram, 256);
     ALLOC(fr.exposure, 16);
     const size_t Ps = (size_t)ctx->screenW * ctx->screenH;
@@ -356,12 +358,9 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     if (!ctx || frame_num < 1) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_denoise_post before rt_init"; return RT_ERR_STATE; }
     const rt_render_pass_settings& ps = ctx->params.pass;
-    if (ps.enableBloomEffect || ps.enableLensFlare) {
-        ctx->err = "bloom / lens flare passes are not part of this build (off by default, settingParams.h:96-97)";
-        return RT_ERR_ARG;
-    }
-    if (ps.enablePostProcess && ps.enableToneMapping && ctx->params.post.toneMappingType != 3) {
-        ctx->err = "only the default tone mapper (Reinhard extended, type 3) is built";
+    if (ps.enablePostProcess && ps.enableToneMapping &&
+        (ctx->params.post.toneMappingType < 0 || ctx->params.post.toneMappingType > 3)) {
+        ctx->err = "toneMappingType must be 0 (Uncharted), 1 (ACES1), 2 (ACES2) or 3 (Reinhard)";
         return RT_ERR_ARG;
     }
     FrameResources& fr = ctx->fr;
@@ -416,6 +415,40 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.rgba = fr.rgba;
     p.bluenoise = ctx->dBlueNoise;
     p.hdrOut = with_hdr ? fr.hdr : nullptr;
+    p.bloom = ps.enablePostProcess && ps.enableBloomEffect;
+    p.toneMappingType = ctx->params.post.toneMappingType;
+    p.bloom4 = fr.bloom4;
+    p.bloom16 = fr.bloom16;
+    p.lensFlare = 0;
+    p.sunPos[0] = p.sunPos[1] = 0.0f;
+    p.sunUv[0] = p.sunUv[1] = 0;
+    if (ps.enablePostProcess && ps.enableLensFlare) {
+        // UpdateFrame's sunPos / sunUv (kernel.cu:126-127): Camera::WorldToScreenSpace(pos + sunDir)
+        HostCamera hc;
+        rt_camera_update(ctx->camera, ctx->renderW, ctx->renderH, hc);
+        const V3 pos = v3(hc.pos[0], hc.pos[1], hc.pos[2]);
+        const V3 sd = v3(fr.sunDir[0], fr.sunDir[1], fr.sunDir[2]);
+        const V3 w = pos + sd;
+        const V3 d = v3(w.x - pos.x, w.y - pos.y, w.z - pos.z);
+        const V3 vs = v3(dot(v3(hc.left[0], hc.left[1], hc.left[2]), d), dot(v3(hc.up[0], hc.up[1], hc.up[2]), d),
+                         dot(v3(hc.dir[0], hc.dir[1], hc.dir[2]), d));
+        const float sx = vs.x / vs.z, sy = vs.y / vs.z;
+        const float nx = sx / hc.tanHalfFov[0], ny = sy / hc.tanHalfFov[1];
+        float px = 0.5f - nx * 0.5f, py = 0.5f - ny * 0.5f;
+        const int ux = (int)floorf(px * (float)ctx->renderW), uy = (int)floorf(py * (float)ctx->renderH);
+        // PostProcessing's predicate (postprocessing.cu:90)
+        if (px > 0 && px < 1 && py > 0 && py < 1 && sd.y > -0.0f &&
+            dot(sd, v3(hc.dir[0], hc.dir[1], hc.dir[2])) > 0) {
+            px -= 0.5f;
+            py -= 0.5f;
+            px *= (float)ctx->renderW / (float)ctx->renderH;
+            p.lensFlare = 1;
+            p.sunPos[0] = px;
+            p.sunPos[1] = py;
+            p.sunUv[0] = ux;
+            p.sunUv[1] = uy;
+        }
+    }
     HIP_TRY(ctx, rtk_denoise_post(&p, ctx->stream));
     if (p.temporal2) std::swap(fr.histColor, fr.histColorAlt);
     fr.renderColor = p.finalColor;
@@ -517,3 +550,96 @@ int rt_get_buffer(const rt_context* cctx, int name, void* dst, size_t bytes) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- camera file I/O, image dumps
+namespace {
+// Camera (kernel.cuh:78-100), __align__(16): the reference's on-disk record
+struct CameraRecord {
+    float pos[3], pitch;
+    float dir[3], focal;
+    float left[3], aperture;
+    float up[3], yaw;
+    float resolution[2], inversedResolution[2];
+    float fov[2], tanHalfFov[2];
+    float adjustedLeft[3], unused3;
+    float adjustedUp[3], unused4;
+    float adjustedFront[3], unused5;
+    float apertureLeft[3], unused6;
+    float apertureUp[3], unused7;
+};
+static_assert(sizeof(CameraRecord) == 176, "Camera record layout");
+}  // namespace
+
+extern "C" int rt_save_camera(const rt_context* cctx, const char* path) {
+    rt_context* ctx = const_cast<rt_context*>(cctx);
+    if (!ctx || !path || !*path) return RT_ERR_ARG;
+    HostCamera hc;
+    rt_camera_update(ctx->camera, ctx->renderW, ctx->renderH, hc);
+    CameraRecord r{};
+    memcpy(r.pos, hc.pos, 12);
+    r.pitch = hc.pitch;
+    memcpy(r.dir, hc.dir, 12);
+    r.focal = hc.focal;
+    memcpy(r.left, hc.left, 12);
+    r.aperture = hc.aperture;
+    memcpy(r.up, hc.up, 12);
+    r.yaw = hc.yaw;
+    memcpy(r.resolution, hc.res, 8);
+    memcpy(r.inversedResolution, hc.invRes, 8);
+    memcpy(r.fov, hc.fov, 8);
+    memcpy(r.tanHalfFov, hc.tanHalfFov, 8);
+    memcpy(r.adjustedLeft, hc.adjustedLeft, 12);
+    memcpy(r.adjustedUp, hc.adjustedUp, 12);
+    memcpy(r.adjustedFront, hc.adjustedFront, 12);
+    memcpy(r.apertureLeft, hc.apertureLeft, 12);
+    memcpy(r.apertureUp, hc.apertureUp, 12);
+    std::ofstream f(path, std::ios::binary | std::ios::trunc);
+    if (!f) { ctx->err = std::string("cannot write camera file ") + path; return RT_ERR_IO; }
+    f.write(reinterpret_cast<const char*>(&r), sizeof(r));
+    return f ? RT_OK : RT_ERR_IO;
+}
+
+extern "C" int rt_load_camera(rt_context* ctx, const char* path) {
+    if (!ctx || !path || !*path) return RT_ERR_ARG;
+    std::ifstream f(path, std::ios::binary);
+    CameraRecord r{};
+    if (!f || !f.read(reinterpret_cast<char*>(&r), sizeof(r))) {
+        ctx->err = std::string("cannot read camera file ") + path;
+        return RT_ERR_IO;
+    }
+    memcpy(ctx->camera.pos, r.pos, 12);
+    ctx->camera.pitch = r.pitch;
+    ctx->camera.yaw = r.yaw;
+    ctx->camera.focal = r.focal;
+    ctx->camera.aperture = r.aperture;
+    ctx->camera.fovX = r.fov[0];
+    return RT_OK;
+}
+
+extern "C" int rt_save_image(rt_context* ctx, const char* path, int kind) {
+    if (!ctx || !path || !*path || (kind != RT_IMAGE_PPM_RGBA8 && kind != RT_IMAGE_PFM_HDR)) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_save_image before rt_init"; return RT_ERR_STATE; }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    std::ofstream f(path, std::ios::binary | std::ios::trunc);
+    if (!f) { ctx->err = std::string("cannot write image ") + path; return RT_ERR_IO; }
+    if (kind == RT_IMAGE_PPM_RGBA8) {
+        const size_t n = (size_t)ctx->screenW * ctx->screenH;
+        std::vector<uint8_t> rgba(n * 4), rgb(n * 3);
+        HIP_TRY(ctx, hipMemcpy(rgba.data(), ctx->fr.rgba, n * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; ++i) memcpy(&rgb[3 * i], &rgba[4 * i], 3);
+        f << "P6\n" << ctx->screenW << " " << ctx->screenH << "\n255\n";
+        f.write(reinterpret_cast<const char*>(rgb.data()), (std::streamsize)rgb.size());
+    } else {
+        const int W = ctx->renderW, H = ctx->renderH;
+        std::vector<uint16_t> c((size_t)W * H * 4);
+        HIP_TRY(ctx, hipMemcpy(c.data(), ctx->fr.renderColor, c.size() * 2, hipMemcpyDeviceToHost));
+        std::vector<float> rgb((size_t)W * H * 3);
+        for (int y = 0; y < H; ++y)  // PFM rows run bottom to top
+            for (int x = 0; x < W; ++x)
+                for (int k = 0; k < 3; ++k)
+                    rgb[((size_t)(H - 1 - y) * W + x) * 3 + k] = rt_h2f(c[((size_t)y * W + x) * 4 + k]);
+        f << "PF\n" << W << " " << H << "\n-1.0\n";  // negative scale: little endian
+        f.write(reinterpret_cast<const char*>(rgb.data()), (std::streamsize)(rgb.size() * 4));
+    }
+    return f ? RT_OK : RT_ERR_IO;
+}

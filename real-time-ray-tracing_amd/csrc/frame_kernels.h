@@ -125,6 +125,12 @@ struct DenoisePostParams {
     float deltaTime;            // ms
     int temporal, localSpatial, visualize, wideSpatial, temporal2;   // RenderPassSettings
     int postProcess, downScale, histogramOn, autoExposure, sharpen, tonemap;
+    int bloom, lensFlare;       // enableBloomEffect; lens-flare pass launched (host predicate)
+    int toneMappingType;        // ToneMappingType: 0 Uncharted, 1 ACES1, 2 ACES2, 3 Reinhard (extended)
+    float sunPos[2];            // LensFlare's sun position (centred, aspect-scaled)
+    int sunUv[2];               // render texel whose depth gates the lens flare (LensFlarePred)
+    uint2* bloom4;              // BloomBuffer4 / BloomBuffer16 (half4)
+    uint2* bloom16;
     float gain, fixedExposure, maxWhite, gamma;                      // PostProcessParams
     rt_denoising_params dn;
     uint2* colorA;              // path-trace colour in; ping-pong pair

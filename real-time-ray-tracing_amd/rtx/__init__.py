@@ -110,7 +110,11 @@ SIGNATURES = {
     "rt_time_stage": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float)]),
     "rt_download": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     "rt_array_bytes": (C.c_size_t, [C.c_void_p, C.c_int]),
+    "rt_save_camera": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "rt_load_camera": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "rt_save_image": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
 }
+IMAGE_PPM_RGBA8, IMAGE_PFM_HDR = 0, 1
 
 _lib = None
 
@@ -136,11 +140,15 @@ class RtError(RuntimeError):
 
 
 def write_config(path: str, width: int, height: int, dynamic: bool = False, chunk_dim: int = 1, spp: int = 1,
-                 extra: str = "", max_size=(3840, 2160)) -> str:
+                 extra: str = "", max_size=(3840, 2160), camera_file: str | None = None) -> str:
     """Write a config.toml with the reference's three tables (resources/config.toml) + extensions."""
     with open(path, "w") as f:
         f.write("[resolution]\nwidth = %d\nheight = %d\n\n" % (width, height))
-        f.write("[file]\nloadCameraAtInit = false\n\n")
+        if camera_file:
+            f.write('[file]\nloadCameraAtInit = true\ninputCameraFileName = "%s"\ncameraSaveFileName = "%s"\n\n'
+                    % (camera_file, camera_file))
+        else:
+            f.write("[file]\nloadCameraAtInit = false\n\n")
         f.write("[optimziation]\nuseDynamicResolution = %s\ntargetFps = 60.0\nmaxWidth = %d\nmaxHeight = %d\n"
                 "minWidth = 640\nminHeight = 480\n\n" % ("true" if dynamic else "false", max_size[0], max_size[1]))
         f.write("[scene]\nchunkDim = %d\n\n[render]\nspp = %d\n" % (chunk_dim, spp))
@@ -248,6 +256,16 @@ class RayTracer:
         ms = C.c_float()
         self._check(self.lib.rt_time_stage(self.h, stage, iters, C.byref(ms)), "rt_time_stage")
         return ms.value
+
+    # ---- camera file I/O and offscreen image dumps
+    def save_camera(self, path: str):
+        self._check(self.lib.rt_save_camera(self.h, path.encode()), "rt_save_camera")
+
+    def load_camera(self, path: str):
+        self._check(self.lib.rt_load_camera(self.h, path.encode()), "rt_load_camera")
+
+    def save_image(self, path: str, kind: int = IMAGE_PPM_RGBA8):
+        self._check(self.lib.rt_save_image(self.h, path.encode(), kind), "rt_save_image")
 
     # ---- downloads
     def download(self, name: str, dtype=np.uint8) -> np.ndarray:

@@ -78,3 +78,33 @@ def test_init_without_gpu_reports_no_device(rtx, tmp_path):
     with pytest.raises(rtx.RtError, match="RT_ERR_NO_DEVICE"):
         rt.init()
     rt.cleanup()
+
+
+def test_camera_file_round_trip(rtx, tmp_path):
+    """SaveCameraToFile / LoadCameraFromFile (inputControl.cu:115-149): the reference's 176-byte
+    Camera record, pos/pitch/dir/focal/left/aperture/up/yaw/resolution/... in struct order."""
+    import numpy as np
+    cfg = rtx.write_config(str(tmp_path / "c.toml"), 320, 180)
+    a = rtx.RayTracer(320, 180, cfg)
+    cam = a.camera
+    cam.pos[:] = (1.5, 7.25, -3.0)
+    cam.yaw, cam.pitch, cam.focal, cam.aperture, cam.fovX = 0.3, -0.2, 4.0, 0.01, 1.2
+    a.camera = cam
+    path = str(tmp_path / "camera.bin")
+    a.save_camera(path)
+    rec = np.fromfile(path, np.float32)
+    assert rec.size == 44
+    assert list(rec[0:3]) == [1.5, 7.25, -3.0] and rec[3] == np.float32(-0.2)  # pos, pitch
+    assert rec[7] == np.float32(4.0) and rec[11] == np.float32(0.01) and rec[15] == np.float32(0.3)
+    assert list(rec[16:18]) == [320.0, 180.0] and rec[20] == np.float32(1.2)  # resolution, fov.x
+    d = rec[4:7]  # Camera::update: dir = (sin yaw cos pitch, sin pitch, cos yaw cos pitch)
+    assert np.allclose(d, [np.sin(0.3) * np.cos(-0.2), np.sin(-0.2), np.cos(0.3) * np.cos(-0.2)], atol=1e-6)
+    b = rtx.RayTracer(320, 180, cfg)
+    b.load_camera(path)
+    cb = b.camera
+    assert list(cb.pos) == list(cam.pos) and (cb.yaw, cb.pitch, cb.focal, cb.aperture, cb.fovX) == (
+        cam.yaw, cam.pitch, cam.focal, cam.aperture, cam.fovX)
+    with pytest.raises(rtx.RtError, match="RT_ERR_IO"):
+        b.load_camera(str(tmp_path / "nope.bin"))
+    a.cleanup()
+    b.cleanup()

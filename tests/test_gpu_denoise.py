@@ -50,7 +50,7 @@ def assert_state(g, o, dn):
 
 
 def run_sequence(rtx, oracle, tmp_path, default_scene, w, h, frames, spp=1, extra="", params_fn=None, ws=None,
-                 hs=None, dynamic=False):
+                 hs=None, dynamic=False, cam_list=None, expect_flare=None):
     ws, hs = ws or w, hs or h
     s, tex = oracle.sky(), oracle.textures()
     if dynamic:
@@ -67,7 +67,7 @@ def run_sequence(rtx, oracle, tmp_path, default_scene, w, h, frames, spp=1, extr
         params_fn(p, op)
         rt.params = p
     dn = oracle.Denoiser(w, h, ws, hs)
-    cs = cams(rtx, oracle, w, h, frames)
+    cs = cam_list or cams(rtx, oracle, w, h, frames)
     for f in range(1, frames + 1):
         oc, rc = cs[f - 1]
         rt.camera = rc
@@ -79,7 +79,11 @@ def run_sequence(rtx, oracle, tmp_path, default_scene, w, h, frames, spp=1, extr
         hist_cam = cs[f - 2][0] if f > 1 else oc
         gb = oracle.pathtrace(default_scene["bvh"], w, h, frame_num=f, spp=spp, cam=oc, hist_cam=hist_cam,
                               sky_out=s, tex=tex)
-        o = dn.draw(gb, f, params=op, delta_time=DT)
+        o = dn.draw(gb, f, params=op, delta_time=DT, cam=oc, sun_dir=s["sun_dir"])
+        if expect_flare is not None:  # the predicate held and the sun's texel is sky (the pass ran)
+            assert o["lens_flare"] == expect_flare
+            ux, uy = o["sun_uv"]
+            assert gb["depth"].reshape(h, w)[uy, ux] == 0x7C00
         assert_state(g, o, dn)
     rt.cleanup()
     return g
@@ -135,3 +139,71 @@ def test_draw_1080p_4spp(rtx, oracle, tmp_path, default_scene):
         got = hdr.reshape(-1, 4)[:, :3]
         assert np.array_equal(got, ref)  # bit-exact (the north-star bar is 1e-3 relative L2)
     rt.cleanup()
+
+
+@pytest.mark.parametrize("tm", [0, 1, 2])
+def test_denoise_post_tone_mappers(rtx, oracle, tmp_path, default_scene, tm):
+    """ToneMappingType Uncharted (0, NaN by construction in the reference), ACES1 (1, ACESFitted
+    with the sRGB->AP1 matrices), ACES2 (2, ACESFilm); Reinhard (3) is the default everywhere else."""
+    def tweak(p, op):
+        p.post.toneMappingType = tm
+        op.toneMappingType = tm
+    run_sequence(rtx, oracle, tmp_path, default_scene, 128, 72, 2, params_fn=tweak)
+
+
+def sun_cams(rtx, oracle, w, h, n):
+    """Cameras above the terrain looking just below the sun, so it sits in the upper half of the view."""
+    import math
+    sd = oracle.sky()["sun_dir"].astype(np.float64)
+    yaw, pitch = math.atan2(sd[0], sd[2]), math.asin(sd[1]) - 0.25
+    return [terrain_camera(rtx, oracle, w, h, pos=(8.0 + 0.1 * k, 15.0, -6.0), yaw=yaw + 0.01 * k, pitch=pitch)
+            for k in range(n)]
+
+
+def test_denoise_post_bloom_lens_flare(rtx, oracle, tmp_path, default_scene):
+    """The off-by-default post passes: BloomGuassian on the 1/4 and 1/16 chains + Bloom, and the
+    lens flare (host sun projection + LensFlarePred's depth test at the sun's texel)."""
+    def tweak(p, op):
+        p.pass_.enableBloomEffect = 1
+        p.pass_.enableLensFlare = 1
+        op.enableBloomEffect = 1
+        op.enableLensFlare = 1
+    w, h = 160, 96
+    run_sequence(rtx, oracle, tmp_path, default_scene, w, h, 2, params_fn=tweak, cam_list=sun_cams(rtx, oracle, w, h, 2),
+                 expect_flare=1)
+
+
+def test_offscreen_dumps_and_camera_at_init(rtx, oracle, tmp_path, default_scene):
+    """The presentation stand-in: PPM of the RGBA8 frame and PFM of the denoised HDR colour, read
+    back and compared with the downloads; a camera saved to file is loaded by rt_init
+    (loadCameraAtInit, init.cu:433-435) and renders the same frame."""
+    w, h = 96, 64
+    cfg = rtx.write_config(str(tmp_path / "a.toml"), w, h)
+    a = rtx.RayTracer(w, h, cfg).init()
+    a.set_delta_time(DT)
+    _, rc = terrain_camera(rtx, oracle, w, h)
+    a.camera = rc
+    rgba = np.zeros((h, w, 4), np.uint8)
+    a.draw(rgba)
+    ppm, pfm, camf = str(tmp_path / "f.ppm"), str(tmp_path / "f.pfm"), str(tmp_path / "cam.bin")
+    a.save_image(ppm, rtx.IMAGE_PPM_RGBA8)
+    a.save_image(pfm, rtx.IMAGE_PFM_HDR)
+    a.save_camera(camf)
+    raw = open(ppm, "rb").read()
+    head = b"P6\n%d %d\n255\n" % (w, h)
+    assert raw.startswith(head)
+    assert np.array_equal(np.frombuffer(raw[len(head):], np.uint8).reshape(h, w, 3), rgba[:, :, :3])
+    raw = open(pfm, "rb").read()
+    head = b"PF\n%d %d\n-1.0\n" % (w, h)
+    assert raw.startswith(head)
+    hdr = np.frombuffer(raw[len(head):], np.float32).reshape(h, w, 3)[::-1]
+    col = a.get_buffer("RENDER_COLOR", (h, w, 4), np.uint16)[:, :, :3].astype(np.uint16).view(np.float16)
+    assert np.array_equal(hdr, col.astype(np.float32))
+    b = rtx.RayTracer(w, h, rtx.write_config(str(tmp_path / "b.toml"), w, h, camera_file=camf)).init()
+    b.set_delta_time(DT)
+    assert list(b.camera.pos) == list(rc.pos) and b.camera.pitch == rc.pitch
+    rgba2 = np.zeros_like(rgba)
+    b.draw(rgba2)
+    assert np.array_equal(rgba, rgba2)
+    a.cleanup()
+    b.cleanup()

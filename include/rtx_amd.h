@@ -210,6 +210,12 @@ int rt_sync(rt_context* ctx);
  * milliseconds between the first launch and the end of the last. */
 int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms);
 
+/* HIP-event split of the path-trace stage (stage 2 above): runs `iters` path traces with an
+ * event recorded between consecutive kernels and writes the average milliseconds of each kernel
+ * (n >= 7: camera, shade, trace bounce queue, resume, trace shadow queue, resume, resolve).
+ * Measurement aid for the roofline in bench.py; no reference counterpart. */
+int rt_time_path_trace_kernels(rt_context* ctx, int iters, float* kernel_ms, int n);
+
 /* Copies device arrays to host (debug dumps of bvh.cu:15-96, traversal outputs). */
 enum rt_array_name {
     RT_ARR_VERTICES = 0,         /* float[nv][3] */

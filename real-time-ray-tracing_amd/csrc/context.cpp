@@ -498,6 +498,31 @@ int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms) {
     return RT_OK;
 }
 
+int rt_time_path_trace_kernels(rt_context* ctx, int iters, float* kernel_ms, int n) {
+    if (!ctx || !kernel_ms || iters < 1 || n < kPtKernels) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_time_path_trace_kernels before rt_init"; return RT_ERR_STATE; }
+    hipEvent_t marks[kPtKernels + 1] = {};
+    int rc = RT_OK;
+    for (auto& m : marks)
+        if (hipEventCreate(&m) != hipSuccess) { rc = RT_ERR_HIP; break; }
+    for (int k = 0; k < kPtKernels; ++k) kernel_ms[k] = 0.0f;
+    for (int i = 0; i < iters && rc == RT_OK; ++i) {
+        ctx->ptMarks = marks;
+        rc = rt_path_trace(ctx, 1 + i, 0);
+        ctx->ptMarks = nullptr;
+        if (rc == RT_OK && hipEventSynchronize(marks[kPtKernels]) != hipSuccess) rc = RT_ERR_HIP;
+        for (int k = 0; k < kPtKernels && rc == RT_OK; ++k) {
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, marks[k], marks[k + 1]) != hipSuccess) rc = RT_ERR_HIP;
+            kernel_ms[k] += ms / (float)iters;
+        }
+    }
+    for (auto& m : marks)
+        if (m) (void)hipEventDestroy(m);
+    if (rc == RT_ERR_HIP) ctx->err = "HIP event timing failed";
+    return rc;
+}
+
 size_t rt_array_bytes(const rt_context* ctx, int what) {
     if (!ctx) return 0;
     const size_t NP = ctx->mesh.triCountPadded, B = ctx->B, P = (size_t)ctx->renderW * ctx->renderH;

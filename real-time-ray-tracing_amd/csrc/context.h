@@ -108,6 +108,7 @@ struct rt_context {
     hipStream_t stream = nullptr;      // stream every stage is enqueued on
     hipStream_t ownStream = nullptr;   // the one rt_init created (destroyed by rt_destroy)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t* ptMarks = nullptr;  // set only inside rt_time_path_trace_kernels
     float* dVerts = nullptr;
     float* dNormals = nullptr;
     uint32_t* dIdx = nullptr;

@@ -334,7 +334,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
         HIP_TRY(ctx, hipMemsetAsync(fr.rays, 0, (size_t)ctx->renderW * ctx->renderH * 4, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(fr.ptStats, 0, (size_t)ctx->renderW * ctx->renderH * 16, ctx->stream));
     }
-    HIP_TRY(ctx, rtk_launch_pathtrace(&p, ctx->stream));
+    HIP_TRY(ctx, rtk_launch_pathtrace(&p, ctx->stream, ctx->ptMarks));
     fr.renderColor = fr.color;
     fr.hist = hist_of(hc);  // HistoryCamera::Setup after PathTrace (kernel.cu:357)
     fr.histValid = true;

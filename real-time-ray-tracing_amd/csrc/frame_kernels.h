@@ -164,5 +164,7 @@ extern "C" hipError_t rtk_denoise_post(DenoisePostParams* p, hipStream_t stream)
 extern "C" hipError_t rtk_launch_sky(const SkyGenParams* p, hipStream_t stream);
 extern "C" hipError_t rtk_launch_scan(const float* in, float* out, float* sums, int size, int blockSize,
                                       hipStream_t stream);
-extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream);
+// kernels of one path-trace launch: camera, shade, trace<3>, resume<3>, trace<4>, resume<4>, resolve
+constexpr int kPtKernels = 7;
+extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks);
 extern "C" int rtk_trace_queue_blocks_per_cu();

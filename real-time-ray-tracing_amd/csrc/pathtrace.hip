@@ -740,22 +740,32 @@ __global__ __launch_bounds__(256) void k_pt_resolve(PathTraceParams P) {
 
 extern "C" hipError_t rtk_launch_trace_queue(const PathTraceParams* p, int step, hipStream_t stream);
 
-extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream) {
+// marks (optional, kPtKernels + 1 events): recorded before the first and after every kernel so
+// a timing host can split the stage per kernel (rt_time_path_trace_kernels)
+extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks) {
     if (p->spp < 1 || p->spp > 64 || p->ws.persistBlocks < 1) return hipErrorInvalidValue;
     if ((size_t)p->rows * p->width >= (1u << 26) || (size_t)p->rows * p->width * p->spp > p->ws.cap)
         return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
+    int k = 0;
+    auto mark = [&]() { return marks ? hipEventRecord(marks[k++], stream) : hipSuccess; };
+    if ((e = mark()) != hipSuccess) return e;
     const int nSW = cam_sample_waves(p->spp);
     const int BW = nSW == 4 ? 8 : 16, BH = nSW == 1 ? 16 : 8;
     const dim3 grid((p->width + BW - 1) / BW, (p->rows + BH - 1) / BH);
     hipLaunchKernelGGL(k_pt_camera, grid, dim3(256), 0, stream, *p);
+    if ((e = mark()) != hipSuccess) return e;
     if (p->ws.glossy) hipLaunchKernelGGL(k_pt_shade0<true>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
     else hipLaunchKernelGGL(k_pt_shade0<false>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
-    if ((e = rtk_launch_trace_queue(p, 3, stream)) != hipSuccess) return e;
+    if ((e = mark()) != hipSuccess) return e;
+    if ((e = rtk_launch_trace_queue(p, 3, stream)) != hipSuccess || (e = mark()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_pt_resume<3>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
-    if ((e = rtk_launch_trace_queue(p, 4, stream)) != hipSuccess) return e;
+    if ((e = mark()) != hipSuccess) return e;
+    if ((e = rtk_launch_trace_queue(p, 4, stream)) != hipSuccess || (e = mark()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_pt_resume<4>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
+    if ((e = mark()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_pt_resolve, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
+    if ((e = mark()) != hipSuccess) return e;
     return hipGetLastError();
 }

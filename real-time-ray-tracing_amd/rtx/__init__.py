@@ -108,6 +108,7 @@ SIGNATURES = {
     "rt_trace_primary": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "rt_sync": (C.c_int, [C.c_void_p]),
     "rt_time_stage": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float)]),
+    "rt_time_path_trace_kernels": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float), C.c_int]),
     "rt_download": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     "rt_array_bytes": (C.c_size_t, [C.c_void_p, C.c_int]),
     "rt_save_camera": (C.c_int, [C.c_void_p, C.c_char_p]),
@@ -256,6 +257,15 @@ class RayTracer:
         ms = C.c_float()
         self._check(self.lib.rt_time_stage(self.h, stage, iters, C.byref(ms)), "rt_time_stage")
         return ms.value
+
+    PT_KERNELS = ("k_pt_camera", "k_pt_shade0", "k_trace_queue<3>", "k_pt_resume<3>", "k_trace_queue<4>",
+                  "k_pt_resume<4>", "k_pt_resolve")
+
+    def time_path_trace_kernels(self, iters=10):
+        """Average ms of each path-trace kernel (HIP events on the context stream)."""
+        ms = (C.c_float * len(self.PT_KERNELS))()
+        self._check(self.lib.rt_time_path_trace_kernels(self.h, iters, ms, len(ms)), "rt_time_path_trace_kernels")
+        return dict(zip(self.PT_KERNELS, (float(v) for v in ms)))
 
     # ---- camera file I/O and offscreen image dumps
     def save_camera(self, path: str):

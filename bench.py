@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the per-stage and 1M-triangle side measurements")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="serial frames (no post stream): denoise of frame f does not overlap the trace of f+1")
     return ap.parse_args()
 
 
@@ -113,7 +115,11 @@ def main():
     rt = rtx.RayTracer(W, H, cfg).init()
     rt.set_delta_time(DELTA_MS)
     rt.set_stream(torch.cuda.current_stream(dev).cuda_stream)  # collectives order with the renderer
-    sg = StripGather(W, H, world, rank, dev, rt) if world > 1 else None
+    pipeline = not args.no_pipeline
+    post = torch.cuda.Stream(dev) if pipeline else None
+    if pipeline:  # denoise/post of frame f on a second stream, overlapping the trace of frame f+1
+        rt.set_post_stream(post.cuda_stream)
+    sg = StripGather(W, H, world, rank, dev, rt, sets=2 if pipeline else 1) if world > 1 else None
 
     def frame(f):
         rt.build_bvh()
@@ -166,8 +172,10 @@ def main():
         "config": {"workload": "BASELINE config 3: %dx%d, %d spp path trace + SVGF denoise + auto-exposure/"
                                "tone map, per-frame LBVH rebuild" % (W, H, S),
                    "width": W, "height": H, "spp": S,
-                   "parallelism": "screen strips x%d + RCCL all-gather of G-buffers" % world if world > 1
-                   else "single GPU"},
+                   "parallelism": ("screen strips x%d + RCCL all-gather of G-buffers" % world if world > 1
+                                   else "single GPU")
+                                  + ("; 2 frames in flight (trace f+1 || denoise f on a second stream)"
+                                     if pipeline else "; serial frames")},
         "fps": round(1000.0 / ms_per_step, 2),
         "rays_per_frame": int(rays // args.steps),
     }

@@ -140,6 +140,7 @@ typedef struct rt_info {
     int32_t frameNum;           /* frame index of the last rt_draw (0 before the first) */
     int32_t deviceId;
     uint32_t spp;               /* samples (reference PathTrace evaluations) per frame */
+    int32_t gbufferSet;         /* G-buffer set the last rt_path_trace wrote (0 or 1, see rt_set_post_stream) */
 } rt_info;
 
 int rt_get_info(const rt_context* ctx, rt_info* out);
@@ -195,6 +196,17 @@ int rt_get_ray_count(rt_context* ctx, uint64_t* rays, int reset);
 /* Enqueue every later stage on `stream` (a hipStream_t, e.g. the caller's framework stream so
  * its collectives order with the renderer); NULL restores the context's own stream. */
 int rt_set_stream(rt_context* ctx, void* stream);
+
+/* Frame pipelining (no reference counterpart; the reference draws frames strictly one after
+ * another): with a post stream set, rt_denoise_post runs the denoiser and post chain on that
+ * stream, after everything enqueued on the context stream so far (path trace, G-buffer
+ * gathers), and the path tracer alternates between two G-buffer sets, so the trace of frame
+ * f+1 overlaps the denoise of frame f.  Results are identical to the serial order.  Host reads
+ * (rt_get_buffer, rt_download, rt_sync, rt_draw's copies) wait for both streams.  NULL turns it
+ * off.  rt_info.gbufferSet names the set the last path trace wrote; bind the second set's
+ * buffers with name | RT_BUF_SET1. */
+#define RT_BUF_SET1 0x100
+int rt_set_post_stream(rt_context* ctx, void* stream);
 
 /* Use caller-owned device memory (>= rt_buffer_bytes, 16-B aligned) as one of the path-trace
  * G-buffers (RT_BUF_RENDER_COLOR / NORMAL / ALBEDO / DEPTH / MOTION), e.g. so a multi-GPU host
@@ -254,10 +266,24 @@ enum rt_array_name {
                                     [8]/[9] longest traversal (iterations) of the step-3/4 queues
                                     (detail launches only), [10] internal errors (must be 0),
                                     [11] pixels with a sample that hit geometry */
+    RT_ARR_PT_Q3_ORIGINS = 33,   /* float4[cap] step-3 queue rays of the last launch: origin xyz, pixel bits */
+    RT_ARR_PT_Q3_DIRS = 34,      /* float4[cap] direction xyz, flags bits ([0] of RT_ARR_PT_QUEUE are valid) */
+    RT_ARR_PT_Q4_ORIGINS = 35,   /* float4[cap] step-4 queue, same layout ([1] valid) */
+    RT_ARR_PT_Q4_DIRS = 36,
     RT_ARR_PT_STATS = 31         /* uint32[W*H][4] rays, node visits, triangle tests, diffuse events
                                     (rt_path_trace with_detail) */
 };
 int rt_download(const rt_context* ctx, int what, void* dst, size_t bytes);
+
+/* Batch ray query: the reference's RaySceneIntersect traversal (traverse.cuh:107-253, the
+ * closest hit of TraverseBvh with its 16-entry stack and 1024-iteration cap) for n caller rays,
+ * run by the persistent queue tracer on the BVH of the last rt_build_bvh.
+ *   rays  n x 8 floats: origin xyz, (unused), direction xyz, (unused)
+ *   hits  n x 4 floats: t (RayMax on a miss), triangle index as int32 bits (-1 on a miss), u, v
+ *   iters optional n x uint32: TraverseBvh loop iterations per ray
+ *   kernel_ms optional: HIP-event time of the tracer kernel alone
+ * n must not exceed width x strip rows x spp (the queue capacity).  Host buffers; synchronous. */
+int rt_trace_rays(rt_context* ctx, const float* rays, uint32_t n, float* hits, uint32_t* iters, float* kernel_ms);
 size_t rt_array_bytes(const rt_context* ctx, int what);
 
 #ifdef __cplusplus

@@ -351,7 +351,9 @@ int rt_init(rt_context* ctx) {
 
 void rt_destroy(rt_context* ctx) {
     if (!ctx) return;
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->stream) (void)sync_streams(ctx);
+    for (hipEvent_t e : {ctx->ptDone[0], ctx->ptDone[1], ctx->postDone[0], ctx->postDone[1], ctx->overlapEv})
+        if (e) (void)hipEventDestroy(e);
     for (void* p : ctx->allocations) (void)hipFree(p);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -411,6 +413,7 @@ int rt_get_info(const rt_context* ctx, rt_info* out) {
     out->frameNum = ctx->lastFrame;
     out->deviceId = ctx->device;
     out->spp = (uint32_t)ctx->spp;
+    out->gbufferSet = ctx->fr.gbSet;
     return RT_OK;
 }
 
@@ -469,8 +472,7 @@ int rt_trace_primary(rt_context* ctx, int frame_num, int with_detail) {
 int rt_sync(rt_context* ctx) {
     if (!ctx) return RT_ERR_ARG;
     if (!ctx->stream) return RT_OK;
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return RT_OK;
+    return sync_streams(ctx);
 }
 
 int rt_draw_frame_internal(rt_context* ctx);  // frame.cpp
@@ -478,6 +480,13 @@ int rt_draw_frame_internal(rt_context* ctx);  // frame.cpp
 int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms) {
     if (!ctx || !total_ms || iters < 1) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_time_stage before rt_init"; return RT_ERR_STATE; }
+    if (ctx->postStream) {  // stages are timed serially on the context stream
+        void* post = ctx->postStream;
+        int rc = rt_set_post_stream(ctx, nullptr);
+        if (rc == RT_OK) rc = rt_time_stage(ctx, stage, iters, total_ms);
+        const int rc2 = rt_set_post_stream(ctx, post);
+        return rc != RT_OK ? rc : rc2;
+    }
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     for (int i = 0; i < iters; ++i) {
         int rc = RT_OK;
@@ -501,6 +510,7 @@ int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms) {
 int rt_time_path_trace_kernels(rt_context* ctx, int iters, float* kernel_ms, int n) {
     if (!ctx || !kernel_ms || iters < 1 || n < kPtKernels) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_time_path_trace_kernels before rt_init"; return RT_ERR_STATE; }
+    if (int rc0 = sync_streams(ctx)) return rc0;
     hipEvent_t marks[kPtKernels + 1] = {};
     int rc = RT_OK;
     for (auto& m : marks)
@@ -561,6 +571,10 @@ size_t rt_array_bytes(const rt_context* ctx, int what) {
         case RT_ARR_RGBA8: return (size_t)ctx->screenW * ctx->screenH * 4;
         case RT_ARR_PT_STATS: return P * 16;
         case RT_ARR_PT_QUEUE: return 64 * 4;
+        case RT_ARR_PT_Q3_ORIGINS:
+        case RT_ARR_PT_Q3_DIRS:
+        case RT_ARR_PT_Q4_ORIGINS:
+        case RT_ARR_PT_Q4_DIRS: return (size_t)ctx->fr.ws.cap * 16;
         default: return 0;
     }
 }
@@ -603,6 +617,10 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
         case RT_ARR_RGBA8: src = ctx->fr.rgba; break;
         case RT_ARR_PT_STATS: src = ctx->fr.ptStats; break;
         case RT_ARR_PT_QUEUE: src = ctx->fr.ws.counters; break;
+        case RT_ARR_PT_Q3_ORIGINS: src = ctx->fr.ws.q3.rayO; break;
+        case RT_ARR_PT_Q3_DIRS: src = ctx->fr.ws.q3.rayD; break;
+        case RT_ARR_PT_Q4_ORIGINS: src = ctx->fr.ws.q4.rayO; break;
+        case RT_ARR_PT_Q4_DIRS: src = ctx->fr.ws.q4.rayD; break;
         case RT_ARR_SUN_DIR: {
             if (bytes < 16) { ctx->err = "destination too small"; return RT_ERR_ARG; }
             float* o = (float*)dst;
@@ -614,7 +632,7 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
     }
     const size_t need = rt_array_bytes(ctx, what);
     if (bytes < need) { ctx->err = "destination too small"; return RT_ERR_ARG; }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = sync_streams(ctx)) return rc;
     HIP_TRY(ctx, hipMemcpy(dst, src, need, hipMemcpyDeviceToHost));
     return RT_OK;
 }

@@ -39,7 +39,16 @@ struct FrameResources {
     // soil textures (init.cu:524-577)
     uint2* texAlbedo = nullptr;
     uint2* texNormal = nullptr;
-    // path-trace G-buffer (pathtrace.cuh:11-128)
+    // path-trace G-buffer (pathtrace.cuh:11-128): the set the last path trace wrote.  With a
+    // post stream (rt_set_post_stream) the path tracer alternates between two sets gX[0/1], so
+    // frame f+1 is traced while frame f is denoised; without one it always uses set 0.
+    uint2* gColor[2] = {};
+    uint2* gNormal[2] = {};
+    uint2* gAlbedo[2] = {};
+    uint16_t* gDepth[2] = {};
+    uint32_t* gMotion[2] = {};
+    int gbSet = 0;
+    bool setInFlight[2] = {false, false};  // a denoise on the post stream reads this set
     uint2* color = nullptr;
     uint2* normal = nullptr;
     uint2* albedo = nullptr;
@@ -108,6 +117,15 @@ struct rt_context {
     hipStream_t stream = nullptr;      // stream every stage is enqueued on
     hipStream_t ownStream = nullptr;   // the one rt_init created (destroyed by rt_destroy)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipStream_t postStream = nullptr;  // optional: denoise + post run here (rt_set_post_stream)
+    hipEvent_t ptDone[2] = {}, postDone[2] = {}, overlapEv = nullptr;
+    // frame pipelining: rt_denoise_post(f) is enqueued on the post stream only once the next
+    // path trace has enqueued kernel `overlapAfter` (so it fills the trace stages' idle tails), or
+    // at the next host read / denoise call, whichever comes first
+    bool postPending = false;
+    int postPendingSet = 0;
+    int overlapAfter = 1;  // after k_pt_shade0: measured best
+    DenoisePostParams postParams{};
     hipEvent_t* ptMarks = nullptr;  // set only inside rt_time_path_trace_kernels
     float* dVerts = nullptr;
     float* dNormals = nullptr;
@@ -156,6 +174,7 @@ int dalloc(rt_context* ctx, T** p, size_t bytes) {
     return rc;
 }
 int rt_frame_init(rt_context* ctx);  // frame.cpp: sky tables, textures, G-buffers
+int sync_streams(rt_context* ctx);   // frame.cpp: context stream + post stream
 std::string rt_data_dir();
 void rt_camera_update(const rt_camera& in, int renderW, int renderH, HostCamera& c);
 TraceCamera rt_trace_camera(const HostCamera& c);

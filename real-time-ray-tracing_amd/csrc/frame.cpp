@@ -7,6 +7,7 @@
 //   sky regeneration    kernel.cu:286-307
 //   PathTrace launch    kernel.cu:330-350; HistoryCamera::Setup kernel.cu:133-136, 357
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
@@ -161,6 +162,53 @@ HistCamera hist_of(const HostCamera& c) {
 
 }  // namespace
 
+// point the G-buffer views at set fr.gbSet
+void select_gbuffers(FrameResources& fr) {
+    const int k = fr.gbSet;
+    if (fr.renderColor == fr.color) fr.renderColor = fr.gColor[k];
+    fr.color = fr.gColor[k];
+    fr.normal = fr.gNormal[k];
+    fr.albedo = fr.gAlbedo[k];
+    fr.depth = fr.gDepth[k];
+    fr.motion = fr.gMotion[k];
+}
+
+// enqueue a deferred rt_denoise_post on the post stream (frame pipelining)
+int issue_pending_post(rt_context* ctx) {
+    if (!ctx->postPending) return RT_OK;
+    ctx->postPending = false;
+    const int set = ctx->postPendingSet;
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->postStream, ctx->ptDone[set], 0));
+    HIP_TRY(ctx, rtk_denoise_post(&ctx->postParams, ctx->postStream));
+    HIP_TRY(ctx, hipEventRecord(ctx->postDone[set], ctx->postStream));
+    ctx->fr.renderColor = ctx->postParams.finalColor;  // the launcher's buffer plan names them
+    ctx->fr.scaledColor = ctx->postParams.finalScaled;
+    return RT_OK;
+}
+
+namespace {
+// PtLaunchHook: the previous frame's denoise starts once this frame's kernel `overlapAfter`
+// has been enqueued, so it runs beside the trace stages' latency-bound tails
+hipError_t overlap_hook(void* arg) {
+    rt_context* ctx = (rt_context*)arg;
+    hipError_t e = hipEventRecord(ctx->overlapEv, ctx->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->postStream, ctx->overlapEv, 0);
+    if (e == hipSuccess && issue_pending_post(ctx) != RT_OK) e = hipErrorUnknown;
+    return e;
+}
+}  // namespace
+
+// wait for the context stream and, when set, the post stream
+int sync_streams(rt_context* ctx) {
+    if (ctx->postStream) {
+        const int rc = issue_pending_post(ctx);
+        if (rc != RT_OK) return rc;
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->postStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->postStream));
+    return RT_OK;
+}
+
 int rt_frame_init(rt_context* ctx) {
     FrameResources& fr = ctx->fr;
     std::string err;
@@ -189,6 +237,11 @@ int rt_frame_init(rt_context* ctx) {
     ALLOC(fr.albedo, P * 8);
     ALLOC(fr.depth, P * 2);
     ALLOC(fr.motion, P * 4);
+    fr.gColor[0] = fr.color;
+    fr.gNormal[0] = fr.normal;
+    fr.gAlbedo[0] = fr.albedo;
+    fr.gDepth[0] = fr.depth;
+    fr.gMotion[0] = fr.motion;
     ALLOC(fr.rays, P * 4);
     ALLOC(fr.ptStats, P * 16);
     ALLOC(fr.rayCounter, 64);
@@ -284,6 +337,11 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     if (!ctx || frame_num < 1) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_path_trace before rt_init"; return RT_ERR_STATE; }
     FrameResources& fr = ctx->fr;
+    if (ctx->postStream) {  // frame pipelining: trace into the set no denoise still reads
+        fr.gbSet ^= 1;
+        select_gbuffers(fr);
+        if (fr.setInFlight[fr.gbSet]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->postDone[fr.gbSet], 0));
+    }
     int rc = update_sky(ctx);
     if (rc != RT_OK) return rc;
     HostCamera hc;
@@ -334,7 +392,9 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
         HIP_TRY(ctx, hipMemsetAsync(fr.rays, 0, (size_t)ctx->renderW * ctx->renderH * 4, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(fr.ptStats, 0, (size_t)ctx->renderW * ctx->renderH * 16, ctx->stream));
     }
-    HIP_TRY(ctx, rtk_launch_pathtrace(&p, ctx->stream, ctx->ptMarks));
+    PtLaunchHook hook{ctx->overlapAfter, overlap_hook, ctx};
+    HIP_TRY(ctx, rtk_launch_pathtrace(&p, ctx->stream, ctx->ptMarks, ctx->postPending ? &hook : nullptr));
+    if (ctx->postPending && (rc = issue_pending_post(ctx)) != RT_OK) return rc;
     fr.renderColor = fr.color;
     fr.hist = hist_of(hc);  // HistoryCamera::Setup after PathTrace (kernel.cu:357)
     fr.histValid = true;
@@ -449,10 +509,23 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
             p.sunUv[1] = uy;
         }
     }
-    HIP_TRY(ctx, rtk_denoise_post(&p, ctx->stream));
+    if (ctx->postStream) {
+        // deferred: enqueued behind the next path trace's first kernels (overlap_hook) or at the
+        // next host read; it waits for everything enqueued so far on the context stream (this
+        // frame's path trace and any G-buffer gathers)
+        int rc = issue_pending_post(ctx);
+        if (rc != RT_OK) return rc;
+        HIP_TRY(ctx, hipEventRecord(ctx->ptDone[fr.gbSet], ctx->stream));
+        ctx->postParams = p;
+        ctx->postPendingSet = fr.gbSet;
+        ctx->postPending = true;
+        fr.setInFlight[fr.gbSet] = true;
+    } else {
+        HIP_TRY(ctx, rtk_denoise_post(&p, ctx->stream));
+        fr.renderColor = p.finalColor;
+        fr.scaledColor = p.finalScaled;
+    }
     if (p.temporal2) std::swap(fr.histColor, fr.histColorAlt);
-    fr.renderColor = p.finalColor;
-    fr.scaledColor = p.finalScaled;
     return RT_OK;
 }
 
@@ -465,7 +538,7 @@ int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
     if ((rc = rt_build_bvh(ctx)) != RT_OK) return rc;
     if ((rc = rt_path_trace(ctx, frame, 0)) != RT_OK) return rc;
     if ((rc = rt_denoise_post(ctx, frame, hdr_out != nullptr)) != RT_OK) return rc;
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if ((rc = sync_streams(ctx)) != RT_OK) return rc;
     if (rgba8_out)
         HIP_TRY(ctx, hipMemcpy(rgba8_out, ctx->fr.rgba, (size_t)ctx->screenW * ctx->screenH * 4, hipMemcpyDeviceToHost));
     if (hdr_out)
@@ -476,30 +549,60 @@ int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
 int rt_set_stream(rt_context* ctx, void* stream) {
     if (!ctx) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_set_stream before rt_init"; return RT_ERR_STATE; }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    int rc = sync_streams(ctx);
+    if (rc != RT_OK) return rc;
     ctx->stream = stream ? (hipStream_t)stream : ctx->ownStream;
+    return RT_OK;
+}
+
+int rt_set_post_stream(rt_context* ctx, void* stream) {
+    if (!ctx) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_set_post_stream before rt_init"; return RT_ERR_STATE; }
+    int rc = sync_streams(ctx);
+    if (rc != RT_OK) return rc;
+    FrameResources& fr = ctx->fr;
+    fr.setInFlight[0] = fr.setInFlight[1] = false;
+    if (!stream) {
+        ctx->postStream = nullptr;
+        return RT_OK;
+    }
+    const size_t P = (size_t)ctx->renderW * ctx->renderH;
+#define ALLOC(p, bytes) if (!(p) && (rc = dalloc(ctx, &(p), (bytes))) != RT_OK) return rc
+    ALLOC(fr.gColor[1], P * 8);
+    ALLOC(fr.gNormal[1], P * 8);
+    ALLOC(fr.gAlbedo[1], P * 8);
+    ALLOC(fr.gDepth[1], P * 2);
+    ALLOC(fr.gMotion[1], P * 4);
+#undef ALLOC
+    for (int k = 0; k < 2; ++k) {
+        if (!ctx->ptDone[k]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ptDone[k], hipEventDisableTiming));
+        if (!ctx->postDone[k]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->postDone[k], hipEventDisableTiming));
+    }
+    if (!ctx->overlapEv) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->overlapEv, hipEventDisableTiming));
+    if (const char* a = getenv("RTX_OVERLAP_AFTER")) ctx->overlapAfter = atoi(a);  // tuning aid
+    ctx->postStream = (hipStream_t)stream;
     return RT_OK;
 }
 
 int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
     if (!ctx || !device_ptr) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_bind_buffer before rt_init"; return RT_ERR_STATE; }
-    const size_t need = rt_buffer_bytes(ctx, name);
+    const size_t need = rt_buffer_bytes(ctx, name & ~RT_BUF_SET1);
     if (need == 0 || bytes < need) { ctx->err = "rt_bind_buffer: unknown buffer or too small"; return RT_ERR_ARG; }
     if (((uintptr_t)device_ptr & 15u) != 0) { ctx->err = "rt_bind_buffer: pointer must be 16-byte aligned"; return RT_ERR_ARG; }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    int rc = sync_streams(ctx);
+    if (rc != RT_OK) return rc;
     FrameResources& fr = ctx->fr;
-    switch (name) {
-        case RT_BUF_RENDER_COLOR:
-            if (fr.renderColor == fr.color) fr.renderColor = (uint2*)device_ptr;
-            fr.color = (uint2*)device_ptr;
-            break;
-        case RT_BUF_NORMAL: fr.normal = (uint2*)device_ptr; break;
-        case RT_BUF_ALBEDO: fr.albedo = (uint2*)device_ptr; break;
-        case RT_BUF_DEPTH: fr.depth = (uint16_t*)device_ptr; break;
-        case RT_BUF_MOTION: fr.motion = (uint32_t*)device_ptr; break;
+    const int set = (name & RT_BUF_SET1) ? 1 : 0;
+    switch (name & ~RT_BUF_SET1) {
+        case RT_BUF_RENDER_COLOR: fr.gColor[set] = (uint2*)device_ptr; break;
+        case RT_BUF_NORMAL: fr.gNormal[set] = (uint2*)device_ptr; break;
+        case RT_BUF_ALBEDO: fr.gAlbedo[set] = (uint2*)device_ptr; break;
+        case RT_BUF_DEPTH: fr.gDepth[set] = (uint16_t*)device_ptr; break;
+        case RT_BUF_MOTION: fr.gMotion[set] = (uint32_t*)device_ptr; break;
         default: ctx->err = "rt_bind_buffer: only the path-trace G-buffers can be bound"; return RT_ERR_ARG;
     }
+    if (set == fr.gbSet) select_gbuffers(fr);
     return RT_OK;
 }
 
@@ -524,6 +627,7 @@ int rt_get_buffer(const rt_context* cctx, int name, void* dst, size_t bytes) {
     rt_context* ctx = const_cast<rt_context*>(cctx);
     if (!ctx || !dst) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_get_buffer before rt_init"; return RT_ERR_STATE; }
+    if (int rc = sync_streams(ctx)) return rc;  // also issues a deferred denoise (buffer plan)
     const FrameResources& fr = ctx->fr;
     const void* src = nullptr;
     switch (name) {
@@ -544,7 +648,7 @@ int rt_get_buffer(const rt_context* cctx, int name, void* dst, size_t bytes) {
     }
     const size_t need = rt_buffer_bytes(ctx, name);
     if (bytes < need) { ctx->err = "destination too small"; return RT_ERR_ARG; }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = sync_streams(ctx)) return rc;
     HIP_TRY(ctx, hipMemcpy(dst, src, need, hipMemcpyDeviceToHost));
     return RT_OK;
 }
@@ -619,7 +723,7 @@ extern "C" int rt_load_camera(rt_context* ctx, const char* path) {
 extern "C" int rt_save_image(rt_context* ctx, const char* path, int kind) {
     if (!ctx || !path || !*path || (kind != RT_IMAGE_PPM_RGBA8 && kind != RT_IMAGE_PFM_HDR)) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_save_image before rt_init"; return RT_ERR_STATE; }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = sync_streams(ctx)) return rc;
     std::ofstream f(path, std::ios::binary | std::ios::trunc);
     if (!f) { ctx->err = std::string("cannot write image ") + path; return RT_ERR_IO; }
     if (kind == RT_IMAGE_PPM_RGBA8) {
@@ -642,4 +746,43 @@ extern "C" int rt_save_image(rt_context* ctx, const char* path, int kind) {
         f.write(reinterpret_cast<const char*>(rgb.data()), (std::streamsize)(rgb.size() * 4));
     }
     return f ? RT_OK : RT_ERR_IO;
+}
+
+// Batch ray query through the persistent queue tracer (the RaySceneIntersect traversal of
+// traverse.cuh:107-253 for caller rays): rays = n x (org.xyz, pad, dir.xyz, pad) floats,
+// hits = n x (t, triangle index as int bits (-1: miss), u, v), iters = per-ray TraverseBvh
+// iterations (optional), kernel_ms = the tracer kernel's HIP-event time (optional).
+int rt_trace_rays(rt_context* ctx, const float* rays, uint32_t n, float* hits, uint32_t* iters, float* kernel_ms) {
+    if (!ctx || (n > 0 && (!rays || !hits))) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_trace_rays before rt_init"; return RT_ERR_STATE; }
+    FrameResources& fr = ctx->fr;
+    if (n > fr.ws.cap) { ctx->err = "more rays than the queue capacity (width x strip rows x spp)"; return RT_ERR_ARG; }
+    if (kernel_ms) *kernel_ms = 0.0f;
+    if (n == 0) return RT_OK;
+    std::vector<float4> o(n), d(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        float tag;
+        memcpy(&tag, &i, 4);  // the queue's pixel slot carries the ray index
+        o[i] = make_float4(rays[8 * i], rays[8 * i + 1], rays[8 * i + 2], tag);
+        d[i] = make_float4(rays[8 * i + 4], rays[8 * i + 5], rays[8 * i + 6], 0.0f);
+    }
+    PathTraceParams p = {};
+    p.triPos = ctx->dTriPos;
+    p.triNrm = ctx->dTriNrm;
+    p.nodes = ctx->dNodes;
+    p.tlasNodes = ctx->dTlasNodes;
+    p.ws = fr.ws;
+    p.ws.itersOut = iters ? reinterpret_cast<uint32_t*>(fr.ws.pathL) : nullptr;  // pathL: per-frame scratch
+    HIP_TRY(ctx, hipMemcpyAsync(fr.ws.q3.rayO, o.data(), (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(fr.ws.q3.rayD, d.data(), (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(fr.ws.counters, 0, kWsCounterWords * sizeof(uint32_t), ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(fr.ws.counters + kCntQ3, &n, 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    HIP_TRY(ctx, rtk_launch_trace_queue(&p, 3, ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(hits, fr.ws.hitRec, (size_t)n * 16, hipMemcpyDeviceToHost, ctx->stream));
+    if (iters) HIP_TRY(ctx, hipMemcpyAsync(iters, p.ws.itersOut, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (kernel_ms) HIP_TRY(ctx, hipEventElapsedTime(kernel_ms, ctx->ev0, ctx->ev1));
+    return RT_OK;
 }

@@ -80,6 +80,7 @@ struct PtWorkspace {
     uint32_t cap;               // entries per queue (= rows * W * spp)
     uint32_t persistBlocks;     // grid of the persistent queue kernels
     int glossy;                 // materials can be glossy: steps 1-2 may trace (materialOverride)
+    uint32_t* itersOut = nullptr;  // optional [cap]: traversal iterations per queue entry (rt_trace_rays)
 };
 
 struct PathTraceParams {
@@ -166,5 +167,12 @@ extern "C" hipError_t rtk_launch_scan(const float* in, float* out, float* sums, 
                                       hipStream_t stream);
 // kernels of one path-trace launch: camera, shade, trace<3>, resume<3>, trace<4>, resume<4>, resolve
 constexpr int kPtKernels = 7;
-extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks);
+struct PtLaunchHook {
+    int after;                        // kernel index (0 = camera, 1 = shade, ...)
+    hipError_t (*fn)(void* arg);
+    void* arg;
+};
+extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
+                                           const PtLaunchHook* hook);
 extern "C" int rtk_trace_queue_blocks_per_cu();
+extern "C" hipError_t rtk_launch_trace_queue(const PathTraceParams* p, int step, hipStream_t stream);

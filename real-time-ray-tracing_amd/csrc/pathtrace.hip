@@ -738,18 +738,27 @@ __global__ __launch_bounds__(256) void k_pt_resolve(PathTraceParams P) {
     }
 }
 
-extern "C" hipError_t rtk_launch_trace_queue(const PathTraceParams* p, int step, hipStream_t stream);
 
 // marks (optional, kPtKernels + 1 events): recorded before the first and after every kernel so
-// a timing host can split the stage per kernel (rt_time_path_trace_kernels)
-extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks) {
+// a timing host can split the stage per kernel (rt_time_path_trace_kernels).
+// hook (optional): called on the host right after kernel hook->after (0 = camera) is enqueued;
+// the frame pipeline issues the previous frame's denoise there (frame.cpp).
+extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
+                                           const PtLaunchHook* hook) {
     if (p->spp < 1 || p->spp > 64 || p->ws.persistBlocks < 1) return hipErrorInvalidValue;
     if ((size_t)p->rows * p->width >= (1u << 26) || (size_t)p->rows * p->width * p->spp > p->ws.cap)
         return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     int k = 0;
-    auto mark = [&]() { return marks ? hipEventRecord(marks[k++], stream) : hipSuccess; };
+    auto mark = [&]() {
+        if (hook && hook->fn && k == hook->after + 1) {
+            const hipError_t he = hook->fn(hook->arg);
+            if (he != hipSuccess) return he;
+        }
+        if (!marks) { ++k; return hipSuccess; }
+        return hipEventRecord(marks[k++], stream);
+    };
     if ((e = mark()) != hipSuccess) return e;
     const int nSW = cam_sample_waves(p->spp);
     const int BW = nSW == 4 ? 8 : 16, BH = nSW == 1 ? 16 : 8;

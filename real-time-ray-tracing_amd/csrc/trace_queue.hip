@@ -124,6 +124,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
             if (done) {
                 P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);
                 P.ws.hitErr[idx] = s.hitErrT;
+                if (P.ws.itersOut) P.ws.itersOut[idx] = s.iters;
                 if (P.statsOut) {
                     const uint32_t p = __float_as_uint(q.rayO[idx].w);
                     atomicAdd(&P.statsOut[p].y, s.visits);

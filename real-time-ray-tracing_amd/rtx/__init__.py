@@ -25,7 +25,8 @@ ARR = dict(VERTICES=0, INDICES=1, NORMALS=2, TRI_POS=3, AABBS=4, MORTON=5, REORD
            TLAS_MORTON=9, TLAS_REORDER=10, TLAS_NODES=11, TLAS_SCENE_AABB=12, BATCH_SCENE_AABBS=13, HITS=14,
            HIT_NORMALS=15, HIT_FAKE_NORMALS=16, HIT_STATS=17, TRI_NRM=18, RAYS=19, SKY_PDF=20, SKY_CDF=21,
            SUN_PDF=22, SUN_CDF=23, SUN_DIR=24, HISTOGRAM=25, EXPOSURE=26, COLOR4=27, COLOR16=28, COLOR64=29,
-           RGBA8=30, PT_STATS=31, PT_QUEUE=32)
+           RGBA8=30, PT_STATS=31, PT_QUEUE=32, PT_Q3_ORIGINS=33, PT_Q3_DIRS=34,
+           PT_Q4_ORIGINS=35, PT_Q4_DIRS=36)
 # rt_buffer_name (Buffer2DName, kernel.cuh:286-315)
 BUF = dict(RENDER_COLOR=0, ACCUMULATION=1, HISTORY_COLOR=2, SCALED_COLOR=3, NORMAL=10, DEPTH=11, HISTORY_DEPTH=12,
            MOTION=13, NOISE_LEVEL=14, NOISE_LEVEL16=15, SKY=16, SUN=17, ALBEDO=18)
@@ -80,7 +81,7 @@ class Info(C.Structure):
     _fields_ = [("triCount", C.c_uint32), ("triCountPadded", C.c_uint32), ("batchCount", C.c_uint32),
                 ("vertexCount", C.c_uint32), ("renderWidth", C.c_int32), ("renderHeight", C.c_int32),
                 ("screenWidth", C.c_int32), ("screenHeight", C.c_int32), ("frameNum", C.c_int32),
-                ("deviceId", C.c_int32), ("spp", C.c_uint32)]
+                ("deviceId", C.c_int32), ("spp", C.c_uint32), ("gbufferSet", C.c_int32)]
 
 
 # every entry point declared in include/rtx_amd.h, with its ctypes signature
@@ -102,6 +103,7 @@ SIGNATURES = {
     "rt_path_trace": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "rt_denoise_post": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "rt_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "rt_set_post_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "rt_bind_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     "rt_get_ray_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "rt_build_bvh": (C.c_int, [C.c_void_p]),
@@ -109,6 +111,7 @@ SIGNATURES = {
     "rt_sync": (C.c_int, [C.c_void_p]),
     "rt_time_stage": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float)]),
     "rt_time_path_trace_kernels": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float), C.c_int]),
+    "rt_trace_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]),
     "rt_download": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     "rt_array_bytes": (C.c_size_t, [C.c_void_p, C.c_int]),
     "rt_save_camera": (C.c_int, [C.c_void_p, C.c_char_p]),
@@ -116,6 +119,7 @@ SIGNATURES = {
     "rt_save_image": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
 }
 IMAGE_PPM_RGBA8, IMAGE_PFM_HDR = 0, 1
+BUF_SET1 = 0x100  # rt_bind_buffer: second G-buffer set (frame pipelining, rt_set_post_stream)
 
 _lib = None
 
@@ -239,8 +243,13 @@ class RayTracer:
     def set_stream(self, stream_ptr: int | None):
         self._check(self.lib.rt_set_stream(self.h, stream_ptr), "rt_set_stream")
 
-    def bind_buffer(self, name: str, device_ptr: int, nbytes: int):
-        self._check(self.lib.rt_bind_buffer(self.h, BUF[name], device_ptr, nbytes), "rt_bind_buffer")
+    def set_post_stream(self, stream_ptr: int | None):
+        """Run denoise + post on a second stream and alternate two G-buffer sets (frame pipelining)."""
+        self._check(self.lib.rt_set_post_stream(self.h, stream_ptr), "rt_set_post_stream")
+
+    def bind_buffer(self, name: str, device_ptr: int, nbytes: int, gbuffer_set: int = 0):
+        what = BUF[name] | (BUF_SET1 if gbuffer_set else 0)
+        self._check(self.lib.rt_bind_buffer(self.h, what, device_ptr, nbytes), "rt_bind_buffer")
 
     def buffer_bytes(self, name: str) -> int:
         return self.lib.rt_buffer_bytes(self.h, BUF[name])
@@ -284,6 +293,23 @@ class RayTracer:
         buf = np.empty(n, dtype=np.uint8)
         self._check(self.lib.rt_download(self.h, what, buf.ctypes.data, n), "rt_download(%s)" % name)
         return buf.view(dtype)
+
+    def trace_rays(self, org, dirs, want_iters=False):
+        """Closest hits of n rays (RaySceneIntersect traversal) through the queue tracer.
+        Returns (t, tri, u, v[, iters], kernel_ms); tri = -1 on a miss."""
+        org = np.asarray(org, np.float32).reshape(-1, 3)
+        dirs = np.asarray(dirs, np.float32).reshape(-1, 3)
+        n = len(org)
+        rays = np.zeros((n, 8), np.float32)
+        rays[:, 0:3] = org
+        rays[:, 4:7] = dirs
+        hits = np.zeros((n, 4), np.float32)
+        iters = np.zeros(n, np.uint32) if want_iters else None
+        ms = C.c_float()
+        self._check(self.lib.rt_trace_rays(self.h, rays.ctypes.data, n, hits.ctypes.data, _ptr(iters), C.byref(ms)),
+                    "rt_trace_rays")
+        out = (hits[:, 0], hits[:, 1].view(np.int32), hits[:, 2], hits[:, 3])
+        return out + ((iters,) if want_iters else ()) + (ms.value,)
 
     def get_buffer(self, name: str, shape=None, dtype=np.uint8) -> np.ndarray:
         if shape is None:

@@ -30,32 +30,42 @@ def strip_rows(height: int, world: int, rank: int) -> tuple[int, int, int]:
 
 
 class StripGather:
-    """Full-frame G-buffer tensors for one rank plus the in-place all-gather of the strips."""
+    """Full-frame G-buffer tensors for one rank plus the in-place all-gather of the strips.
 
-    def __init__(self, width: int, height: int, world: int, rank: int, device, rt=None):
+    With ``sets=2`` (frame pipelining, ``RayTracer.set_post_stream``) both G-buffer sets of the
+    renderer are bound and ``gather`` assembles the set the last path trace wrote."""
+
+    def __init__(self, width: int, height: int, world: int, rank: int, device, rt=None, sets: int = 1):
         import torch
 
         self.W, self.H, self.world, self.rank = width, height, world, rank
+        self.rt = rt
         self.y0, self.rows, self.per = strip_rows(height, world, rank)
-        self.tensors = {}
-        for name, bpp in GBUFFERS:
-            t = torch.zeros(world * self.per * width * bpp, dtype=torch.uint8, device=device)
-            self.tensors[name] = t
-            if rt is not None:
-                rt.bind_buffer(name, t.data_ptr(), t.numel())
+        self.sets = []
+        for k in range(sets):
+            tensors = {}
+            for name, bpp in GBUFFERS:
+                t = torch.zeros(world * self.per * width * bpp, dtype=torch.uint8, device=device)
+                tensors[name] = t
+                if rt is not None:
+                    rt.bind_buffer(name, t.data_ptr(), t.numel(), gbuffer_set=k)
+            self.sets.append(tensors)
+        self.tensors = self.sets[0]
 
-    def chunk(self, name: str):
-        t = self.tensors[name]
+    def chunk(self, name: str, gbuffer_set: int = 0):
+        t = self.sets[gbuffer_set][name]
         n = t.numel() // self.world
         return t[self.rank * n:(self.rank + 1) * n]
 
-    def gather(self, group=None):
+    def gather(self, group=None, gbuffer_set: int | None = None):
         """All-gather every rank's strip into every rank's full-frame tensors (in place)."""
         import torch.distributed as dist
 
+        if gbuffer_set is None:
+            gbuffer_set = self.rt.info().gbufferSet if (self.rt is not None and len(self.sets) > 1) else 0
         nccl = dist.get_backend(group) == "nccl"
         for name, _ in GBUFFERS:
-            t = self.tensors[name]
+            t = self.sets[gbuffer_set][name]
             n = t.numel() // self.world
             mine = t[self.rank * n:(self.rank + 1) * n]
             if nccl:

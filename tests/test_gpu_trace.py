@@ -56,3 +56,40 @@ def test_primary_bit_exact_1080p(rtx, oracle, tmp_path):
 def test_primary_bit_exact_1m_scene(rtx, oracle, tmp_path):
     g, o = run(rtx, oracle, tmp_path, 320, 180, 2, chunk_dim=4)
     assert_same(g, o)
+
+
+def test_trace_rays_queue_and_random_bit_exact(rtx, oracle, tmp_path):
+    """rt_trace_rays (the persistent queue tracer) on the real incoherent bounce rays of a
+    1080p 4-spp frame plus random rays (axis-parallel directions, origins outside the scene),
+    vs oracle.intersect: t, triangle, barycentrics and TraverseBvh iterations."""
+    w, h = 1920, 1080
+    cfg = rtx.write_config(str(tmp_path / "c.toml"), w, h, spp=4)
+    rt = rtx.RayTracer(w, h, cfg).init()
+    rt.set_delta_time(16.667)
+    rt.build_bvh()
+    rt.path_trace(1)
+    rt.sync()
+    n3 = int(rt.download("PT_QUEUE", np.uint32)[0])
+    o3 = rt.download("PT_Q3_ORIGINS", np.float32).reshape(-1, 4)[:n3, :3]
+    d3 = rt.download("PT_Q3_DIRS", np.float32).reshape(-1, 4)[:n3, :3]
+    rng = np.random.default_rng(7)
+    m = 20000
+    ro = rng.uniform(-40.0, 100.0, (m, 3)).astype(np.float32)
+    rd = rng.normal(size=(m, 3)).astype(np.float32)
+    rd[: m // 4, rng.integers(0, 3)] = 0.0     # axis-parallel components (safe_divide path)
+    rd /= np.linalg.norm(rd, axis=1, keepdims=True).astype(np.float32)
+    org = np.concatenate([o3, ro])
+    dirs = np.concatenate([d3, rd])
+    t, tri, u, v, iters, ms = rt.trace_rays(org, dirs, want_iters=True)
+    rt.cleanup()
+    assert n3 > 100000 and ms > 0.0
+    vtx, idx, nt = oracle.scene(1)
+    ob = oracle.build_bvh(vtx, idx, nt, oracle.smooth_normals(vtx, idx))
+    o = oracle.intersect(ob, np.concatenate([org, dirs], axis=1))
+    bits = lambda a: np.ascontiguousarray(a, np.float32).view(np.uint32)
+    assert np.array_equal(bits(t), bits(o["t"]))
+    assert np.array_equal(tri, o["objectIdx"])
+    assert np.array_equal(bits(u), bits(o["u"]))
+    assert np.array_equal(bits(v), bits(o["v"]))
+    assert np.array_equal(iters, o["iterations"])
+    assert (tri >= 0).mean() > 0.05

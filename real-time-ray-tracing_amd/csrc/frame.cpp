@@ -244,7 +244,7 @@ int rt_frame_init(rt_context* ctx) {
     fr.gMotion[0] = fr.motion;
     ALLOC(fr.rays, P * 4);
     ALLOC(fr.ptStats, P * 16);
-    ALLOC(fr.rayCounter, 64);
+    ALLOC(fr.rayCounter, (size_t)kRayCounterSlots * kRayCounterStride * 8);
     {  // wavefront workspace: one entry per traced sample of the strip
         const size_t cap = (size_t)ctx->renderW * ctx->stripRows * ctx->spp;
         if (cap >= (1ull << 31)) { ctx->err = "strip x spp too large for the path-trace queues"; return RT_ERR_ARG; }
@@ -316,7 +316,7 @@ int rt_frame_init(rt_context* ctx) {
     HIP_TRY(ctx, hipMemset(fr.motion, 0, P * 4));
     HIP_TRY(ctx, hipMemset(fr.rays, 0, P * 4));
     HIP_TRY(ctx, hipMemset(fr.ptStats, 0, P * 16));
-    HIP_TRY(ctx, hipMemset(fr.rayCounter, 0, 64));
+    HIP_TRY(ctx, hipMemset(fr.rayCounter, 0, (size_t)kRayCounterSlots * kRayCounterStride * 8));
     HIP_TRY(ctx, hipMemset(fr.colorB, 0, P * 8));
     HIP_TRY(ctx, hipMemset(fr.accum, 0, P * 8));
     HIP_TRY(ctx, hipMemset(fr.histColor, 0, P * 8));
@@ -406,10 +406,13 @@ int rt_get_ray_count(rt_context* ctx, uint64_t* rays, int reset) {
     if (!ctx || !rays) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_get_ray_count before rt_init"; return RT_ERR_STATE; }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<unsigned long long> part((size_t)kRayCounterSlots * kRayCounterStride);
+    const size_t bytes = part.size() * 8;
+    HIP_TRY(ctx, hipMemcpy(part.data(), ctx->fr.rayCounter, bytes, hipMemcpyDeviceToHost));
     unsigned long long v = 0;
-    HIP_TRY(ctx, hipMemcpy(&v, ctx->fr.rayCounter, 8, hipMemcpyDeviceToHost));
+    for (int k = 0; k < kRayCounterSlots; ++k) v += part[(size_t)k * kRayCounterStride];
     *rays = v;
-    if (reset) HIP_TRY(ctx, hipMemset(ctx->fr.rayCounter, 0, 8));
+    if (reset) HIP_TRY(ctx, hipMemset(ctx->fr.rayCounter, 0, bytes));
     return RT_OK;
 }
 

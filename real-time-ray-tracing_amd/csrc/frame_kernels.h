@@ -83,6 +83,12 @@ struct PtWorkspace {
     uint32_t* itersOut = nullptr;  // optional [cap]: traversal iterations per queue entry (rt_trace_rays)
 };
 
+// The frame's traced-ray count is kept as partial sums in kRayCounterSlots slots 128 B apart
+// (one atomic per workgroup into slot blockId % slots; the host adds them): a device-scope
+// atomic on one address serialises at the memory side, and one per workgroup on a single
+// counter cost ~190 us of a 1080p camera-ray launch.
+constexpr int kRayCounterSlots = 256, kRayCounterStride = 16;  // stride in u64
+
 struct PathTraceParams {
     TraceCamera cam;
     float tanHalfFov[2];
@@ -114,7 +120,7 @@ struct PathTraceParams {
     uint32_t* motionOut;        // [W*H] half2
     uint32_t* raysOut;          // optional [W*H] RaySceneIntersect calls that traced
     uint4* statsOut;            // optional [W*H] rays, node visits, triangle tests, diffuse events
-    unsigned long long* rayCounter;  // optional: total traced rays (one atomic per workgroup)
+    unsigned long long* rayCounter;  // optional: total traced rays, kRayCounterSlots partial sums
     PtWorkspace ws;
 };
 

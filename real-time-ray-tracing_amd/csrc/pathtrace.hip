@@ -364,7 +364,8 @@ RT_DEV void add_rays(const PathTraceParams& P, unsigned long long* wgSlots, uint
     const int tid = threadIdx.x;
     if ((tid & 63) == 0) wgSlots[tid >> 6] = r;
     __syncthreads();
-    if (tid == 0) atomicAdd(P.rayCounter, wgSlots[0] + wgSlots[1] + wgSlots[2] + wgSlots[3]);
+    const uint32_t slot = (blockIdx.y * gridDim.x + blockIdx.x) % kRayCounterSlots;
+    if (tid == 0) atomicAdd(&P.rayCounter[slot * kRayCounterStride], wgSlots[0] + wgSlots[1] + wgSlots[2] + wgSlots[3]);
 }
 
 // per-sample init of PathTrace (pathtrace.cuh:20-60) and GenerateRay (raygen.cuh:7-38)

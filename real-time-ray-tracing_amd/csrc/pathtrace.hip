@@ -531,22 +531,34 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
 
 // Steps 0 (hit from k_pt_camera) .. 3 of every sample of the surface pixels.  kGlossy: the
 // material table holds mirror/glass, so steps 1 and 2 may trace (inline, LDS stack).
+//
+// Work layout as in k_pt_camera: a workgroup takes 64-pixel groups of the surface list, and
+// each of its nSW sample waves shades one sample of those pixels per round, so a lane runs one
+// sample's dependent chain (hit, textures, light-CDF searches, BSDF) rather than all spp of
+// them back to back.  The folding thread (sample wave 0) then combines the round's samples in
+// sample order through LDS — colour and albedo sums, the first deferred sample, the per-sample
+// colours the resolve kernel needs — exactly as the sequential loop of PathTrace's caller does.
 template <bool kGlossy>
-__global__ __launch_bounds__(256) void k_pt_shade0(PathTraceParams P) {
+__global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
     __shared__ uint32_t stkA[kGlossy ? 16 * 256 : 1];
     __shared__ float stkT[kGlossy ? 16 * 256 : 1];
     __shared__ uint32_t sob[256];
+    __shared__ float4 foldL[4][64];  // this round's samples: finished colour xyz, w = 1 when deferred
+    __shared__ float4 foldA[4][64];  // their albedo
     __shared__ unsigned long long wgRays[4];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     bn_stage_sobol(P.bluenoise, sob, tid, 256);
     __syncthreads();
     const uint32_t n = P.ws.counters[kCntSurface];
+    const int nSW = cam_sample_waves(P.spp), sw = w % nSW, g = w / nSW;
+    const uint32_t perWg = 64u * (uint32_t)(4 / nSW);
+    const int rounds = ((int)P.spp + nSW - 1) / nSW;
     const SceneView sc = scene_of(P);
     const size_t plane = (size_t)P.rows * P.width;
     uint32_t raysWg = 0;
 #pragma unroll 1
-    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {  // block-uniform
-        const uint32_t i = base + (uint32_t)tid;
+    for (uint32_t base = blockIdx.x * perWg; base < n; base += gridDim.x * perWg) {  // block-uniform
+        const uint32_t i = base + (uint32_t)g * 64u + (uint32_t)lane;
         const bool active = i < n;
         const uint32_t pl = active ? P.ws.surface[i] : 0u;
         const int x = (int)(pl % P.width), yl = (int)(pl / P.width);
@@ -560,17 +572,20 @@ __global__ __launch_bounds__(256) void k_pt_shade0(PathTraceParams P) {
             coneSpread = ray_cone_width(P, x, y);
             centerDir = center_dir(P.cam, x, y);
         }
+        // folding thread (sw == 0) state; sample 0 runs on this same thread in round 0
         F3 L = f3(0.0f), A = f3(0.0f), L0s = f3(0.0f), A0s = f3(0.0f), N0 = f3(0.0f);
         float D0 = 0.0f;
         F2 M0 = {0.0f, 0.0f};
         uint32_t mask0 = 0u;
         int sd = -1;  // first deferred sample
 #pragma unroll 1
-        for (uint32_t s = 0; s < P.spp; ++s) {  // uniform trip count: every lane reaches the appends
+        for (int r = 0; r < rounds; ++r) {  // uniform trip count: every thread reaches the barriers
+            const int s = r * nSW + sw;
+            const bool run = active && s < (int)P.spp;
             PathVars v;
             int kd = 5;
-            if (active) {
-                c.frameIdx = (int)P.spp * (P.frameNum - 1) + 1 + (int)s;
+            if (run) {
+                c.frameIdx = (int)P.spp * (P.frameNum - 1) + 1 + s;
                 start_sample(c, v, x, y, coneSpread, centerDir);
                 const size_t q = (size_t)s * plane + pl;
                 const float4 hr = P.ws.hit0Rec[q];
@@ -585,10 +600,10 @@ __global__ __launch_bounds__(256) void k_pt_shade0(PathTraceParams P) {
             }
             const uint32_t slot3 = wave_append(kd == 3, &P.ws.counters[kCntQ3]);
             const uint32_t slot4 = wave_append(kd == 4, &P.ws.counters[kCntQ4]);
-            if (active) {
-                A = A + v.rs.albedo;
+            float4 outL = make_float4(0.0f, 0.0f, 0.0f, 0.0f), outA = outL;
+            if (run) {
+                outA = make_float4(v.rs.albedo.x, v.rs.albedo.y, v.rs.albedo.z, 0.0f);
                 if (s == 0) {
-                    A0s = v.rs.albedo;
                     N0 = v.outNormal;
                     D0 = v.outDepth;
                     M0 = v.mv;
@@ -596,21 +611,42 @@ __global__ __launch_bounds__(256) void k_pt_shade0(PathTraceParams P) {
                 }
                 if (kd < 5) {
                     ++c.rays;  // the deferred RaySceneIntersect
-                    enqueue(kd == 3 ? P.ws.q3 : P.ws.q4, kd == 3 ? slot3 : slot4, v, p, s);
-                    if (sd < 0) {
-                        sd = (int)s;
-                        if (s > 0) P.ws.pathL[(size_t)pl * P.spp + s - 1] = make_float4(L.x, L.y, L.z, 0.0f);
-                    }
+                    enqueue(kd == 3 ? P.ws.q3 : P.ws.q4, kd == 3 ? slot3 : slot4, v, p, (uint32_t)s);
+                    outL.w = 1.0f;
                 } else {
                     const F3 Ls = finish(c, v);
-                    if (s == 0) L0s = Ls;
-                    if (sd < 0) L = L + Ls;
-                    else P.ws.pathL[(size_t)pl * P.spp + s] = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
+                    outL = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
                 }
             }
+            foldL[w][lane] = outL;
+            foldA[w][lane] = outA;
+            __syncthreads();
+            if (sw == 0 && active) {
+#pragma unroll 1
+                for (int k = 0; k < nSW; ++k) {  // this round's samples in sample order
+                    const int sk = r * nSW + k;
+                    if (sk >= (int)P.spp) break;
+                    const float4 o = foldL[g * nSW + k][lane];
+                    const float4 a = foldA[g * nSW + k][lane];
+                    A = A + f3(a.x, a.y, a.z);
+                    if (sk == 0) A0s = f3(a.x, a.y, a.z);
+                    if (o.w != 0.0f) {
+                        if (sd < 0) {
+                            sd = sk;
+                            if (sk > 0) P.ws.pathL[(size_t)pl * P.spp + sk - 1] = make_float4(L.x, L.y, L.z, 0.0f);
+                        }
+                    } else {
+                        const F3 Ls = f3(o.x, o.y, o.z);
+                        if (sk == 0) L0s = Ls;
+                        if (sd < 0) L = L + Ls;
+                        else P.ws.pathL[(size_t)pl * P.spp + sk] = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
+                    }
+                }
+            }
+            __syncthreads();
         }
-        const uint32_t pslot = wave_append(active && sd >= 0, &P.ws.counters[kCntPending]);
-        if (active) {
+        const uint32_t pslot = wave_append(sw == 0 && active && sd >= 0, &P.ws.counters[kCntPending]);
+        if (sw == 0 && active) {
             if (P.spp == 1) {
                 L = L0s;
                 A = A0s;
@@ -631,15 +667,17 @@ __global__ __launch_bounds__(256) void k_pt_shade0(PathTraceParams P) {
             P.albedoOut[p] = pack_h4(A.x, A.y, A.z, 0u);
             P.depthOut[p] = rt_f2h(D0);
             P.motionOut[p] = (uint32_t)rt_f2h(M0.x) | ((uint32_t)rt_f2h(M0.y) << 16);
-            if (P.raysOut && c.rays) atomicAdd(&P.raysOut[p], c.rays);
-            if (P.statsOut) {
-                if (c.rays) atomicAdd(&P.statsOut[p].x, c.rays);
-                if (c.visits) atomicAdd(&P.statsOut[p].y, c.visits);
-                if (c.tests) atomicAdd(&P.statsOut[p].z, c.tests);
-                if (c.diffuse) atomicAdd(&P.statsOut[p].w, c.diffuse);
-            }
-            raysWg += c.rays;
         }
+        if (active && c.rays) {
+            if (P.raysOut) atomicAdd(&P.raysOut[p], c.rays);
+            if (P.statsOut) atomicAdd(&P.statsOut[p].x, c.rays);
+        }
+        if (active && P.statsOut) {
+            if (c.visits) atomicAdd(&P.statsOut[p].y, c.visits);
+            if (c.tests) atomicAdd(&P.statsOut[p].z, c.tests);
+            if (c.diffuse) atomicAdd(&P.statsOut[p].w, c.diffuse);
+        }
+        raysWg += c.rays;
     }
     add_rays(P, wgRays, raysWg);
 }

@@ -114,12 +114,18 @@ def main():
                            extra="stripY0 = %d\nstripRows = %d\n" % (y0, rows))
     rt = rtx.RayTracer(W, H, cfg).init()
     rt.set_delta_time(DELTA_MS)
-    rt.set_stream(torch.cuda.current_stream(dev).cuda_stream)  # collectives order with the renderer
     pipeline = not args.no_pipeline
-    post = torch.cuda.Stream(dev) if pipeline else None
+    if pipeline:  # the trace chain is the critical path: its stream outranks the denoise stream
+        lo, hi = torch.cuda.Stream.priority_range()
+        main_stream = torch.cuda.Stream(dev, priority=hi)
+        post = torch.cuda.Stream(dev, priority=lo)
+        torch.cuda.set_stream(main_stream)
+    else:
+        post = None
+    rt.set_stream(torch.cuda.current_stream(dev).cuda_stream)  # collectives order with the renderer
     if pipeline:  # denoise/post of frame f on a second stream, overlapping the trace of frame f+1
         rt.set_post_stream(post.cuda_stream)
-    sg = StripGather(W, H, world, rank, dev, rt, sets=2 if pipeline else 1) if world > 1 else None
+    sg = StripGather(W, H, world, rank, dev, rt, sets=rtx.GBUFFER_SETS if pipeline else 1) if world > 1 else None
 
     def frame(f):
         rt.build_bvh()

@@ -140,7 +140,7 @@ typedef struct rt_info {
     int32_t frameNum;           /* frame index of the last rt_draw (0 before the first) */
     int32_t deviceId;
     uint32_t spp;               /* samples (reference PathTrace evaluations) per frame */
-    int32_t gbufferSet;         /* G-buffer set the last rt_path_trace wrote (0 or 1, see rt_set_post_stream) */
+    int32_t gbufferSet;         /* G-buffer set the last rt_path_trace wrote (0..2, see rt_set_post_stream) */
 } rt_info;
 
 int rt_get_info(const rt_context* ctx, rt_info* out);
@@ -201,11 +201,14 @@ int rt_set_stream(rt_context* ctx, void* stream);
  * another): with a post stream set, rt_denoise_post runs the denoiser and post chain on that
  * stream, after everything enqueued on the context stream so far (path trace, G-buffer
  * gathers), and the path tracer alternates between two G-buffer sets, so the trace of frame
- * f+1 overlaps the denoise of frame f.  Results are identical to the serial order.  Host reads
- * (rt_get_buffer, rt_download, rt_sync, rt_draw's copies) wait for both streams.  NULL turns it
- * off.  rt_info.gbufferSet names the set the last path trace wrote; bind the second set's
- * buffers with name | RT_BUF_SET1. */
+ * f+1 overlaps the denoise of frame f; the LBVH build and camera rays of the next frame run on
+ * an internal third stream beside the current frame's trace kernels (two LBVH sets, three
+ * G-buffer sets).  Results are identical to the serial order.  Host reads (rt_get_buffer,
+ * rt_download, rt_sync, rt_draw's copies) wait for all streams.  NULL turns it off.
+ * rt_info.gbufferSet names the set the last path trace wrote; bind the other sets' buffers
+ * with name | RT_BUF_SET1 / RT_BUF_SET2. */
 #define RT_BUF_SET1 0x100
+#define RT_BUF_SET2 0x200
 int rt_set_post_stream(rt_context* ctx, void* stream);
 
 /* Use caller-owned device memory (>= rt_buffer_bytes, 16-B aligned) as one of the path-trace

@@ -304,6 +304,9 @@ int rt_init(rt_context* ctx) {
     ALLOC(ctx->dTlasReorder, 4096);
     ALLOC(ctx->dTlasNodes, (size_t)ctx->B * 64);
     ALLOC(ctx->dCounter, 64);
+    ctx->bvh[0] = BvhBufs{ctx->dTriPos, ctx->dTriNrm, ctx->dAabbs, ctx->dBatchScene, ctx->dMorton, ctx->dReorder,
+                          ctx->dNodes, ctx->dTlasAabbs, ctx->dTlasScene, ctx->dTlasMorton, ctx->dTlasReorder,
+                          ctx->dTlasNodes, ctx->dCounter};
     ALLOC(ctx->dBlueNoise, 327680);
     const size_t P = (size_t)ctx->renderW * ctx->renderH;
     ALLOC(ctx->dHits, P * 16);
@@ -352,8 +355,12 @@ int rt_init(rt_context* ctx) {
 void rt_destroy(rt_context* ctx) {
     if (!ctx) return;
     if (ctx->stream) (void)sync_streams(ctx);
-    for (hipEvent_t e : {ctx->ptDone[0], ctx->ptDone[1], ctx->postDone[0], ctx->postDone[1], ctx->overlapEv})
+    for (hipEvent_t e : {ctx->overlapEv, ctx->cameraGate, ctx->buildDone[0], ctx->buildDone[1], ctx->bvhFree[0], ctx->bvhFree[1]})
         if (e) (void)hipEventDestroy(e);
+    for (int k = 0; k < kGbSets; ++k)
+        for (hipEvent_t e : {ctx->ptDone[k], ctx->postDone[k], ctx->camDone[k], ctx->restDone[k]})
+            if (e) (void)hipEventDestroy(e);
+    if (ctx->sideStream) (void)hipStreamDestroy(ctx->sideStream);
     for (void* p : ctx->allocations) (void)hipFree(p);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -417,9 +424,34 @@ int rt_get_info(const rt_context* ctx, rt_info* out) {
     return RT_OK;
 }
 
+void bvh_select(rt_context* ctx, int k) {
+    const BvhBufs& b = ctx->bvh[k];
+    ctx->bvhSet = k;
+    ctx->dTriPos = b.triPos;
+    ctx->dTriNrm = b.triNrm;
+    ctx->dAabbs = b.aabbs;
+    ctx->dBatchScene = b.batchScene;
+    ctx->dMorton = b.morton;
+    ctx->dReorder = b.reorder;
+    ctx->dNodes = b.nodes;
+    ctx->dTlasAabbs = b.tlasAabbs;
+    ctx->dTlasScene = b.tlasScene;
+    ctx->dTlasMorton = b.tlasMorton;
+    ctx->dTlasReorder = b.tlasReorder;
+    ctx->dTlasNodes = b.tlasNodes;
+    ctx->dCounter = b.counter;
+}
+
 int rt_build_bvh(rt_context* ctx) {
     if (!ctx) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_build_bvh before rt_init"; return RT_ERR_STATE; }
+    hipStream_t stream = ctx->stream;
+    if (ctx->postStream) {  // frame pipelining: build into the other set, on the side stream
+        const int k = ctx->bvhSet ^ 1;
+        if (ctx->bvhInFlight[k]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->sideStream, ctx->bvhFree[k], 0));
+        bvh_select(ctx, k);
+        stream = ctx->sideStream;
+    }
     BvhBuildParams p;
     p.vertices = ctx->dVerts;
     p.normals = ctx->dNormals;
@@ -440,7 +472,18 @@ int rt_build_bvh(rt_context* ctx) {
     p.tlasReorder = ctx->dTlasReorder;
     p.tlasNodes = ctx->dTlasNodes;
     p.counter = ctx->dCounter;
-    HIP_TRY(ctx, rtk_launch_build_bvh(&p, ctx->stream));
+    HIP_TRY(ctx, rtk_launch_build_bvh(&p, stream));
+    if (ctx->postStream) {
+        HIP_TRY(ctx, hipEventRecord(ctx->buildDone[ctx->bvhSet], stream));
+        ctx->buildOnSide[ctx->bvhSet] = true;
+    }
+    return RT_OK;
+}
+
+// a context-stream user of the current LBVH waits for its build on the side stream
+int wait_bvh(rt_context* ctx) {
+    if (ctx->postStream && ctx->buildOnSide[ctx->bvhSet])
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->buildDone[ctx->bvhSet], 0));
     return RT_OK;
 }
 
@@ -465,6 +508,7 @@ int rt_trace_primary(rt_context* ctx, int frame_num, int with_detail) {
     p.normalOut = with_detail ? ctx->dHitNrm : nullptr;
     p.fakeNormalOut = with_detail ? ctx->dHitFake : nullptr;
     p.statsOut = with_detail ? ctx->dHitStats : nullptr;
+    if (int rc = wait_bvh(ctx)) return rc;
     HIP_TRY(ctx, rtk_launch_trace_primary(&p, ctx->stream));
     return RT_OK;
 }
@@ -510,7 +554,13 @@ int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms) {
 int rt_time_path_trace_kernels(rt_context* ctx, int iters, float* kernel_ms, int n) {
     if (!ctx || !kernel_ms || iters < 1 || n < kPtKernels) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_time_path_trace_kernels before rt_init"; return RT_ERR_STATE; }
-    if (int rc0 = sync_streams(ctx)) return rc0;
+    if (ctx->postStream) {  // kernels are timed serially on the context stream
+        void* post = ctx->postStream;
+        int rc = rt_set_post_stream(ctx, nullptr);
+        if (rc == RT_OK) rc = rt_time_path_trace_kernels(ctx, iters, kernel_ms, n);
+        const int rc2 = rt_set_post_stream(ctx, post);
+        return rc != RT_OK ? rc : rc2;
+    }
     hipEvent_t marks[kPtKernels + 1] = {};
     int rc = RT_OK;
     for (auto& m : marks)

@@ -19,6 +19,26 @@ struct HostCamera {  // Camera::update outputs (kernel.cuh:103-121)
 };
 
 // Device buffers of RayTracer::draw after the BVH (kernel.cu:259-398)
+// Build outputs and scratch of one LBVH (bvh_build.hip).  With frame pipelining there are two,
+// so frame f+1's build and camera rays run beside frame f's trace kernels.
+struct BvhBufs {
+    float4* triPos = nullptr;
+    float4* triNrm = nullptr;
+    float* aabbs = nullptr;
+    float* batchScene = nullptr;
+    uint32_t* morton = nullptr;
+    uint32_t* reorder = nullptr;
+    void* nodes = nullptr;
+    float* tlasAabbs = nullptr;
+    float* tlasScene = nullptr;
+    uint32_t* tlasMorton = nullptr;
+    uint32_t* tlasReorder = nullptr;
+    void* tlasNodes = nullptr;
+    uint32_t* counter = nullptr;
+};
+
+constexpr int kGbSets = 3;  // G-buffer / camera-output sets in flight with frame pipelining
+
 struct FrameResources {
     bool ready = false;
     // sky / sun (kernel.cu:280-307)
@@ -40,15 +60,16 @@ struct FrameResources {
     uint2* texAlbedo = nullptr;
     uint2* texNormal = nullptr;
     // path-trace G-buffer (pathtrace.cuh:11-128): the set the last path trace wrote.  With a
-    // post stream (rt_set_post_stream) the path tracer alternates between two sets gX[0/1], so
-    // frame f+1 is traced while frame f is denoised; without one it always uses set 0.
-    uint2* gColor[2] = {};
-    uint2* gNormal[2] = {};
-    uint2* gAlbedo[2] = {};
-    uint16_t* gDepth[2] = {};
-    uint32_t* gMotion[2] = {};
+    // post stream (rt_set_post_stream) the path tracer cycles through kGbSets sets, so the
+    // camera rays of frame f+1 and the rest of frame f are traced while frame f-1 is denoised;
+    // without one it always uses set 0.
+    uint2* gColor[kGbSets] = {};
+    uint2* gNormal[kGbSets] = {};
+    uint2* gAlbedo[kGbSets] = {};
+    uint16_t* gDepth[kGbSets] = {};
+    uint32_t* gMotion[kGbSets] = {};
     int gbSet = 0;
-    bool setInFlight[2] = {false, false};  // a denoise on the post stream reads this set
+    bool setInFlight[kGbSets] = {};  // a denoise on the post stream reads this set
     uint2* color = nullptr;
     uint2* normal = nullptr;
     uint2* albedo = nullptr;
@@ -58,6 +79,13 @@ struct FrameResources {
     uint4* ptStats = nullptr;
     unsigned long long* rayCounter = nullptr;
     PtWorkspace ws{};              // wavefront queues of the path tracer (pathtrace.hip)
+    // camera-kernel outputs, one slot per G-buffer set (the camera rays of frame f+1 are traced
+    // while the shade/trace kernels of frame f still read slot f's hit records)
+    float4* camHit0Rec[kGbSets] = {};
+    float* camHit0Err[kGbSets] = {};
+    uint32_t* camSurface[kGbSets] = {};
+    uint32_t* camCount[kGbSets] = {};
+    bool camInFlight[kGbSets] = {};
     HistCamera hist{};
     bool histValid = false;
     // denoise + post (denoising.cu, postprocessing.cu)
@@ -118,13 +146,21 @@ struct rt_context {
     hipStream_t ownStream = nullptr;   // the one rt_init created (destroyed by rt_destroy)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t postStream = nullptr;  // optional: denoise + post run here (rt_set_post_stream)
-    hipEvent_t ptDone[2] = {}, postDone[2] = {}, overlapEv = nullptr;
+    hipStream_t sideStream = nullptr;  // pipelining: LBVH build + camera rays of the next frame
+    hipEvent_t ptDone[kGbSets] = {}, postDone[kGbSets] = {}, overlapEv = nullptr;
+    hipEvent_t buildDone[2] = {}, bvhFree[2] = {}, camDone[kGbSets] = {}, restDone[kGbSets] = {};
+    bool bvhInFlight[2] = {false, false}, buildOnSide[2] = {false, false};
+    BvhBufs bvh[2];
+    int bvhSet = 0;
     // frame pipelining: rt_denoise_post(f) is enqueued on the post stream only once the next
     // path trace has enqueued kernel `overlapAfter` (so it fills the trace stages' idle tails), or
     // at the next host read / denoise call, whichever comes first
     bool postPending = false;
     int postPendingSet = 0;
     int overlapAfter = 1;  // after k_pt_shade0: measured best
+    int cameraAfter = 3;   // the next frame's camera rays start after this frame's kernel #3
+    hipEvent_t cameraGate = nullptr;
+    bool cameraGated = false;
     DenoisePostParams postParams{};
     hipEvent_t* ptMarks = nullptr;  // set only inside rt_time_path_trace_kernels
     float* dVerts = nullptr;
@@ -174,7 +210,9 @@ int dalloc(rt_context* ctx, T** p, size_t bytes) {
     return rc;
 }
 int rt_frame_init(rt_context* ctx);  // frame.cpp: sky tables, textures, G-buffers
-int sync_streams(rt_context* ctx);   // frame.cpp: context stream + post stream
+int sync_streams(rt_context* ctx);   // frame.cpp: context, post and side streams
+extern "C" void bvh_select(rt_context* ctx, int k);  // context.cpp: point the dTriPos.. views at bvh[k]
+extern "C" int wait_bvh(rt_context* ctx);  // context.cpp: context stream waits for the LBVH build
 std::string rt_data_dir();
 void rt_camera_update(const rt_camera& in, int renderW, int renderH, HostCamera& c);
 TraceCamera rt_trace_camera(const HostCamera& c);

@@ -116,6 +116,10 @@ int update_sky(rt_context* ctx) {
     const V3 sunDir = sun_direction(sp.timeOfDay, sp.sunAxisAngle);
     fr.sunDir[0] = sunDir.x; fr.sunDir[1] = sunDir.y; fr.sunDir[2] = sunDir.z;
     if (fr.skyValid && !sp.needRegenerate && sky_params_equal(sp, fr.lastSky)) return RT_OK;
+    if (ctx->postStream) {  // frame pipelining: nothing may read the sky while it is rewritten
+        const int rc = sync_streams(ctx);
+        if (rc != RT_OK) return rc;
+    }
     sp.sunScalar = sp.sunScalar > 0.00001f ? sp.sunScalar : 0.00001f;
     sp.skyScalar = sp.skyScalar > 0.00001f ? sp.skyScalar : 0.00001f;
     sp.sunAngle = sp.sunAngle > 0.51f ? sp.sunAngle : 0.51f;
@@ -143,6 +147,7 @@ int update_sky(rt_context* ctx) {
     p.sunCdf = fr.sunCdf;
     p.scanSums = fr.scanSums;
     HIP_TRY(ctx, rtk_launch_sky(&p, ctx->stream));
+    if (ctx->postStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // before the side stream's camera rays
     fr.sunArea = rt_powf(rt_tanf(sunRadius), 2.0f) * kPi;
     fr.cosThetaMax = p.cosThetaMax;
     fr.skyValid = true;
@@ -187,13 +192,21 @@ int issue_pending_post(rt_context* ctx) {
 }
 
 namespace {
-// PtLaunchHook: the previous frame's denoise starts once this frame's kernel `overlapAfter`
-// has been enqueued, so it runs beside the trace stages' latency-bound tails
-hipError_t overlap_hook(void* arg) {
+// PtLaunchHook of a pipelined frame: after kernel `overlapAfter` the previous frame's denoise
+// is issued (it then runs beside the trace stages' latency-bound tails), and after kernel
+// `cameraAfter` the gate event the next frame's camera rays wait for is recorded
+hipError_t overlap_hook(void* arg, int kernel) {
     rt_context* ctx = (rt_context*)arg;
-    hipError_t e = hipEventRecord(ctx->overlapEv, ctx->stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->postStream, ctx->overlapEv, 0);
-    if (e == hipSuccess && issue_pending_post(ctx) != RT_OK) e = hipErrorUnknown;
+    hipError_t e = hipSuccess;
+    if (kernel == ctx->overlapAfter && ctx->postPending) {
+        e = hipEventRecord(ctx->overlapEv, ctx->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(ctx->postStream, ctx->overlapEv, 0);
+        if (e == hipSuccess && issue_pending_post(ctx) != RT_OK) e = hipErrorUnknown;
+    }
+    if (e == hipSuccess && kernel == ctx->cameraAfter) {
+        e = hipEventRecord(ctx->cameraGate, ctx->stream);
+        ctx->cameraGated = e == hipSuccess;
+    }
     return e;
 }
 }  // namespace
@@ -204,6 +217,7 @@ int sync_streams(rt_context* ctx) {
         const int rc = issue_pending_post(ctx);
         if (rc != RT_OK) return rc;
     }
+    if (ctx->sideStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->sideStream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->postStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->postStream));
     return RT_OK;
@@ -264,6 +278,11 @@ int rt_frame_init(rt_context* ctx) {
         ALLOC(ws.pathL, cap * 16);
         ALLOC(ws.pending, (size_t)ctx->renderW * ctx->stripRows * 4);
         ALLOC(ws.surface, (size_t)ctx->renderW * ctx->stripRows * 4);
+        ALLOC(fr.camCount[0], 64);
+        fr.camHit0Rec[0] = ws.hit0Rec;
+        fr.camHit0Err[0] = ws.hit0Err;
+        fr.camSurface[0] = ws.surface;
+        ws.camCount = fr.camCount[0];
         ALLOC(ws.counters, kWsCounterWords * 4);
         ws.fetch = ws.counters + 64;
         int dev = 0, cus = 0;
@@ -338,7 +357,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     if (!ctx->inited) { ctx->err = "rt_path_trace before rt_init"; return RT_ERR_STATE; }
     FrameResources& fr = ctx->fr;
     if (ctx->postStream) {  // frame pipelining: trace into the set no denoise still reads
-        fr.gbSet ^= 1;
+        fr.gbSet = (fr.gbSet + 1) % kGbSets;
         select_gbuffers(fr);
         if (fr.setInFlight[fr.gbSet]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->postDone[fr.gbSet], 0));
     }
@@ -384,17 +403,46 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.statsOut = with_detail ? fr.ptStats : nullptr;
     p.rayCounter = fr.rayCounter;
     p.ws = fr.ws;
+    const int g = fr.gbSet;  // camera-output slot = G-buffer set
+    p.ws.hit0Rec = fr.camHit0Rec[g];
+    p.ws.hit0Err = fr.camHit0Err[g];
+    p.ws.surface = fr.camSurface[g];
+    p.ws.camCount = fr.camCount[g];
     {  // material table (init.cu:215-251): only mirror / glass ids make steps 1-2 trace
         const int m = ctx->materialOverride;
         p.ws.glossy = m >= 0 && (m == 1 || m == 5 || m >= 10);
     }
-    if (with_detail) {
+    if (with_detail) {  // per-pixel counters: everything in order on the context stream
+        if (ctx->postStream && (rc = sync_streams(ctx)) != RT_OK) return rc;
         HIP_TRY(ctx, hipMemsetAsync(fr.rays, 0, (size_t)ctx->renderW * ctx->renderH * 4, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(fr.ptStats, 0, (size_t)ctx->renderW * ctx->renderH * 16, ctx->stream));
     }
-    PtLaunchHook hook{ctx->overlapAfter, overlap_hook, ctx};
-    HIP_TRY(ctx, rtk_launch_pathtrace(&p, ctx->stream, ctx->ptMarks, ctx->postPending ? &hook : nullptr));
+    // Frame pipelining: the camera rays go to the side stream behind this frame's LBVH build,
+    // so they run beside the previous frame's trace tails; they wait only for the readers of
+    // this slot's G-buffers (the denoise of frame f-2) and camera outputs (shade of frame f-2).
+    const bool side = ctx->postStream && !with_detail;
+    hipStream_t cs = side ? ctx->sideStream : ctx->stream;
+    if (side) {
+        if (fr.setInFlight[g]) HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->postDone[g], 0));
+        if (fr.camInFlight[g]) HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->restDone[g], 0));
+        if (ctx->cameraGated) HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->cameraGate, 0));
+    } else if ((rc = wait_bvh(ctx)) != RT_OK) {
+        return rc;
+    }
+    HIP_TRY(ctx, rtk_launch_pt_camera(&p, cs, ctx->ptMarks));
+    if (side) {
+        HIP_TRY(ctx, hipEventRecord(ctx->camDone[g], cs));
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->camDone[g], 0));
+    }
+    PtLaunchHook hook{overlap_hook, ctx};
+    HIP_TRY(ctx, rtk_launch_pt_rest(&p, ctx->stream, ctx->ptMarks, ctx->postStream ? &hook : nullptr));
     if (ctx->postPending && (rc = issue_pending_post(ctx)) != RT_OK) return rc;
+    if (ctx->postStream) {
+        HIP_TRY(ctx, hipEventRecord(ctx->restDone[g], ctx->stream));
+        fr.camInFlight[g] = true;
+        HIP_TRY(ctx, hipEventRecord(ctx->bvhFree[ctx->bvhSet], ctx->stream));
+        ctx->bvhInFlight[ctx->bvhSet] = true;
+    }
     fr.renderColor = fr.color;
     fr.hist = hist_of(hc);  // HistoryCamera::Setup after PathTrace (kernel.cu:357)
     fr.histValid = true;
@@ -564,25 +612,69 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
     int rc = sync_streams(ctx);
     if (rc != RT_OK) return rc;
     FrameResources& fr = ctx->fr;
-    fr.setInFlight[0] = fr.setInFlight[1] = false;
+    for (int k = 0; k < kGbSets; ++k) fr.setInFlight[k] = false;
     if (!stream) {
         ctx->postStream = nullptr;
         return RT_OK;
     }
     const size_t P = (size_t)ctx->renderW * ctx->renderH;
 #define ALLOC(p, bytes) if (!(p) && (rc = dalloc(ctx, &(p), (bytes))) != RT_OK) return rc
-    ALLOC(fr.gColor[1], P * 8);
-    ALLOC(fr.gNormal[1], P * 8);
-    ALLOC(fr.gAlbedo[1], P * 8);
-    ALLOC(fr.gDepth[1], P * 2);
-    ALLOC(fr.gMotion[1], P * 4);
+    for (int k = 1; k < kGbSets; ++k) {  // further G-buffer sets and camera-output slots
+        const size_t cap = fr.ws.cap, strip = (size_t)ctx->renderW * ctx->stripRows;
+        ALLOC(fr.gColor[k], P * 8);
+        ALLOC(fr.gNormal[k], P * 8);
+        ALLOC(fr.gAlbedo[k], P * 8);
+        ALLOC(fr.gDepth[k], P * 2);
+        ALLOC(fr.gMotion[k], P * 4);
+        ALLOC(fr.camHit0Rec[k], cap * 16);
+        ALLOC(fr.camHit0Err[k], cap * 4);
+        ALLOC(fr.camSurface[k], strip * 4);
+        ALLOC(fr.camCount[k], 64);
+    }
+    {  // second LBVH set: frame f+1's build and camera rays beside frame f's traces
+        const size_t NP = ctx->mesh.triCountPadded, B = ctx->B;
+        BvhBufs& b = ctx->bvh[1];
+        ALLOC(b.triPos, NP * 48);
+        ALLOC(b.triNrm, NP * 48);
+        ALLOC(b.aabbs, NP * 24);
+        ALLOC(b.batchScene, B * 24);
+        ALLOC(b.morton, B * 4096);
+        ALLOC(b.reorder, B * 4096);
+        ALLOC(b.nodes, B * 1024 * 64);
+        ALLOC(b.tlasAabbs, B * 24);
+        ALLOC(b.tlasScene, 24);
+        ALLOC(b.tlasMorton, 4096);
+        ALLOC(b.tlasReorder, 4096);
+        ALLOC(b.tlasNodes, B * 64);
+        if (!b.counter) {
+            ALLOC(b.counter, 64);
+            HIP_TRY(ctx, hipMemset(b.counter, 0, 64));
+        }
+    }
 #undef ALLOC
-    for (int k = 0; k < 2; ++k) {
+    if (!ctx->sideStream) {  // lowest priority: it should fill what the trace chain leaves idle
+        int least = 0, greatest = 0;
+        HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(ctx, hipStreamCreateWithPriority(&ctx->sideStream, hipStreamNonBlocking, least));
+    }
+    for (hipEvent_t* e : {&ctx->buildDone[0], &ctx->buildDone[1], &ctx->bvhFree[0], &ctx->bvhFree[1]})
+        if (!*e) HIP_TRY(ctx, hipEventCreateWithFlags(e, hipEventDisableTiming));
+    for (int k = 0; k < kGbSets; ++k) {
+        if (!ctx->camDone[k]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->camDone[k], hipEventDisableTiming));
+        if (!ctx->restDone[k]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->restDone[k], hipEventDisableTiming));
+        fr.camInFlight[k] = false;
+    }
+    ctx->bvhInFlight[0] = ctx->bvhInFlight[1] = false;
+    ctx->buildOnSide[0] = ctx->buildOnSide[1] = false;
+    for (int k = 0; k < kGbSets; ++k) {
         if (!ctx->ptDone[k]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ptDone[k], hipEventDisableTiming));
         if (!ctx->postDone[k]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->postDone[k], hipEventDisableTiming));
     }
     if (!ctx->overlapEv) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->overlapEv, hipEventDisableTiming));
-    if (const char* a = getenv("RTX_OVERLAP_AFTER")) ctx->overlapAfter = atoi(a);  // tuning aid
+    if (!ctx->cameraGate) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->cameraGate, hipEventDisableTiming));
+    ctx->cameraGated = false;
+    if (const char* a = getenv("RTX_OVERLAP_AFTER")) ctx->overlapAfter = atoi(a);  // tuning aids
+    if (const char* a = getenv("RTX_CAMERA_AFTER")) ctx->cameraAfter = atoi(a);
     ctx->postStream = (hipStream_t)stream;
     return RT_OK;
 }
@@ -590,14 +682,16 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
 int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
     if (!ctx || !device_ptr) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_bind_buffer before rt_init"; return RT_ERR_STATE; }
-    const size_t need = rt_buffer_bytes(ctx, name & ~RT_BUF_SET1);
+    const int set = (name >> 8) & 3;  // RT_BUF_SET1 / RT_BUF_SET2
+    name &= 0xFF;
+    if (set >= kGbSets) { ctx->err = "rt_bind_buffer: no such G-buffer set"; return RT_ERR_ARG; }
+    const size_t need = rt_buffer_bytes(ctx, name);
     if (need == 0 || bytes < need) { ctx->err = "rt_bind_buffer: unknown buffer or too small"; return RT_ERR_ARG; }
     if (((uintptr_t)device_ptr & 15u) != 0) { ctx->err = "rt_bind_buffer: pointer must be 16-byte aligned"; return RT_ERR_ARG; }
     int rc = sync_streams(ctx);
     if (rc != RT_OK) return rc;
     FrameResources& fr = ctx->fr;
-    const int set = (name & RT_BUF_SET1) ? 1 : 0;
-    switch (name & ~RT_BUF_SET1) {
+    switch (name) {
         case RT_BUF_RENDER_COLOR: fr.gColor[set] = (uint2*)device_ptr; break;
         case RT_BUF_NORMAL: fr.gNormal[set] = (uint2*)device_ptr; break;
         case RT_BUF_ALBEDO: fr.gAlbedo[set] = (uint2*)device_ptr; break;
@@ -776,6 +870,7 @@ int rt_trace_rays(rt_context* ctx, const float* rays, uint32_t n, float* hits, u
     p.tlasNodes = ctx->dTlasNodes;
     p.ws = fr.ws;
     p.ws.itersOut = iters ? reinterpret_cast<uint32_t*>(fr.ws.pathL) : nullptr;  // pathL: per-frame scratch
+    if (int rc = sync_streams(ctx)) return rc;  // the queue buffers are shared with in-flight frames
     HIP_TRY(ctx, hipMemcpyAsync(fr.ws.q3.rayO, o.data(), (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(fr.ws.q3.rayD, d.data(), (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(fr.ws.counters, 0, kWsCounterWords * sizeof(uint32_t), ctx->stream));

@@ -75,6 +75,7 @@ struct PtWorkspace {
     float4* pathL;              // [rows*W*spp] per-sample radiance of pixels resolved late
     uint32_t* pending;          // [rows*W] pixel (strip-local) | first deferred sample << 26
     uint32_t* surface;          // [rows*W] strip-local pixels with a sample that hit geometry
+    uint32_t* camCount;         // [16] k_pt_camera's append counter of `surface` (copied to counters[kCntSurface])
     uint32_t* counters;         // [kCntSlots]
     uint32_t* fetch;            // [2][8 parts x 16]: k_trace_queue fetch counters, 64 B apart
     uint32_t cap;               // entries per queue (= rows * W * spp)
@@ -174,11 +175,15 @@ extern "C" hipError_t rtk_launch_scan(const float* in, float* out, float* sums, 
 // kernels of one path-trace launch: camera, shade, trace<3>, resume<3>, trace<4>, resume<4>, resolve
 constexpr int kPtKernels = 7;
 struct PtLaunchHook {
-    int after;                        // kernel index (0 = camera, 1 = shade, ...)
-    hipError_t (*fn)(void* arg);
+    hipError_t (*fn)(void* arg, int kernel);  // after each kernel is enqueued (1 = shade, 2 = trace<3>, ...)
     void* arg;
 };
-extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
-                                           const PtLaunchHook* hook);
+// The camera kernel (writes the hit records, the surface list and the sky pixels' G-buffer) and
+// the rest (shade .. resolve) can go to different streams: the frame pipeline runs the camera
+// rays of frame f+1 beside the trace tails of frame f (frame.cpp).  marks: kPtKernels + 1 events,
+// [0..1] recorded by the camera launcher, [1..7] by the rest (rt_time_path_trace_kernels).
+extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks);
+extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
+                                         const PtLaunchHook* hook);
 extern "C" int rtk_trace_queue_blocks_per_cu();
 extern "C" hipError_t rtk_launch_trace_queue(const PathTraceParams* p, int step, hipStream_t stream);

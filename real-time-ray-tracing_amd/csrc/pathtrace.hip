@@ -510,7 +510,7 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
         if (P.raysOut) atomicAdd(&P.raysOut[p], rays);
         if (P.statsOut) atomicAdd(&P.statsOut[p].x, rays);
     }
-    const uint32_t slot = wave_append(sw == 0 && surface, &P.ws.counters[kCntSurface]);
+    const uint32_t slot = wave_append(sw == 0 && surface, P.ws.camCount);
     if (sw == 0 && active) {
         if (surface) {
             P.ws.surface[slot] = pl;
@@ -778,32 +778,39 @@ __global__ __launch_bounds__(256) void k_pt_resolve(PathTraceParams P) {
 }
 
 
-// marks (optional, kPtKernels + 1 events): recorded before the first and after every kernel so
-// a timing host can split the stage per kernel (rt_time_path_trace_kernels).
-// hook (optional): called on the host right after kernel hook->after (0 = camera) is enqueued;
-// the frame pipeline issues the previous frame's denoise there (frame.cpp).
-extern "C" hipError_t rtk_launch_pathtrace(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
-                                           const PtLaunchHook* hook) {
+extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks) {
     if (p->spp < 1 || p->spp > 64 || p->ws.persistBlocks < 1) return hipErrorInvalidValue;
     if ((size_t)p->rows * p->width >= (1u << 26) || (size_t)p->rows * p->width * p->spp > p->ws.cap)
         return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
+    hipError_t e = hipMemsetAsync(p->ws.camCount, 0, 16 * sizeof(uint32_t), stream);
+    if (e == hipSuccess && marks) e = hipEventRecord(marks[0], stream);
     if (e != hipSuccess) return e;
-    int k = 0;
+    const int nSW = cam_sample_waves(p->spp);
+    const int BW = nSW == 4 ? 8 : 16, BH = nSW == 1 ? 16 : 8;
+    const dim3 grid((p->width + BW - 1) / BW, (p->rows + BH - 1) / BH);
+    hipLaunchKernelGGL(k_pt_camera, grid, dim3(256), 0, stream, *p);
+    if (marks && (e = hipEventRecord(marks[1], stream)) != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+// hook (optional): called on the host right after each kernel is enqueued; the frame pipeline
+// issues the previous frame's denoise and gates the next frame's camera rays there (frame.cpp).
+extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
+                                         const PtLaunchHook* hook) {
+    hipError_t e = hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(p->ws.counters + kCntSurface, p->ws.camCount, sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                           stream);
+    if (e != hipSuccess) return e;
+    int k = 2;  // marks[2] = end of the shade kernel
     auto mark = [&]() {
-        if (hook && hook->fn && k == hook->after + 1) {
-            const hipError_t he = hook->fn(hook->arg);
+        if (hook && hook->fn) {
+            const hipError_t he = hook->fn(hook->arg, k - 1);
             if (he != hipSuccess) return he;
         }
         if (!marks) { ++k; return hipSuccess; }
         return hipEventRecord(marks[k++], stream);
     };
-    if ((e = mark()) != hipSuccess) return e;
-    const int nSW = cam_sample_waves(p->spp);
-    const int BW = nSW == 4 ? 8 : 16, BH = nSW == 1 ? 16 : 8;
-    const dim3 grid((p->width + BW - 1) / BW, (p->rows + BH - 1) / BH);
-    hipLaunchKernelGGL(k_pt_camera, grid, dim3(256), 0, stream, *p);
-    if ((e = mark()) != hipSuccess) return e;
     if (p->ws.glossy) hipLaunchKernelGGL(k_pt_shade0<true>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
     else hipLaunchKernelGGL(k_pt_shade0<false>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
     if ((e = mark()) != hipSuccess) return e;

@@ -119,7 +119,8 @@ SIGNATURES = {
     "rt_save_image": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
 }
 IMAGE_PPM_RGBA8, IMAGE_PFM_HDR = 0, 1
-BUF_SET1 = 0x100  # rt_bind_buffer: second G-buffer set (frame pipelining, rt_set_post_stream)
+BUF_SET1, BUF_SET2 = 0x100, 0x200  # rt_bind_buffer: further G-buffer sets (frame pipelining)
+GBUFFER_SETS = 3  # G-buffer sets a pipelined context cycles through (rt_set_post_stream)
 
 _lib = None
 
@@ -248,7 +249,7 @@ class RayTracer:
         self._check(self.lib.rt_set_post_stream(self.h, stream_ptr), "rt_set_post_stream")
 
     def bind_buffer(self, name: str, device_ptr: int, nbytes: int, gbuffer_set: int = 0):
-        what = BUF[name] | (BUF_SET1 if gbuffer_set else 0)
+        what = BUF[name] | (int(gbuffer_set) << 8)  # RT_BUF_SET1 / RT_BUF_SET2
         self._check(self.lib.rt_bind_buffer(self.h, what, device_ptr, nbytes), "rt_bind_buffer")
 
     def buffer_bytes(self, name: str) -> int:

@@ -32,8 +32,8 @@ def strip_rows(height: int, world: int, rank: int) -> tuple[int, int, int]:
 class StripGather:
     """Full-frame G-buffer tensors for one rank plus the in-place all-gather of the strips.
 
-    With ``sets=2`` (frame pipelining, ``RayTracer.set_post_stream``) both G-buffer sets of the
-    renderer are bound and ``gather`` assembles the set the last path trace wrote."""
+    With ``sets=rtx.GBUFFER_SETS`` (frame pipelining, ``RayTracer.set_post_stream``) every G-buffer
+    set of the renderer is bound and ``gather`` assembles the set the last path trace wrote."""
 
     def __init__(self, width: int, height: int, world: int, rank: int, device, rt=None, sets: int = 1):
         import torch

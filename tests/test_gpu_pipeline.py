@@ -54,7 +54,7 @@ def run(rtx, tmp_path, pipelined, per_frame):
 def test_pipelined_frames_match_serial(rtx, tmp_path):
     ref, ref_imgs, s0 = run(rtx, tmp_path, False, True)
     got, _, s1 = run(rtx, tmp_path, True, False)
-    assert s0 == 0 and s1 == FRAMES % 2
+    assert s0 == 0 and s1 == FRAMES % rtx.GBUFFER_SETS
     for k in ref:
         assert np.array_equal(ref[k], got[k]), k
     _, imgs, _ = run(rtx, tmp_path, True, True)

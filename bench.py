@@ -15,6 +15,12 @@ horizontal strip of the frame, the strips' G-buffers are all-gathered in place o
 (rtx/dist.py), and every rank runs the denoise/post chain on the full frame (exact vs 1 GPU).
 Total work per frame is fixed as N grows ("strong" scaling).  Timing: barrier + device sync on
 both sides of exactly K frames, max over ranks; value = rays of all ranks / that time.
+
+Frames are pipelined (rt_set_post_stream; --no-pipeline for serial frames): the denoise/post
+chain of frame f runs on a second stream beside the trace kernels of frame f+1, and the LBVH
+build + camera rays of frame f+1 on a third beside the trace tails of frame f.  Every frame's
+full work is inside the timed region: the last frame's deferred denoise is issued and waited
+for (rt.sync) before the closing device sync.
 """
 import argparse
 import json
@@ -35,7 +41,7 @@ HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (spec peak)
 DELTA_MS = 16.667      # fixed AutoExposure step (SURVEY §8d determinism settings)
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_pathtrace.json")
 
-# algorithmic bytes of one path-trace stage launch (DESIGN.md §6): per traced ray the node and
+# algorithmic bytes of one path-trace stage launch (DESIGN.md §4.1): per traced ray the node and
 # triangle records a traversal must read, per pixel the G-buffer it writes, per diffuse event
 # the 48 texel taps of the triplanar soil textures
 NODE_B, TRI_B, GBUF_B, TEX_B = 64, 48, 30, 48 * 8
@@ -145,6 +151,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         frame(args.warmup + 1 + k)
+    rt.sync()  # issues the last frame's deferred denoise/post and waits for every renderer stream
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -180,13 +187,14 @@ def main():
                    "width": W, "height": H, "spp": S,
                    "parallelism": ("screen strips x%d + RCCL all-gather of G-buffers" % world if world > 1
                                    else "single GPU")
-                                  + ("; 2 frames in flight (trace f+1 || denoise f on a second stream)"
-                                     if pipeline else "; serial frames")},
+                                  + ("; pipelined frames: denoise/post of f-1 and LBVH build + camera rays of "
+                                     "f+1 on their own streams beside the trace kernels of f" if pipeline
+                                     else "; serial frames")},
         "fps": round(1000.0 / ms_per_step, 2),
         "rays_per_frame": int(rays // args.steps),
     }
 
-    # ---- roofline of the path-trace stage over this rank's strip (DESIGN.md §6): the stage is the
+    # ---- roofline of the path-trace stage over this rank's strip (DESIGN.md §4.1): the stage is the
     # dominant part of the frame; its seven kernels hand rays to each other through queues in HBM,
     # so the stage, not one kernel of it, is the unit whose algorithmic bytes are defined
     rt.path_trace(args.warmup + args.steps + 1, detail=True)

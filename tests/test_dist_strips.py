@@ -84,3 +84,40 @@ def test_strip_rows_cover_frame(h, world):
 def test_strip_rows_rejects_too_many_ranks():
     with pytest.raises(ValueError):
         strip_rows(10, 8, 7)
+
+
+def worker_sets(rank, world, port, result_dir):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sg = StripGather(W, H, world, rank, torch.device("cpu"), sets=3)
+        for k in range(3):  # rank r writes value 10 * k + r into its strip of set k
+            for name, bpp in GBUFFERS:
+                sg.chunk(name, k).fill_(10 * k + rank)
+        sg.gather(gbuffer_set=1)  # only set 1 is assembled
+        out = {"%s_%d" % (name, k): sg.sets[k][name].numpy().copy() for name, _ in GBUFFERS for k in range(3)}
+        np.savez(os.path.join(result_dir, "rank%d.npz" % rank), **out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_strip_allgather_pipelined_sets(tmp_path):
+    """Frame pipelining binds three G-buffer sets; gather(set k) assembles set k only."""
+    import torch.multiprocessing as mp
+
+    world = 2
+    mp.start_processes(worker_sets, args=(world, free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
+    for r in range(world):
+        d = np.load(tmp_path / ("rank%d.npz" % r))
+        for name, bpp in GBUFFERS:
+            per = d["%s_0" % name].size // world
+            for k in range(3):
+                a = d["%s_%d" % (name, k)]
+                for q in range(world):
+                    # gathered set: every rank's strip; the others: this rank's own strip only
+                    want = 10 * k + q if (k == 1 or q == r) else 0
+                    assert (a[q * per:(q + 1) * per] == want).all(), (r, name, k, q)

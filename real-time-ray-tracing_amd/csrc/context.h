@@ -52,6 +52,8 @@ struct FrameResources {
     float* sunPdf = nullptr;
     float* sunCdf = nullptr;
     float* scanSums = nullptr;
+    float* skyTree = nullptr;   // light-CDF probe heaps (kSkyTreeNodes / kSunTreeNodes)
+    float* sunTree = nullptr;
     bool skyValid = false;
     rt_sky_params lastSky{};
     float sunDir[3] = {0, 1, 0};

@@ -146,6 +146,8 @@ int update_sky(rt_context* ctx) {
     p.sunPdf = fr.sunPdf;
     p.sunCdf = fr.sunCdf;
     p.scanSums = fr.scanSums;
+    p.skyTree = fr.skyTree;
+    p.sunTree = fr.sunTree;
     HIP_TRY(ctx, rtk_launch_sky(&p, ctx->stream));
     if (ctx->postStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // before the side stream's camera rays
     fr.sunArea = rt_powf(rt_tanf(sunRadius), 2.0f) * kPi;
@@ -243,6 +245,8 @@ int rt_frame_init(rt_context* ctx) {
     ALLOC(fr.sunPdf, (size_t)kSunSize * 4);
     ALLOC(fr.sunCdf, (size_t)kSunSize * 4);
     ALLOC(fr.scanSums, 512 * 4);
+    ALLOC(fr.skyTree, (size_t)kSkyTreeNodes * 4);
+    ALLOC(fr.sunTree, (size_t)kSunTreeNodes * 4);
     ALLOC(fr.texAlbedo, (size_t)kTexTexels * 8);
     ALLOC(fr.texNormal, (size_t)kTexTexels * 8);
     const size_t P = (size_t)ctx->renderW * ctx->renderH;
@@ -392,6 +396,8 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.sunBuffer = fr.sun;
     p.skyCdf = fr.skyCdf;
     p.sunCdf = fr.sunCdf;
+    p.skyTree = fr.skyTree;
+    p.sunTree = fr.sunTree;
     memcpy(p.sunDir, fr.sunDir, 12);
     p.cosThetaMax = fr.cosThetaMax;
     p.colorOut = fr.color;

@@ -42,7 +42,15 @@ struct SkyGenParams {
     float* sunPdf;        // [1024]
     float* sunCdf;        // [1024]
     float* scanSums;      // [>= 512] block totals
+    float* skyTree;       // [kSkyTreeNodes] bisection probe tree of skyCdf (cdf_tree)
+    float* sunTree;       // [kSunTreeNodes] of sunCdf
 };
+
+// The first levels of SampleLight's CDF bisection (light.cuh:9-31) as a heap: node 1 holds the
+// CDF value the search probes first, node j's children 2j / 2j + 1 the values it probes after
+// a[mid] >= target / a[mid] < target.  Kernels stage the heap in LDS and walk it for the first
+// log2(nodes) probes, then continue in global memory: the same probes, the same result.
+constexpr int kSkyTreeNodes = 4096, kSunTreeNodes = 1024;
 
 struct HistCamera { float pos[3], left[3], up[3], dir[3]; };  // HistoryCamera (kernel.cuh:135-155)
 
@@ -112,6 +120,8 @@ struct PathTraceParams {
     const float4* sunBuffer;
     const float* skyCdf;
     const float* sunCdf;
+    const float* skyTree;       // [kSkyTreeNodes] (SkyGenParams::skyTree)
+    const float* sunTree;       // [kSunTreeNodes]
     float sunDir[3];
     float cosThetaMax;
     uint2* colorOut;            // [W*H] half3 demodulated colour + ushort material mask

@@ -49,7 +49,15 @@ struct PathCtx {
     BnPixel bp;
     int frameIdx;
     uint32_t rays, visits, tests, diffuse;
+    const float* skyTree = nullptr;  // LDS copies of the light-CDF probe heaps (stage_cdf_trees)
+    const float* sunTree = nullptr;
 };
+
+// copy the light-CDF probe heaps into LDS (all threads of the workgroup; caller syncs)
+RT_DEV void stage_cdf_trees(const PathTraceParams& P, float* sky, float* sun, int tid, int nthreads) {
+    for (int i = tid; i < kSkyTreeNodes / 4; i += nthreads) reinterpret_cast<float4*>(sky)[i] = reinterpret_cast<const float4*>(P.skyTree)[i];
+    for (int i = tid; i < kSunTreeNodes / 4; i += nthreads) reinterpret_cast<float4*>(sun)[i] = reinterpret_cast<const float4*>(P.sunTree)[i];
+}
 
 // blue-noise sample (frameIdx * 4 + k, dim d) of this pixel (pathtrace.cuh:116-129)
 RT_DEV float rnd(const PathCtx& c, int k, int d) { return bn_value(c.sob, c.bp, c.frameIdx * 4 + k, d); }
@@ -196,7 +204,7 @@ RT_DEV void diffuse(PathCtx& c, int bounce, RayState& rs, F3& beta) {
     F3 lDir;
     float lPdf = 1.0f;
     int lIdx;
-    sample_light(P, c.sunDir, lDir, lPdf, lIdx, r2[0], r2[1]);
+    sample_light(P, c.sunDir, lDir, lPdf, lIdx, r2[0], r2[1], c.skyTree, c.sunTree);
     F3 sDir, sBsdf, lBsdf, tmp;
     float sPdf = 0.0f;
     if (rs.matType == LAMBERTIAN) {
@@ -546,8 +554,11 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
     __shared__ float4 foldL[4][64];  // this round's samples: finished colour xyz, w = 1 when deferred
     __shared__ float4 foldA[4][64];  // their albedo
     __shared__ unsigned long long wgRays[4];
+    __shared__ __align__(16) float sSkyTree[kSkyTreeNodes];
+    __shared__ __align__(16) float sSunTree[kSunTreeNodes];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     bn_stage_sobol(P.bluenoise, sob, tid, 256);
+    stage_cdf_trees(P, sSkyTree, sSunTree, tid, 256);
     __syncthreads();
     const uint32_t n = P.ws.counters[kCntSurface];
     const int nSW = cam_sample_waves(P.spp), sw = w % nSW, g = w / nSW;
@@ -565,6 +576,8 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
         const int y = (int)P.y0 + yl;
         const uint32_t p = (uint32_t)y * P.width + (uint32_t)x;
         PathCtx c{P, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), sob, BnPixel{0u, 0u}, 0, 0u, 0u, 0u, 0u};
+        c.skyTree = sSkyTree;
+        c.sunTree = sSunTree;
         float coneSpread = 0.0f;
         F3 centerDir = f3(0.0f);
         if (active) {  // per-pixel invariants of the sample loop
@@ -687,8 +700,12 @@ template <int kStep>
 __global__ __launch_bounds__(256) void k_pt_resume(PathTraceParams P) {
     __shared__ uint32_t sob[256];
     __shared__ unsigned long long wgRays[4];
+    // step 4 ends the path before any diffuse interaction: no light sampling there
+    __shared__ __align__(16) float sSkyTree[kStep == 3 ? kSkyTreeNodes : 4];
+    __shared__ __align__(16) float sSunTree[kStep == 3 ? kSunTreeNodes : 4];
     const int tid = threadIdx.x;
     bn_stage_sobol(P.bluenoise, sob, tid, 256);
+    if (kStep == 3) stage_cdf_trees(P, sSkyTree, sSunTree, tid, 256);
     __syncthreads();
     const PtQueue& q = kStep == 3 ? P.ws.q3 : P.ws.q4;
     const uint32_t n = P.ws.counters[kStep == 3 ? kCntQ3 : kCntQ4];
@@ -699,6 +716,8 @@ __global__ __launch_bounds__(256) void k_pt_resume(PathTraceParams P) {
         const uint32_t i = base + (uint32_t)tid;
         const bool active = i < n;
         PathCtx c{P, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), sob, BnPixel{0u, 0u}, 0, 0u, 0u, 0u, 0u};
+        c.skyTree = sSkyTree;
+        c.sunTree = sSunTree;
         PathVars v;
         int kd = 5;
         uint32_t p = 0, s = 0;

@@ -197,13 +197,32 @@ RT_DEV int cdf_search(const float* a, int left, int right, float target) {
     return left;
 }
 
-RT_DEV void sample_light(const PathTraceParams& P, F3 sunDir, F3& dir, float& pdf, int& lightIdx, float r0, float r1) {
+// BinarySearch (light.cuh:9-31) with its first probes read from the LDS heap `tree` (see
+// kSkyTreeNodes): identical probes, identical result, fewer dependent global loads
+RT_DEV int cdf_search_tree(const float* a, int right, float target, const float* tree, int nodes) {
+    int left = 0, j = 1;
+    while (right - left > 1) {
+        const int mid = (left + right) / 2;
+        const float v = j < nodes ? tree[j] : a[mid];
+        if (v < target) {
+            left = mid;
+            j = 2 * j + 1;
+        } else {
+            right = mid;
+            j = 2 * j;
+        }
+    }
+    return left;
+}
+
+RT_DEV void sample_light(const PathTraceParams& P, F3 sunDir, F3& dir, float& pdf, int& lightIdx, float r0, float r1,
+                         const float* skyTree, const float* sunTree) {
     const float maxSky = P.skyCdf[kSkySize - 1], maxSun = P.sunCdf[kSunSize - 1];
     const float totalSky = maxSky * kTwoPi / kSkySize;
     const float totalSun = maxSun * kTwoPi * (1.0f - P.cosThetaMax) / kSunSize;
     const float pSky = totalSky / (totalSky + totalSun);
     if (pSky > r1) {
-        const int idx = cdf_search(P.skyCdf, 0, kSkySize - 2, r0 * maxSky) + 1;
+        const int idx = cdf_search_tree(P.skyCdf, kSkySize - 2, r0 * maxSky, skyTree, kSkyTreeNodes) + 1;
         float p = (P.skyCdf[idx] - P.skyCdf[idx - 1]) / maxSky;
         p = p * kSkySize / kTwoPi;
         const float u = ((float)(idx % kSkyW) + 0.5f) / kSkyW;
@@ -211,7 +230,7 @@ RT_DEV void sample_light(const PathTraceParams& P, F3 sunDir, F3& dir, float& pd
         dir = equal_area_map(u, v);
         pdf = p * 1.0f * pSky;
     } else {
-        const int idx = cdf_search(P.sunCdf, 0, kSunSize - 2, r0 * maxSun) + 1;
+        const int idx = cdf_search_tree(P.sunCdf, kSunSize - 2, r0 * maxSun, sunTree, kSunTreeNodes) + 1;
         float p = (P.sunCdf[idx] - P.sunCdf[idx - 1]) / maxSun;
         p = p * kSunSize / (kTwoPi * (1.0f - P.cosThetaMax));
         const float u = ((float)(idx % kSunW) + 0.5f) / kSunW;

@@ -194,10 +194,34 @@ extern "C" hipError_t rtk_launch_scan(const float* in, float* out, float* sums, 
     return hipGetLastError();
 }
 
+// heap node j of the bisection over [0, right0] of `cdf` (see kSkyTreeNodes); nodes the
+// search can never reach (its interval already closed) hold NaN
+__global__ void k_cdf_tree(const float* cdf, int right0, float* tree, int nodes) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nodes) return;
+    if (j == 0) { tree[0] = __builtin_nanf(""); return; }
+    const int depth = 31 - __clz(j);
+    int left = 0, right = right0;
+    bool live = right - left > 1;
+    for (int b = depth - 1; b >= 0 && live; --b) {
+        const int mid = (left + right) / 2;
+        if ((j >> b) & 1) left = mid;
+        else right = mid;
+        live = right - left > 1;
+    }
+    tree[j] = live ? cdf[(left + right) / 2] : __builtin_nanf("");
+}
+
 extern "C" hipError_t rtk_launch_sky(const SkyGenParams* p, hipStream_t stream) {
     hipLaunchKernelGGL(k_sky, dim3(kSkySize / 256), dim3(256), 0, stream, *p);
     hipError_t e = rtk_launch_scan(p->skyPdf, p->skyCdf, p->scanSums, kSkySize, kSkyScanBlock, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sun, dim3(kSunSize / 256), dim3(256), 0, stream, *p);
-    return rtk_launch_scan(p->sunPdf, p->sunCdf, p->scanSums, kSunSize, kSunScanBlock, stream);
+    if ((e = rtk_launch_scan(p->sunPdf, p->sunCdf, p->scanSums, kSunSize, kSunScanBlock, stream)) != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(k_cdf_tree, dim3(kSkyTreeNodes / 256), dim3(256), 0, stream, p->skyCdf, kSkySize - 2,
+                       p->skyTree, kSkyTreeNodes);
+    hipLaunchKernelGGL(k_cdf_tree, dim3(kSunTreeNodes / 256), dim3(256), 0, stream, p->sunCdf, kSunSize - 2,
+                       p->sunTree, kSunTreeNodes);
+    return hipGetLastError();
 }

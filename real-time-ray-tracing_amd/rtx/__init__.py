@@ -125,11 +125,13 @@ GBUFFER_SETS = 3  # G-buffer sets a pipelined context cycles through (rt_set_pos
 _lib = None
 
 
-def load_library(path: str = LIB_PATH) -> C.CDLL:
-    """Load librtx.so; raises if it is missing (no fallback path exists)."""
+def load_library(path: str | None = None) -> C.CDLL:
+    """Load librtx.so (RTX_LIB overrides the in-tree path, for ablation builds); raises if it is
+    missing (no fallback path exists)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("RTX_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError("librtx.so not found at %s — run `make` (or __graft_entry__.build())" % path)
     lib = C.CDLL(path)

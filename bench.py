@@ -10,9 +10,10 @@ camera: per-frame two-level LBVH rebuild (kernel.cu:330-331), the path tracer at
 Mray/s (every RaySceneIntersect that ran a traversal: primary, bounce and shadow rays, counted
 on the GPU) with ms/frame and the LBVH build ms as extra fields.
 
-N ranks (torch.distributed.run, one per GPU): each rank rebuilds the BVH, path traces its
-horizontal strip of the frame, the strips' G-buffers are all-gathered in place over RCCL
-(rtx/dist.py), and every rank runs the denoise/post chain on the full frame (exact vs 1 GPU).
+N ranks (torch.distributed.run, one per GPU): each rank rebuilds the BVH, path traces its rows
+of the frame (16-row blocks dealt round-robin, so every rank gets its share of the geometry
+rows), the ranks' G-buffer blocks are all-gathered over RCCL (rtx/dist.py, one collective per
+frame), and every rank runs the denoise/post chain on the full frame (exact vs 1 GPU).
 Total work per frame is fixed as N grows ("strong" scaling).  Timing: barrier + device sync on
 both sides of exactly K frames, max over ranks; value = rays of all ranks / that time.
 
@@ -103,7 +104,7 @@ def main():
     import torch.distributed as dist
 
     import rtx
-    from rtx.dist import StripGather, strip_rows
+    from rtx.dist import StripGather, strip_blocks, strip_config
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -114,10 +115,10 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     W, H, S = args.width, args.height, args.spp
-    y0, rows, _ = strip_rows(H, world, rank)
+    rows = sum(r for _, r in strip_blocks(H, world, rank))
     tmp = tempfile.mkdtemp(prefix="rtxbench")
     cfg = rtx.write_config(os.path.join(tmp, "bench.toml"), W, H, dynamic=False, chunk_dim=1, spp=S,
-                           extra="stripY0 = %d\nstripRows = %d\n" % (y0, rows))
+                           extra=strip_config(world, rank))
     rt = rtx.RayTracer(W, H, cfg).init()
     rt.set_delta_time(DELTA_MS)
     pipeline = not args.no_pipeline
@@ -185,7 +186,7 @@ def main():
         "config": {"workload": "BASELINE config 3: %dx%d, %d spp path trace + SVGF denoise + auto-exposure/"
                                "tone map, per-frame LBVH rebuild" % (W, H, S),
                    "width": W, "height": H, "spp": S,
-                   "parallelism": ("screen strips x%d + RCCL all-gather of G-buffers" % world if world > 1
+                   "parallelism": ("interleaved 16-row strips x%d + RCCL all-gather of G-buffers" % world if world > 1
                                    else "single GPU")
                                   + ("; pipelined frames: denoise/post of f-1 and LBVH build + camera rays of "
                                      "f+1 on their own streams beside the trace kernels of f" if pipeline
@@ -198,7 +199,7 @@ def main():
     # dominant part of the frame; its seven kernels hand rays to each other through queues in HBM,
     # so the stage, not one kernel of it, is the unit whose algorithmic bytes are defined
     rt.path_trace(args.warmup + args.steps + 1, detail=True)
-    st = rt.download("PT_STATS", np.uint32).reshape(-1, 4)[y0 * W:(y0 + rows) * W].astype(np.uint64)
+    st = rt.download("PT_STATS", np.uint32).reshape(-1, 4).astype(np.uint64)  # zero outside this rank's rows
     n_rays, visits, tests, diffuse = (int(st[:, k].sum()) for k in range(4))
     alg_bytes = NODE_B * visits + TRI_B * tests + GBUF_B * W * rows + TEX_B * diffuse
     iters = 20

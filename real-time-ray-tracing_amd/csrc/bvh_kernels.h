@@ -32,10 +32,34 @@ struct TraceCamera {
     float invRes[2];
 };
 
+// The frame rows one context traces (multi-GPU split).  Strip-local row yl maps to
+// frame row y0 + yl for a contiguous strip (nStrips = 1); with nStrips > 1 the frame's blocks of
+// kRowBlock rows are dealt round-robin and this context owns every block b with b mod nStrips ==
+// strip (starting at y0 = 0), so every rank gets an equal share of the expensive (geometry)
+// rows wherever the camera puts them.
+constexpr uint32_t kRowBlock = 16;
+__host__ __device__ inline uint32_t row_of(uint32_t y0, uint32_t nStrips, uint32_t strip, uint32_t yl) {
+    return y0 + ((yl / kRowBlock) * nStrips + strip) * kRowBlock + yl % kRowBlock;
+}
+__host__ __device__ inline uint32_t local_row(uint32_t y0, uint32_t nStrips, uint32_t y) {
+    const uint32_t r = y - y0;
+    return (r / kRowBlock / nStrips) * kRowBlock + r % kRowBlock;
+}
+// rows of strip `strip` in a frame of `height` rows
+inline uint32_t strip_row_count(uint32_t height, uint32_t nStrips, uint32_t strip) {
+    uint32_t n = 0;
+    for (uint32_t b = strip; b * kRowBlock < height; b += nStrips) {
+        const uint32_t lo = b * kRowBlock, hi = lo + kRowBlock < height ? lo + kRowBlock : height;
+        n += hi - lo;
+    }
+    return n;
+}
+
 struct TracePrimaryParams {
     TraceCamera cam;
     uint32_t width, height;
-    uint32_t y0, rows;          // rows [y0, y0 + rows) of the frame are traced
+    uint32_t y0, rows;          // strip rows (row_of): contiguous [y0, y0 + rows) when nStrips = 1
+    uint32_t nStrips, strip;
     int frameNum;
     const uint8_t* bluenoise;   // sobol | scrambling | ranking
     const float4* triPos;

@@ -226,6 +226,8 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
     ctx->device = rttoml::find_or_int(doc, "render", "device", -1);
     ctx->stripY0 = rttoml::find_or_int(doc, "render", "stripY0", 0);
     ctx->stripRows = rttoml::find_or_int(doc, "render", "stripRows", -1);
+    ctx->stripCount = rttoml::find_or_int(doc, "render", "stripCount", 1);
+    ctx->stripIndex = rttoml::find_or_int(doc, "render", "stripIndex", 0);
     ctx->materialOverride = rttoml::find_or_int(doc, "render", "materialOverride", -1);
     if (ctx->screenW <= 0 || ctx->screenH <= 0 || ctx->screenW > 16384 || ctx->screenH > 16384 || ctx->spp < 1 ||
         ctx->spp > 64 || ctx->chunkDim < 1 || ctx->chunkDim > 8) {
@@ -236,8 +238,16 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
     // init.cu:58-67: dynamic resolution renders at the max size
     if (ctx->useDynamicResolution) { ctx->renderW = ctx->maxWidth; ctx->renderH = ctx->maxHeight; }
     else { ctx->renderW = ctx->screenW; ctx->renderH = ctx->screenH; }
+    if (ctx->stripCount > 1) {  // interleaved row blocks (row_of): stripY0 / stripRows do not apply
+        if (ctx->stripIndex < 0 || ctx->stripIndex >= ctx->stripCount || ctx->stripY0 != 0 || ctx->stripRows >= 0) {
+            g_createError = "stripCount > 1 needs 0 <= stripIndex < stripCount and no stripY0 / stripRows";
+            delete ctx;
+            return RT_ERR_ARG;
+        }
+        ctx->stripRows = (int)strip_row_count((uint32_t)ctx->renderH, (uint32_t)ctx->stripCount, (uint32_t)ctx->stripIndex);
+    }
     if (ctx->stripRows < 0) ctx->stripRows = ctx->renderH - ctx->stripY0;
-    if (ctx->stripY0 < 0 || ctx->stripRows < 1 || ctx->stripY0 + ctx->stripRows > ctx->renderH) {
+    if (ctx->stripCount < 1 || ctx->stripY0 < 0 || ctx->stripRows < 1 || ctx->stripY0 + ctx->stripRows > ctx->renderH) {
         g_createError = "invalid strip rows";
         delete ctx;
         return RT_ERR_ARG;
@@ -498,6 +508,8 @@ int rt_trace_primary(rt_context* ctx, int frame_num, int with_detail) {
     p.height = (uint32_t)ctx->renderH;
     p.y0 = (uint32_t)ctx->stripY0;
     p.rows = (uint32_t)ctx->stripRows;
+    p.nStrips = (uint32_t)ctx->stripCount;
+    p.strip = (uint32_t)ctx->stripIndex;
     p.frameNum = frame_num;
     p.bluenoise = ctx->dBlueNoise;
     p.triPos = ctx->dTriPos;

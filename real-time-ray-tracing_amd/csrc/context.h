@@ -128,6 +128,7 @@ struct rt_context {
     std::string meshFile;  // [scene] meshFile: meshProcessor .bin instead of the procedural scene
     int spp = 1;
     int stripY0 = 0, stripRows = -1;  // [render] stripY0/stripRows: screen-strip split
+    int stripCount = 1, stripIndex = 0;  // [render] stripCount/stripIndex: interleaved row blocks (row_of)
     int device = -1;
     int materialOverride = -1;  // [render] materialOverride: one material for every triangle (tests)
 

@@ -381,6 +381,8 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.height = (uint32_t)ctx->renderH;
     p.y0 = (uint32_t)ctx->stripY0;
     p.rows = (uint32_t)ctx->stripRows;
+    p.nStrips = (uint32_t)ctx->stripCount;
+    p.strip = (uint32_t)ctx->stripIndex;
     p.frameNum = frame_num;
     p.spp = (uint32_t)ctx->spp;
     p.materialOverride = ctx->materialOverride;

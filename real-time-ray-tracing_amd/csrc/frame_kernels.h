@@ -104,7 +104,8 @@ struct PathTraceParams {
     float res[2];
     HistCamera hist;
     uint32_t width, height;     // full render size (strides)
-    uint32_t y0, rows;          // rows [y0, y0 + rows) are traced
+    uint32_t y0, rows;          // strip rows (row_of): contiguous [y0, y0 + rows) when nStrips = 1
+    uint32_t nStrips, strip;
     int frameNum;
     uint32_t spp;               // samples per pixel (>= 1), frame index spp*(frameNum-1)+1+s
     int materialOverride;       // < 0: reference material table (material 3 everywhere)

@@ -432,7 +432,7 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
     const int x = blockIdx.x * BW + (g % tilesX) * 8 + (lane & 7);
     const int yl = blockIdx.y * BH + (g / tilesX) * 8 + (lane >> 3);
     const bool active = x < (int)P.width && yl < (int)P.rows;
-    const int y = (int)P.y0 + yl;
+    const int y = (int)row_of(P.y0, P.nStrips, P.strip, (uint32_t)yl);
     const uint32_t p = (uint32_t)y * P.width + (uint32_t)x;
     const uint32_t pl = (uint32_t)yl * P.width + (uint32_t)x;
     const size_t plane = (size_t)P.rows * P.width;
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
         const bool active = i < n;
         const uint32_t pl = active ? P.ws.surface[i] : 0u;
         const int x = (int)(pl % P.width), yl = (int)(pl / P.width);
-        const int y = (int)P.y0 + yl;
+        const int y = (int)row_of(P.y0, P.nStrips, P.strip, (uint32_t)yl);
         const uint32_t p = (uint32_t)y * P.width + (uint32_t)x;
         PathCtx c{P, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), sob, BnPixel{0u, 0u}, 0, 0u, 0u, 0u, 0u};
         c.skyTree = sSkyTree;
@@ -759,7 +759,7 @@ __global__ __launch_bounds__(256) void k_pt_resume(PathTraceParams P) {
                 enqueue(P.ws.q4, slot, v, p, s);
             } else {
                 const F3 Ls = finish(c, v);
-                const uint32_t pl = p - P.y0 * P.width;
+                const uint32_t pl = local_row(P.y0, P.nStrips, p / P.width) * P.width + p % P.width;
                 P.ws.pathL[(size_t)pl * P.spp + s] = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
             }
             if (P.raysOut && c.rays) atomicAdd(&P.raysOut[p], c.rays);
@@ -790,7 +790,7 @@ __global__ __launch_bounds__(256) void k_pt_resolve(PathTraceParams P) {
             for (uint32_t s = sd; s < P.spp; ++s) L = L + f3(ls[s].x, ls[s].y, ls[s].z);
             L = L / (float)P.spp;
         }
-        const uint32_t p = pl + P.y0 * P.width;
+        const uint32_t p = row_of(P.y0, P.nStrips, P.strip, pl / P.width) * P.width + pl % P.width;
         const uint32_t mask = P.colorOut[p].y >> 16;
         P.colorOut[p] = pack_h4(L.x, L.y, L.z, mask);
     }

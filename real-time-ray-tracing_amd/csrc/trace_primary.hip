@@ -22,7 +22,7 @@ __global__ __launch_bounds__(256) void k_trace_primary(TracePrimaryParams P) {
     const int x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
     const int yl = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
     if (x >= (int)P.width || yl >= (int)P.rows) return;
-    const int y = (int)P.y0 + yl;
+    const int y = (int)row_of(P.y0, P.nStrips, P.strip, (uint32_t)yl);
 
     const int s = P.frameNum * 4 + 0;
     const F2 pix = {bluenoise(P.bluenoise, x, y, s, 0), bluenoise(P.bluenoise, x, y, s, 1)};

@@ -10,9 +10,9 @@ import socket
 import numpy as np
 import pytest
 
-from rtx.dist import GBUFFERS, StripGather, strip_rows
+from rtx.dist import GBUFFERS, ROW_BLOCK, StripGather, strip_blocks, strip_rows
 
-W, H = 48, 30
+W, H = 48, 72
 ORACLE_KEYS = dict(RENDER_COLOR="color", NORMAL="normal", ALBEDO="albedo", DEPTH="depth", MOTION="motion")
 
 
@@ -44,11 +44,12 @@ def worker(rank, world, port, result_dir):
         v, i, n = O.scene(1)
         bvh = O.build_bvh(v, i, n, O.smooth_normals(v, i))
         sg = StripGather(W, H, world, rank, torch.device("cpu"))
-        g = O.pathtrace(bvh, W, H, frame_num=2, cam=camera(O), y0=sg.y0, rows=sg.rows, threads=1)
-        for name, bpp in GBUFFERS:
-            a = np.ascontiguousarray(g[ORACLE_KEYS[name]]).view(np.uint8).reshape(-1)
-            lo, hi = sg.y0 * W * bpp, (sg.y0 + sg.rows) * W * bpp
-            sg.tensors[name][lo:hi] = torch.from_numpy(a[lo:hi].copy())
+        for y0, rows in strip_blocks(H, world, rank):  # this rank's interleaved row blocks
+            g = O.pathtrace(bvh, W, H, frame_num=2, cam=camera(O), y0=y0, rows=rows, threads=1)
+            for name, bpp in GBUFFERS:
+                a = np.ascontiguousarray(g[ORACLE_KEYS[name]]).view(np.uint8).reshape(-1)
+                lo, hi = y0 * W * bpp, (y0 + rows) * W * bpp
+                sg.tensors[name][lo:hi] = torch.from_numpy(a[lo:hi].copy())
         sg.gather()
         out = {name: sg.tensors[name][:W * H * bpp].numpy().copy() for name, bpp in GBUFFERS}
         np.savez(os.path.join(result_dir, "rank%d.npz" % rank), **out)
@@ -69,6 +70,17 @@ def test_strip_allgather_matches_full_frame(tmp_path, world, oracle):
         for name, _ in GBUFFERS:
             ref = np.ascontiguousarray(full[ORACLE_KEYS[name]]).view(np.uint8).reshape(-1)
             assert np.array_equal(got[name], ref), (r, name)
+
+
+@pytest.mark.parametrize("h,world", [(1080, 1), (1080, 2), (1080, 8), (1081, 8), (2160, 8), (30, 2), (144, 3)])
+def test_strip_blocks_cover_frame(h, world):
+    """Interleaved row blocks: every row owned by exactly one rank, block b by rank b mod N."""
+    covered = np.zeros(h, np.int32)
+    for r in range(world):
+        for y0, rows in strip_blocks(h, world, r):
+            assert (y0 // ROW_BLOCK) % world == r and 1 <= rows <= ROW_BLOCK
+            covered[y0:y0 + rows] += 1
+    assert (covered == 1).all()
 
 
 @pytest.mark.parametrize("h,world", [(1080, 1), (1080, 2), (1080, 8), (1081, 8), (2160, 8), (30, 3)])
@@ -95,9 +107,9 @@ def worker_sets(rank, world, port, result_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         sg = StripGather(W, H, world, rank, torch.device("cpu"), sets=3)
-        for k in range(3):  # rank r writes value 10 * k + r into its strip of set k
+        for k in range(3):  # rank r writes value 10 * k + r into its row blocks of set k
             for name, bpp in GBUFFERS:
-                sg.chunk(name, k).fill_(10 * k + rank)
+                sg.mine(name, k).fill_(10 * k + rank)
         sg.gather(gbuffer_set=1)  # only set 1 is assembled
         out = {"%s_%d" % (name, k): sg.sets[k][name].numpy().copy() for name, _ in GBUFFERS for k in range(3)}
         np.savez(os.path.join(result_dir, "rank%d.npz" % rank), **out)
@@ -114,10 +126,10 @@ def test_strip_allgather_pipelined_sets(tmp_path):
     for r in range(world):
         d = np.load(tmp_path / ("rank%d.npz" % r))
         for name, bpp in GBUFFERS:
-            per = d["%s_0" % name].size // world
+            blk = ROW_BLOCK * W * bpp
             for k in range(3):
-                a = d["%s_%d" % (name, k)]
+                a = d["%s_%d" % (name, k)].reshape(-1, world, blk)  # [round, owner rank, block]
                 for q in range(world):
-                    # gathered set: every rank's strip; the others: this rank's own strip only
+                    # gathered set: every rank's blocks; the others: this rank's own blocks only
                     want = 10 * k + q if (k == 1 or q == r) else 0
-                    assert (a[q * per:(q + 1) * per] == want).all(), (r, name, k, q)
+                    assert (a[:, q] == want).all(), (r, name, k, q)

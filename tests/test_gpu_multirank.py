@@ -1,4 +1,4 @@
-"""The multi-GPU frame path (rtx/dist.py: screen strips + in-place G-buffer gather, frame
+"""The multi-GPU frame path (rtx/dist.py: interleaved row blocks + G-buffer all-gather, frame
 pipelining with three bound G-buffer sets) run by two ranks sharing one GPU over gloo, which
 moves the same device tensors RCCL would.  Every rank's final RGBA8 image and HDR colour must
 equal a single-rank render of the same frames, bit for bit."""
@@ -26,7 +26,7 @@ def render(rank, world, port, out_dir):
     import torch.distributed as dist
 
     import rtx
-    from rtx.dist import StripGather, strip_rows
+    from rtx.dist import StripGather, strip_config
 
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -34,9 +34,7 @@ def render(rank, world, port, out_dir):
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    y0, rows, _ = strip_rows(H, world, rank)
-    cfg = rtx.write_config(os.path.join(out_dir, "c%d.toml" % rank), W, H, spp=2,
-                           extra="stripY0 = %d\nstripRows = %d\n" % (y0, rows))
+    cfg = rtx.write_config(os.path.join(out_dir, "c%d.toml" % rank), W, H, spp=2, extra=strip_config(world, rank))
     rt = rtx.RayTracer(W, H, cfg).init()
     rt.set_delta_time(16.667)
     rt.set_stream(torch.cuda.current_stream(dev).cuda_stream)

@@ -180,6 +180,27 @@ def test_pathtrace_strip(rtx, oracle, tmp_path, default_scene, sky_tex):
     assert_gbuffers_equal(g, o, rows=slice(y0 * w, (y0 + rows) * w))
 
 
+def test_pathtrace_interleaved_strip(rtx, oracle, tmp_path, default_scene, sky_tex):
+    """Interleaved strips (stripCount / stripIndex, the multi-GPU load balance): the context
+    renders exactly its 16-row blocks of the full frame, deferred samples included (spp 2)."""
+    from rtx.dist import strip_blocks
+
+    s, tex = sky_tex
+    w, h, n, r = 128, 100, 3, 1
+    rt = make_rt(rtx, tmp_path, w, h, spp=2, extra="stripCount = %d\nstripIndex = %d\n" % (n, r))
+    ocam, rcam = terrain_camera(rtx, oracle, w, h)
+    rt.camera = rcam
+    rt.path_trace(1, detail=True)
+    rt.sync()
+    g = gpu_gbuffers(rt, w, h)
+    rt.cleanup()
+    o = oracle.pathtrace(default_scene["bvh"], w, h, frame_num=1, spp=2, cam=ocam, sky_out=s, tex=tex)
+    owned = np.concatenate([np.arange(y0 * w, (y0 + rows) * w) for y0, rows in strip_blocks(h, n, r)])
+    assert owned.size == 2 * 16 * w
+    assert_gbuffers_equal(g, o, rows=owned)
+    assert (g["rays"][np.setdiff1d(np.arange(w * h), owned)] == 0).all()  # nothing outside its blocks
+
+
 def test_pathtrace_1080p_bit_exact(rtx, oracle, tmp_path, default_scene, sky_tex):
     s, tex = sky_tex
     w, h = 1920, 1080

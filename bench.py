@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the per-stage and 1M-triangle side measurements")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="gloo: rehearse the multi-rank path with ranks sharing a GPU (not a measurement)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="serial frames (no post stream): denoise of frame f does not overlap the trace of f+1")
     return ap.parse_args()
@@ -109,10 +111,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":  # rehearsal of the N-rank path with ranks sharing GPUs
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     W, H, S = args.width, args.height, args.spp
     rows = sum(r for _, r in strip_blocks(H, world, rank))
@@ -138,6 +145,8 @@ def main():
         rt.build_bvh()
         rt.path_trace(f)
         if sg is not None:
+            if args.dist_backend == "gloo":
+                rt.sync()  # gloo copies through the host: the strip must be complete
             sg.gather()
         rt.denoise_post(f)
 

@@ -620,27 +620,27 @@ __global__ void k_auto_exposure(float* e, const uint32_t* hist, float area, floa
 // BicubicScale's source column / row of output pixel x (t1 of the 16-tap Catmull-Rom footprint)
 RT_DEV int scale_t1(int x, int Ws, int W) { return (int)floorf((float)x / Ws * (float)W - 0.5f); }
 
-// clamped reads of a W x H image staged in LDS: rows [Y0, Y0 + TH), columns [X0, X0 + TW)
-struct LdsImage {
-    const uint2* s;
-    int X0, Y0, TW, W, H;
-    RT_DEV uint2 at(int x, int y) const { return s[(clampi(y, 0, H - 1) - Y0) * TW + (clampi(x, 0, W - 1) - X0)]; }
-};
+
+// BicubicScale's per-axis part (postprocessing.cuh:785-802): the first tap t1 and the four
+// Catmull-Rom weights of screen coordinate x (Ws screen texels over W render texels)
+RT_DEV int bicubic_axis(int x, int Ws, int W, float w[4]) {
+    const float uv = (float)x / Ws;
+    const float UV = uv * (float)W;
+    const float fx0 = floorf(UV - 0.5f);
+    const float f = UV - (fx0 + 0.5f);
+    const float f2 = f * f;
+    const float f3v = f2 * f;
+    w[0] = f2 - 0.5f * (f3v + f);
+    w[1] = 1.5f * f3v - 2.5f * f2 + 1.0f;
+    w[3] = 0.5f * (f3v - f2);
+    w[2] = 1.0f - w[0] - w[1] - w[3];
+    return (int)fx0;
+}
 
 template <class Img>
 RT_DEV uint2 bicubic_scale_px(const Img& im, int W, int H, int x, int y, int Ws, int Hs) {
-    const F2 uv = {(float)x / Ws, (float)y / Hs};
-    const F2 UV = {uv.x * (float)W, uv.y * (float)H};
-    const float fx0 = floorf(UV.x - 0.5f), fy0 = floorf(UV.y - 0.5f);
-    const F2 f = {UV.x - (fx0 + 0.5f), UV.y - (fy0 + 0.5f)};
-    const F2 f2 = {f.x * f.x, f.y * f.y};
-    const F2 f3v = {f2.x * f.x, f2.y * f.y};
-    const F2 w0 = {f2.x - 0.5f * (f3v.x + f.x), f2.y - 0.5f * (f3v.y + f.y)};
-    const F2 w1 = {1.5f * f3v.x - 2.5f * f2.x + 1.0f, 1.5f * f3v.y - 2.5f * f2.y + 1.0f};
-    const F2 w3 = {0.5f * (f3v.x - f2.x), 0.5f * (f3v.y - f2.y)};
-    const F2 w2 = {1.0f - w0.x - w1.x - w3.x, 1.0f - w0.y - w1.y - w3.y};
-    const int t1x = (int)fx0, t1y = (int)fy0;
-    const float wx[4] = {w0.x, w1.x, w2.x, w3.x}, wy[4] = {w0.y, w1.y, w2.y, w3.y};
+    float wx[4], wy[4];
+    const int t1x = bicubic_axis(x, Ws, W, wx), t1y = bicubic_axis(y, Hs, H, wy);
     F3 o = f3(0.0f);
     float sw = 0.0f;
 #pragma unroll
@@ -842,11 +842,49 @@ __global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const u
         for (int i = threadIdx.x; i < TW * TH; i += 256) sIn[i] = render[(size_t)(iy0 + i / TW) * W + ix0 + i % TW];
         __syncthreads();
     }
-    const LdsImage li{sIn, ix0, iy0, TW, W, H};
-    const View2 gi{render, W, H};
-    for (int i = threadIdx.x; i < 18 * 18; i += 256) {
-        const int sx = clampi(X0 + i % 18, 0, Ws - 1), sy = clampi(Y0 + i / 18, 0, Hs - 1);
-        sS[i] = staged ? bicubic_scale_px(li, W, H, sx, sy, Ws, Hs) : bicubic_scale_px(gi, W, H, sx, sy, Ws, Hs);
+    if (staged) {
+        // the x weights and tap columns depend on the apron column only, the y ones on the row
+        // only: 36 axis evaluations instead of 2 per texel, same arithmetic (bicubic_axis)
+        __shared__ float sW[2][18][4];
+        __shared__ int sT[2][18][4];  // tap column within the tile / tap row offset (row * TW)
+        const int t = threadIdx.x;
+        if (t < 36) {
+            const int ax = t / 18, k = t % 18;
+            float w[4];
+            if (ax == 0) {
+                const int t1 = bicubic_axis(clampi(X0 + k, 0, Ws - 1), Ws, W, w);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sT[0][k][i] = clampi(t1 - 1 + i, 0, W - 1) - ix0;
+            } else {
+                const int t1 = bicubic_axis(clampi(Y0 + k, 0, Hs - 1), Hs, H, w);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) sT[1][k][j] = (clampi(t1 - 1 + j, 0, H - 1) - iy0) * TW;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sW[ax][k][i] = w[i];
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < 18 * 18; i += 256) {
+            const int cx = i % 18, ry = i / 18;
+            F3 o = f3(0.0f);
+            float sw = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {  // the loop order of bicubic_scale_px
+                    const float w = sW[0][cx][k] * sW[1][ry][j];
+                    sw += w;
+                    o = o + rgb_of(sIn[sT[1][ry][j] + sT[0][cx][k]]) * w;
+                }
+            o = o / sw;
+            sS[i] = pack_color(o, 0x3C00u);
+        }
+    } else {
+        const View2 gi{render, W, H};
+        for (int i = threadIdx.x; i < 18 * 18; i += 256) {
+            const int sx = clampi(X0 + i % 18, 0, Ws - 1), sy = clampi(Y0 + i / 18, 0, Hs - 1);
+            sS[i] = bicubic_scale_px(gi, W, H, sx, sy, Ws, Hs);
+        }
     }
     __syncthreads();
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);

@@ -158,6 +158,26 @@ int update_sky(rt_context* ctx) {
     return RT_OK;
 }
 
+// LocalizeSample(sunDir) (sampler / sky.cuh): u = cross(n, w), v = cross(n, u) with the
+// reference's fma-based DiffOfProducts cross, exactly as the device evaluates it
+float dop_host(float a, float b, float c, float d) {
+    const float cd = c * d;
+    const float err = fmaf(-c, d, cd);
+    const float dp = fmaf(a, b, -cd);
+    return dp + err;
+}
+void sun_frame(const float n[3], float t[3], float b[3]) {
+    float w[3] = {1.0f, 0.0f, 0.0f};
+    if (fabsf(n[0]) > 0.707f) { w[0] = 0.0f; w[1] = 1.0f; }
+    auto cross = [](const float* a, const float* c, float* r) {
+        r[0] = dop_host(a[1], c[2], a[2], c[1]);
+        r[1] = dop_host(a[2], c[0], a[0], c[2]);
+        r[2] = dop_host(a[0], c[1], a[1], c[0]);
+    };
+    cross(n, w, t);
+    cross(n, t, b);
+}
+
 HistCamera hist_of(const HostCamera& c) {
     HistCamera h;
     memcpy(h.pos, c.pos, 12);
@@ -402,6 +422,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.sunTree = fr.sunTree;
     memcpy(p.sunDir, fr.sunDir, 12);
     p.cosThetaMax = fr.cosThetaMax;
+    sun_frame(fr.sunDir, p.sunT, p.sunB);
     p.colorOut = fr.color;
     p.normalOut = fr.normal;
     p.albedoOut = fr.albedo;

@@ -124,6 +124,7 @@ struct PathTraceParams {
     const float* skyTree;       // [kSkyTreeNodes] (SkyGenParams::skyTree)
     const float* sunTree;       // [kSunTreeNodes]
     float sunDir[3];
+    float sunT[3], sunB[3];     // LocalizeSample(sunDir) frame (sky.cuh:64-87), evaluated once on the host
     float cosThetaMax;
     uint2* colorOut;            // [W*H] half3 demodulated colour + ushort material mask
     uint2* normalOut;           // [W*H] half4

@@ -113,15 +113,19 @@ RT_DEV void localize_sample(F3 n, F3& u, F3& v) {
     v = cross(n, u);
 }
 
-RT_DEV F3 equal_area_map_cone(F3 sunDir, float u, float v, float cosThetaMax) {
+RT_DEV F3 equal_area_map_cone(F3 sunDir, F3 t, F3 b, float u, float v, float cosThetaMax) {
     const float cosTheta = (1.0f - u) + u * cosThetaMax;
     const float sinTheta = __builtin_sqrtf(1.0f - cosTheta * cosTheta);
     const float phi = v * kTwoPi;
-    F3 t, b;
-    localize_sample(sunDir, t, b);
     const F3 c = f3(rt_cosf(phi) * sinTheta, cosTheta, rt_sinf(phi) * sinTheta);
     return f3(inner3(t.x, c.x, sunDir.x, c.y, b.x, c.z), inner3(t.y, c.x, sunDir.y, c.y, b.y, c.z),
               inner3(t.z, c.x, sunDir.z, c.y, b.z, c.z));
+}
+
+RT_DEV F3 equal_area_map_cone(F3 sunDir, float u, float v, float cosThetaMax) {
+    F3 t, b;
+    localize_sample(sunDir, t, b);
+    return equal_area_map_cone(sunDir, t, b, u, v, cosThetaMax);
 }
 
 // SampleBicubicSmoothStep over a float4 env buffer.  sky: RepeatX/ClampY on 512x256.
@@ -173,14 +177,12 @@ RT_DEV F3 env_light(const PathTraceParams& P, F3 sunDir, F3 rd) {
         const float w = clampf((rd.y + 0.4f) * (1.0f / 0.5f));
         color = f3(0.0f) + (mist + (w * w * (3.0f - 2.0f * w)) * (sky - mist));
     }
-    // EqualAreaMapCone inverse (sky.cuh:64-87)
-    F3 t, b;
-    localize_sample(sunDir, t, b);
-    const F3 c = f3(inner3(t.x, rd.x, t.y, rd.y, t.z, rd.z), inner3(sunDir.x, rd.x, sunDir.y, rd.y, sunDir.z, rd.z),
-                    inner3(b.x, rd.x, b.y, rd.y, b.z, rd.z));
+    // EqualAreaMapCone inverse (sky.cuh:64-87); the sun frame (t, b) = LocalizeSample(sunDir) is
+    // per frame (P.sunT / P.sunB), and c.x is needed only inside the sun cone
     const float cosMax = P.cosThetaMax;
-    const float cosTheta = c.y;
+    const float cosTheta = inner3(sunDir.x, rd.x, sunDir.y, rd.y, sunDir.z, rd.z);
     if (cosTheta < cosMax) return color;
+    const F3 c = f3(inner3(P.sunT[0], rd.x, P.sunT[1], rd.y, P.sunT[2], rd.z), cosTheta, 0.0f);
     const float u = (1.0f - cosTheta) / (1.0f - cosMax);
     const float sinTheta = __builtin_sqrtf(1.0f - cosTheta * cosTheta);
     if (sinTheta < 1e-5f || (c.x / sinTheta) < -1.0f || (c.x / sinTheta) > 1.0f) return color;
@@ -235,7 +237,8 @@ RT_DEV void sample_light(const PathTraceParams& P, F3 sunDir, F3& dir, float& pd
         p = p * kSunSize / (kTwoPi * (1.0f - P.cosThetaMax));
         const float u = ((float)(idx % kSunW) + 0.5f) / kSunW;
         const float v = ((float)(idx / kSunW) + 0.5f) / kSunH;
-        dir = equal_area_map_cone(sunDir, u, v, P.cosThetaMax);
+        dir = equal_area_map_cone(sunDir, f3(P.sunT[0], P.sunT[1], P.sunT[2]), f3(P.sunB[0], P.sunB[1], P.sunB[2]), u,
+                                  v, P.cosThetaMax);
         pdf = p * 1.0f;
     }
     lightIdx = kEnvLightId;

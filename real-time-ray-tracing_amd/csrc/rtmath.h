@@ -368,6 +368,16 @@ RT_HD float rt_acosf(float x) {
 
 // powf with the C99 special cases that matter on the path (x >= 0 in practice)
 RT_HD float rt_powf(float xf, float yf) {
+    // common case first (textures' ^2.2, the tone mapper's gamma): x positive and finite, y not
+    // NaN.  None of the special cases below applies to it, so this is the same computation as
+    // the tail of the general path, without its double-precision classification.
+    if (xf > 0.0f && xf < rtm::bits_to_float(0x7F800000u) && yf == yf) {
+        float lh, ll;
+        rtm::log2_pair(xf, lh, ll);
+        const float th = yf * lh;
+        const float tl = rtm::f_fma(yf, lh, -th) + yf * ll;
+        return rtm::exp2_pair(th, tl);
+    }
     double x = (double)xf, y = (double)yf;
     if (y == 0.0) return 1.0f;
     if (x == 1.0) return 1.0f;

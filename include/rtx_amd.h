@@ -194,7 +194,9 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr);
 int rt_get_ray_count(rt_context* ctx, uint64_t* rays, int reset);
 
 /* Enqueue every later stage on `stream` (a hipStream_t, e.g. the caller's framework stream so
- * its collectives order with the renderer); NULL restores the context's own stream. */
+ * its collectives order with the renderer).  NULL is the device's null stream (a framework's
+ * default stream, e.g. torch's, is that stream); RT_OWN_STREAM restores the context's own. */
+#define RT_OWN_STREAM ((void*)(intptr_t)-1)
 int rt_set_stream(rt_context* ctx, void* stream);
 
 /* Frame pipelining (no reference counterpart; the reference draws frames strictly one after

@@ -631,7 +631,7 @@ int rt_set_stream(rt_context* ctx, void* stream) {
     if (!ctx->inited) { ctx->err = "rt_set_stream before rt_init"; return RT_ERR_STATE; }
     int rc = sync_streams(ctx);
     if (rc != RT_OK) return rc;
-    ctx->stream = stream ? (hipStream_t)stream : ctx->ownStream;
+    ctx->stream = stream == RT_OWN_STREAM ? ctx->ownStream : (hipStream_t)stream;  // NULL: the null stream
     return RT_OK;
 }
 

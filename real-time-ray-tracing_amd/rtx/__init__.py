@@ -244,7 +244,10 @@ class RayTracer:
         self._check(self.lib.rt_denoise_post(self.h, frame_num, 1 if hdr else 0), "rt_denoise_post")
 
     def set_stream(self, stream_ptr: int | None):
-        self._check(self.lib.rt_set_stream(self.h, stream_ptr), "rt_set_stream")
+        """Enqueue on a hipStream_t handle (0: the null stream, torch's default stream); None
+        restores the context's own stream (RT_OWN_STREAM)."""
+        ptr = C.c_void_p(-1) if stream_ptr is None else C.c_void_p(stream_ptr)
+        self._check(self.lib.rt_set_stream(self.h, ptr), "rt_set_stream")
 
     def set_post_stream(self, stream_ptr: int | None):
         """Run denoise + post on a second stream and alternate two G-buffer sets (frame pipelining)."""

@@ -21,7 +21,7 @@ def free_port():
     return p
 
 
-def render(rank, world, port, out_dir):
+def render(rank, world, port, out_dir, pipelined):
     import torch
     import torch.distributed as dist
 
@@ -38,9 +38,11 @@ def render(rank, world, port, out_dir):
     rt = rtx.RayTracer(W, H, cfg).init()
     rt.set_delta_time(16.667)
     rt.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    post = torch.cuda.Stream(dev)
-    rt.set_post_stream(post.cuda_stream)
-    sg = StripGather(W, H, world, rank, dev, rt, sets=rtx.GBUFFER_SETS) if world > 1 else None
+    if pipelined:
+        post = torch.cuda.Stream(dev)
+        rt.set_post_stream(post.cuda_stream)
+    sets = rtx.GBUFFER_SETS if pipelined else 1
+    sg = StripGather(W, H, world, rank, dev, rt, sets=sets) if world > 1 else None
     cam0 = rt.camera
     for f in range(1, FRAMES + 1):
         c = rt.camera
@@ -60,11 +62,14 @@ def render(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
-def test_two_ranks_one_gpu_match_single_rank(tmp_path):
+@pytest.mark.parametrize("pipelined", [True, False])
+def test_two_ranks_one_gpu_match_single_rank(tmp_path, pipelined):
+    """The renderer runs on torch's default stream (the null stream, handle 0) like the gathers:
+    serial frames exercise exactly that ordering."""
     import torch.multiprocessing as mp
 
-    mp.start_processes(render, args=(1, 0, str(tmp_path)), nprocs=1, start_method="spawn")
-    mp.start_processes(render, args=(2, free_port(), str(tmp_path)), nprocs=2, start_method="spawn")
+    mp.start_processes(render, args=(1, 0, str(tmp_path), pipelined), nprocs=1, start_method="spawn")
+    mp.start_processes(render, args=(2, free_port(), str(tmp_path), pipelined), nprocs=2, start_method="spawn")
     ref = np.load(tmp_path / "r0_of1.npz")
     for r in range(2):
         got = np.load(tmp_path / ("r%d_of2.npz" % r))

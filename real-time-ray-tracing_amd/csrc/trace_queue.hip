@@ -119,7 +119,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
             f.resLo += k < avail ? k : avail;
         }
         if (__ballot(active) == 0ull) break;
-        if (active) {
+        if (trav_lane_steps(active, s)) {
             const bool done = trav_step(sc, r, s, stkA + tid, stkT + tid, kTraceBlock) || s.iters >= 1024u;
             if (done) {
                 P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);

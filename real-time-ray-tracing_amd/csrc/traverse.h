@@ -288,6 +288,19 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint3
     return false;
 }
 
+// Wave-level leaf batching for the lanes of one wave that each run their own traversal: a lane
+// whose next step is a BLAS leaf (a triangle test, ~1 iteration in 20) waits until enough lanes
+// are at leaves, so the triangle-test code runs for many lanes at once instead of in nearly
+// every trip of the loop.  Each ray's own sequence of steps is unchanged (a waiting lane only
+// pauses), hence its hits, counters and 1024-step cap.  Returns whether this lane steps now.
+RT_DEV bool trav_lane_steps(bool active, const TravState& s) {
+    const bool atLeaf = active && s.cLeaf && s.cBlas;
+    const unsigned long long lm = __ballot(atLeaf), am = __ballot(active);
+    const int nl = __popcll(lm), na = __popcll(am);
+    const bool doLeaf = nl >= 16 || nl * 4 >= na;
+    return active && (!atLeaf || doLeaf);
+}
+
 // hit finalisation (traverse.h:161-174, traverse.cuh:192-217), once for the closest hit
 RT_DEV void finalize_hit(const SceneView& sc, F3 org, F3 dir, float t, int hitIdx, float hitU, float hitV,
                          float hitErrT, HitInfo& out) {

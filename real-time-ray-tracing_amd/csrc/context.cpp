@@ -678,7 +678,7 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
         case RT_ARR_COLOR64: src = ctx->fr.c64; break;
         case RT_ARR_RGBA8: src = ctx->fr.rgba; break;
         case RT_ARR_PT_STATS: src = ctx->fr.ptStats; break;
-        case RT_ARR_PT_QUEUE: src = ctx->fr.ws.counters; break;
+        case RT_ARR_PT_QUEUE: src = ctx->fr.lastCounters ? ctx->fr.lastCounters : ctx->fr.ws.counters; break;
         case RT_ARR_PT_Q3_ORIGINS: src = ctx->fr.ws.q3.rayO; break;
         case RT_ARR_PT_Q3_DIRS: src = ctx->fr.ws.q3.rayD; break;
         case RT_ARR_PT_Q4_ORIGINS: src = ctx->fr.ws.q4.rayO; break;

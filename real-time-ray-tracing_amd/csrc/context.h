@@ -86,7 +86,8 @@ struct FrameResources {
     float4* camHit0Rec[kGbSets] = {};
     float* camHit0Err[kGbSets] = {};
     uint32_t* camSurface[kGbSets] = {};
-    uint32_t* camCount[kGbSets] = {};
+    uint32_t* camCount[kGbSets] = {};  // counter block per slot (PtWorkspace::counters)
+    uint32_t* lastCounters = nullptr;  // the block of the last path trace (RT_ARR_PT_QUEUE)
     bool camInFlight[kGbSets] = {};
     HistCamera hist{};
     bool histValid = false;

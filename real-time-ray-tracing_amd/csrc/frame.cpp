@@ -302,12 +302,11 @@ int rt_frame_init(rt_context* ctx) {
         ALLOC(ws.pathL, cap * 16);
         ALLOC(ws.pending, (size_t)ctx->renderW * ctx->stripRows * 4);
         ALLOC(ws.surface, (size_t)ctx->renderW * ctx->stripRows * 4);
-        ALLOC(fr.camCount[0], 64);
+        ALLOC(fr.camCount[0], kWsCounterWords * 4);
         fr.camHit0Rec[0] = ws.hit0Rec;
         fr.camHit0Err[0] = ws.hit0Err;
         fr.camSurface[0] = ws.surface;
-        ws.camCount = fr.camCount[0];
-        ALLOC(ws.counters, kWsCounterWords * 4);
+        ws.counters = fr.camCount[0];
         ws.fetch = ws.counters + 64;
         int dev = 0, cus = 0;
         HIP_TRY(ctx, hipGetDevice(&dev));
@@ -436,7 +435,9 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.ws.hit0Rec = fr.camHit0Rec[g];
     p.ws.hit0Err = fr.camHit0Err[g];
     p.ws.surface = fr.camSurface[g];
-    p.ws.camCount = fr.camCount[g];
+    p.ws.counters = fr.camCount[g];
+    p.ws.fetch = p.ws.counters + 64;
+    fr.lastCounters = p.ws.counters;
     {  // material table (init.cu:215-251): only mirror / glass ids make steps 1-2 trace
         const int m = ctx->materialOverride;
         p.ws.glossy = m >= 0 && (m == 1 || m == 5 || m >= 10);
@@ -658,7 +659,7 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
         ALLOC(fr.camHit0Rec[k], cap * 16);
         ALLOC(fr.camHit0Err[k], cap * 4);
         ALLOC(fr.camSurface[k], strip * 4);
-        ALLOC(fr.camCount[k], 64);
+        ALLOC(fr.camCount[k], kWsCounterWords * 4);
     }
     {  // second LBVH set: frame f+1's build and camera rays beside frame f's traces
         const size_t NP = ctx->mesh.triCountPadded, B = ctx->B;

@@ -83,8 +83,10 @@ struct PtWorkspace {
     float4* pathL;              // [rows*W*spp] per-sample radiance of pixels resolved late
     uint32_t* pending;          // [rows*W] pixel (strip-local) | first deferred sample << 26
     uint32_t* surface;          // [rows*W] strip-local pixels with a sample that hit geometry
-    uint32_t* camCount;         // [16] k_pt_camera's append counter of `surface` (copied to counters[kCntSurface])
-    uint32_t* counters;         // [kCntSlots]
+    // counters + fetch: one block per camera-output slot, zeroed on the camera's stream right
+    // before k_pt_camera appends to counters[kCntSurface], so the shade..resolve kernels start
+    // with no memset or copy of their own
+    uint32_t* counters;         // [kWsCounterWords]: kCntSlots counters, then `fetch`
     uint32_t* fetch;            // [2][8 parts x 16]: k_trace_queue fetch counters, 64 B apart
     uint32_t cap;               // entries per queue (= rows * W * spp)
     uint32_t persistBlocks;     // grid of the persistent queue kernels

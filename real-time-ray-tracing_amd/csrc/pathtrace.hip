@@ -518,7 +518,7 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
         if (P.raysOut) atomicAdd(&P.raysOut[p], rays);
         if (P.statsOut) atomicAdd(&P.statsOut[p].x, rays);
     }
-    const uint32_t slot = wave_append(sw == 0 && surface, P.ws.camCount);
+    const uint32_t slot = wave_append(sw == 0 && surface, &P.ws.counters[kCntSurface]);
     if (sw == 0 && active) {
         if (surface) {
             P.ws.surface[slot] = pl;
@@ -801,7 +801,7 @@ extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t
     if (p->spp < 1 || p->spp > 64 || p->ws.persistBlocks < 1) return hipErrorInvalidValue;
     if ((size_t)p->rows * p->width >= (1u << 26) || (size_t)p->rows * p->width * p->spp > p->ws.cap)
         return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(p->ws.camCount, 0, 16 * sizeof(uint32_t), stream);
+    hipError_t e = hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
     if (e == hipSuccess && marks) e = hipEventRecord(marks[0], stream);
     if (e != hipSuccess) return e;
     const int nSW = cam_sample_waves(p->spp);
@@ -816,11 +816,7 @@ extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t
 // issues the previous frame's denoise and gates the next frame's camera rays there (frame.cpp).
 extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
                                          const PtLaunchHook* hook) {
-    hipError_t e = hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(p->ws.counters + kCntSurface, p->ws.camCount, sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                           stream);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;  // the counters were zeroed before the camera kernel (rtk_launch_pt_camera)
     int k = 2;  // marks[2] = end of the shade kernel
     auto mark = [&]() {
         if (hook && hook->fn) {

@@ -218,6 +218,72 @@ RT_HD double atan2d(double y, double x) {
     return yneg ? -r : r;
 }
 
+// ---- float-result cores (the kernels' hot trig): double internals, short polynomials
+//
+// sin/cos for |x| <= 1e5: the same Cody-Waite reduction as sincosd, then minimax kernels on
+// |r| <= pi/4 with relative error < 2^-37 (the sin/cos kernels of musl / FreeBSD
+// k_sinf.c / k_cosf.c, coefficients in hex-float form), so the float result is the correctly
+// rounded one except within ~2^-13 ulp of a rounding boundary.
+RT_HD void sincosf_core(double x, double& s, double& c) {
+    const double k = d_round(x * 0.63661977236758134308);
+    const double r = (x - k * 1.57079632673412561417e+00) - k * 6.07710050650619224932e-11;
+    const double z = r * r, w = z * z;
+    const double S1 = -0x15555554cbac77.0p-55, S2 = 0x111110896efbb2.0p-59, S3 = -0x1a00f9e2cae774.0p-65,
+                 S4 = 0x16cd878c3b46a7.0p-71;
+    const double C0 = -0x1ffffffd0c5e81.0p-54, C1 = 0x155553e1053a42.0p-57, C2 = -0x16c087e80f1e27.0p-62,
+                 C3 = 0x199342e0ee5069.0p-68;
+    const double zr = z * r;
+    const double sr = (r + zr * (S1 + z * S2)) + zr * w * (S3 + z * S4);
+    const double cr = ((1.0 + z * C0) + w * C1) + (w * z) * (C2 + z * C3);
+    const int q = (int)((int64_t)k & 3);
+    if (q == 0) { s = sr; c = cr; }
+    else if (q == 1) { s = cr; c = -sr; }
+    else if (q == 2) { s = -sr; c = -cr; }
+    else { s = -cr; c = sr; }
+}
+
+// atan(num / den) for 0 <= num, den finite, not both 0: one double division.  The ratio
+// q = num/den is split as atan(c) + atan((num - c den) / (den + c num)) with c = i/8 nearest to
+// min(q, 1/q) (i from a float estimate; any i keeps the identity exact), so |t| <= 1/16 + eps
+// and five odd terms leave < 1e-15.
+RT_HD double atan_ratio(double num, double den) {
+    const bool swap = num > den;
+    const double a = swap ? den : num, b = swap ? num : den;  // a <= b, a / b in [0, 1]
+    const float qf = (float)a / (float)b;
+    const int i = (int)(qf * 8.0f + 0.5f);
+    const double c = (double)i * 0.125;
+    const double t = (a - c * b) / (b + c * a);
+    const double t2 = t * t;
+    double p = 1.0 / 9.0;
+    p = d_mad(p, t2, -1.0 / 7.0);
+    p = d_mad(p, t2, 1.0 / 5.0);
+    p = d_mad(p, t2, -1.0 / 3.0);
+    const double at = d_mad(t * t2, p, t);
+    // atan(i / 8), i = 0..8
+    const double kAtan8[9] = {0.0, 0.12435499454676144, 0.24497866312686414, 0.35877067027057225, 0.4636476090008061, 0.5585993153435624, 0.6435011087932844, 0.7188299996216245, 0.7853981633974483};
+    const double r = kAtan8[i] + at;
+    return swap ? 1.57079632679489661923 - r : r;
+}
+
+RT_HD double atan2f_core(double y, double x) {
+    if (d_isnan(x) || d_isnan(y)) return d_nan();
+    const double pi = 3.14159265358979323846;
+    const bool yneg = (double_to_bits(y) >> 63) != 0;
+    const bool xneg = (double_to_bits(x) >> 63) != 0;
+    const double ay = d_abs(y), ax = d_abs(x);
+    double r;
+    if (ay == 0.0) r = xneg ? pi : 0.0;
+    else if (ax == 0.0) r = pi * 0.5;
+    else if (ax == d_inf() && ay == d_inf()) r = xneg ? pi * 0.75 : pi * 0.25;
+    else if (ax == d_inf()) r = xneg ? pi : 0.0;
+    else if (ay == d_inf()) r = pi * 0.5;
+    else {
+        const double a = atan_ratio(ay, ax);
+        r = xneg ? pi - a : a;
+    }
+    return yneg ? -r : r;
+}
+
 }  // namespace rtm
 
 // ------------------------------------------------------------------ float API
@@ -347,23 +413,33 @@ RT_HD float rt_logf(float x) {
     return ph + (rtm::f_fma(h, Nh, -ph) + rtm::f_fma(h, Nl, l * Nh));
 }
 RT_HD float rt_log10f(float x) { return (float)(rtm::logd((double)x) * 0.43429448190325182765); }
-RT_HD float rt_sinf(float x) { double s, c; rtm::sincosd((double)x, s, c); return (float)s; }
-RT_HD float rt_cosf(float x) { double s, c; rtm::sincosd((double)x, s, c); return (float)c; }
-RT_HD void rt_sincosf(float x, float* s, float* c) {
-    double sd, cd; rtm::sincosd((double)x, sd, cd); *s = (float)sd; *c = (float)cd;
+RT_HD void rt_sincos_d(float x, double& s, double& c) {
+    if (rtm::d_abs((double)x) <= 1e5) rtm::sincosf_core((double)x, s, c);  // NaN and inf fail the test
+    else rtm::sincosd((double)x, s, c);
 }
-RT_HD float rt_tanf(float x) { double s, c; rtm::sincosd((double)x, s, c); return (float)(s / c); }
-RT_HD float rt_atanf(float x) { return (float)rtm::atand((double)x); }
-RT_HD float rt_atan2f(float y, float x) { return (float)rtm::atan2d((double)y, (double)x); }
+RT_HD float rt_sinf(float x) { double s, c; rt_sincos_d(x, s, c); return (float)s; }
+RT_HD float rt_cosf(float x) { double s, c; rt_sincos_d(x, s, c); return (float)c; }
+RT_HD void rt_sincosf(float x, float* s, float* c) {
+    double sd, cd; rt_sincos_d(x, sd, cd); *s = (float)sd; *c = (float)cd;
+}
+RT_HD float rt_tanf(float x) { double s, c; rt_sincos_d(x, s, c); return (float)(s / c); }
+RT_HD float rt_atanf(float x) {
+    if (x != x) return x;
+    const double a = (double)x;
+    if (rtm::d_abs(a) == rtm::d_inf()) return a > 0 ? 1.57079632679489661923f : -1.57079632679489661923f;
+    const double r = a == 0.0 ? 0.0 : rtm::atan_ratio(rtm::d_abs(a), 1.0);
+    return (float)(a < 0.0 ? -r : (a == 0.0 ? a : r));
+}
+RT_HD float rt_atan2f(float y, float x) { return (float)rtm::atan2f_core((double)y, (double)x); }
 RT_HD float rt_asinf(float x) {
     double d = (double)x;
     if (!(d >= -1.0 && d <= 1.0)) return (float)rtm::d_nan();
-    return (float)rtm::atan2d(d, __builtin_sqrt((1.0 - d) * (1.0 + d)));
+    return (float)rtm::atan2f_core(d, __builtin_sqrt((1.0 - d) * (1.0 + d)));
 }
 RT_HD float rt_acosf(float x) {
     double d = (double)x;
     if (!(d >= -1.0 && d <= 1.0)) return (float)rtm::d_nan();
-    return (float)rtm::atan2d(__builtin_sqrt((1.0 - d) * (1.0 + d)), d);
+    return (float)rtm::atan2f_core(__builtin_sqrt((1.0 - d) * (1.0 + d)), d);
 }
 
 // powf with the C99 special cases that matter on the path (x >= 0 in practice)

@@ -40,8 +40,11 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
  * resource, uploads blue-noise/sky tables, runs the frame-1 smooth normals. */
 int rt_init(rt_context* ctx);
 
-/* RayTracer::draw, kernel.cu:259-398: one synchronous frame.  rgba8_out (screen W*H*4)
- * and hdr_out (render W*H*4 floats, pre-tone-map HDR) may each be NULL. */
+/* RayTracer::draw, kernel.cu:259-398 (with UpdateFrame, kernel.cu:61-137): one synchronous
+ * frame.  rgba8_out (screen W*H*4) and hdr_out (render W*H*4 floats, pre-tone-map HDR) may
+ * each be NULL.  With [optimziation] useDynamicResolution the render size follows the frame
+ * time from the second frame on (rt_get_info's renderWidth/Height); size hdr_out for
+ * maxWidth x maxHeight. */
 int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out);
 
 /* RayTracer::cleanup + ~RayTracer, init.cu:601-663, kernel.cuh:443-446 */

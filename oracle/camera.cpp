@@ -154,3 +154,23 @@ extern "C" float orc_rtmath(int fn, float x, float y) {
         default: return 0.0f;
     }
 }
+
+// UpdateFrame's dynamic resolution (kernel.cu:77-100), restated: outside the targetFps +-2 band
+// the width is scaled (int *= float) by sqrt(target frame time / dt); it is then snapped to the
+// nearest multiple of 16 (ties of 8 round up), clamped by clampi to [minW, maxW], and the height
+// is (w / 16) * 9.
+extern "C" void orc_dynamic_resolution(int w, float dt, float targetFps, int minW, int maxW, int maxH, int* outW,
+                                       int* outH) {
+    const float high = 1000.0f / (targetFps - 2), low = 1000.0f / (targetFps + 2);
+    if (high < dt || low > dt) {
+        float ratio = (1000.0f / targetFps) / dt;
+        ratio = sqrtf(ratio);
+        w = (int)((float)w * ratio);
+    }
+    const int rem = w % 16;
+    w = rem < 8 ? w - rem : w + (16 - rem);
+    w = w < minW ? minW : (w > maxW ? maxW : w);
+    const int h = (w / 16) * 9;
+    *outW = w;
+    *outH = h > maxH ? maxH : h;
+}

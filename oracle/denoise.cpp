@@ -119,6 +119,7 @@ T warp_tree_sum(const T* v) {
 
 struct Ctx {
     int W, H, frameNum;
+    int hW, hH;  // historyDim (kernel.cu:266): size the accumulation / history colour were written at
     const rt_params* prm;
     const uint16_t *normal, *albedo, *depth, *motion;
     Img nrm() const { return Img{W, H, normal, 4}; }
@@ -134,7 +135,7 @@ void store_color(uint16_t* dst, size_t p, F3 c, uint16_t mask) {
 
 void temporal_filter(const Ctx& c, const uint16_t* in, uint16_t* out, const uint16_t* accum) {
     const rt_denoising_params& dp = c.prm->denoise;
-    const Img col{c.W, c.H, in, 4}, nrm = c.nrm(), dep = c.dep(), acc{c.W, c.H, accum, 4};
+    const Img col{c.W, c.H, in, 4}, nrm = c.nrm(), dep = c.dep(), acc{c.hW, c.hH, accum, 4};
     memcpy(out, in, (size_t)c.W * c.H * 8);
     for (int y = 0; y < c.H; ++y)
         for (int x = 0; x < c.W; ++x) {
@@ -186,7 +187,7 @@ void temporal_filter(const Ctx& c, const uint16_t* in, uint16_t* out, const uint
             float lumaH = cHy.x;
             const float lumaMin = nMin.x, lumaMax = nMax.x, lumaC = ycocg(cV).x;
             float discard = 0.0f;
-            const int hx = (int)floorf(huv.x * (float)c.W), hy = (int)floorf(huv.y * (float)c.H);
+            const int hx = (int)floorf(huv.x * (float)c.hW), hy = (int)floorf(huv.y * (float)c.hH);
             for (int i = 0; i < 4; ++i) discard += (mV != acc.u16(hx + i % 2, hy + i / 2, 3)) ? 1.0f : 0.0f;
             discard /= 4.0f;
             cH = cH * (1.0f - discard) + filt * discard;
@@ -361,7 +362,7 @@ void apply_albedo(const Ctx& c, uint16_t* color) {
 }
 
 void temporal_filter2(const Ctx& c, const uint16_t* in, uint16_t* out, const uint16_t* hist) {
-    const Img col{c.W, c.H, in, 4}, hc{c.W, c.H, hist, 4};
+    const Img col{c.W, c.H, in, 4}, hc{c.hW, c.hH, hist, 4};
     memcpy(out, in, (size_t)c.W * c.H * 8);
     const float FLTMIN = 1.17549435e-38f, FLTMAX = 3.402823466e+38f;
     for (int y = 0; y < c.H; ++y)
@@ -396,7 +397,7 @@ void temporal_filter2(const Ctx& c, const uint16_t* in, uint16_t* out, const uin
             float lumaH = cHy.x;
             const float lumaMin = nMin.x, lumaMax = nMax.x, lumaC = ycocg(cV).x;
             float discard = 0.0f;
-            const int hx = (int)floorf(huv.x * (float)c.W), hy = (int)floorf(huv.y * (float)c.H);
+            const int hx = (int)floorf(huv.x * (float)c.hW), hy = (int)floorf(huv.y * (float)c.hH);
             for (int i = 0; i < 4; ++i) discard += (mV != (int)hc.u16(hx + i % 2, hy + i / 2, 3)) ? 1.0f : 0.0f;
             discard /= 4.0f;
             if (discard == 1.0f) continue;
@@ -767,7 +768,8 @@ extern "C" int orc_denoise_post(const OrcDrawIO* io) {
     const rt_params& prm = *io->params;
     const rt_render_pass_settings& ps = prm.pass;
     if (ps.enableToneMapping && (prm.post.toneMappingType < 0 || prm.post.toneMappingType > 3)) return -1;
-    Ctx c{W, H, io->frameNum, io->params, io->normal, io->albedo, io->depth, io->motion};
+    Ctx c{W, H, io->frameNum, io->histW ? (int)io->histW : W, io->histH ? (int)io->histH : H, io->params,
+          io->normal, io->albedo, io->depth, io->motion};
     OrcPostState& st = *io->state;
     std::vector<uint16_t> tmp(P * 4);
     uint16_t* cur = io->color;

@@ -177,7 +177,12 @@ typedef struct OrcDrawIO {
     int lensFlare;          // the host-side lens-flare predicate held (orc_lens_flare_setup)
     float sunPos[2];        // LensFlare's sun position (already centred and aspect-scaled)
     int sunUv[2];           // render texel of the sun (LensFlarePred's depth test)
+    uint32_t histW, histH;  // historyDim (kernel.cu:266): the previous frame's render size; 0: (W, H)
 } OrcDrawIO;
+
+// UpdateFrame's dynamic resolution (kernel.cu:77-100): the next render size from the current
+// width and the frame time (ms).  Height clamped to maxH as the renderer does.
+void orc_dynamic_resolution(int w, float dt, float targetFps, int minW, int maxW, int maxH, int* outW, int* outH);
 
 // UpdateFrame's sunPos / sunUv (kernel.cu:126-127) and PostProcessing's lens-flare predicate
 // (postprocessing.cu:88-94).  Returns 1 when the lens flare pass is launched.

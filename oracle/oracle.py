@@ -220,6 +220,9 @@ def _bind_frame_api(L):
     L.orc_lens_flare_setup.argtypes = [C.POINTER(CameraIn), C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p,
                                        C.c_void_p]
     L.orc_lens_flare_setup.restype = C.c_int
+    L.orc_dynamic_resolution.argtypes = [C.c_int, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int,
+                                         C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.orc_dynamic_resolution.restype = None
 
 
 def sky_tables() -> list:
@@ -352,7 +355,15 @@ class DrawIO(C.Structure):
                 ("motion", C.c_void_p), ("noise8", C.c_void_p), ("noise16", C.c_void_p), ("c4", C.c_void_p),
                 ("c16", C.c_void_p), ("c64", C.c_void_p), ("histogram", C.c_void_p), ("scaled", C.c_void_p),
                 ("rgba", C.c_void_p), ("state", C.c_void_p), ("bloom4", C.c_void_p), ("bloom16", C.c_void_p),
-                ("lensFlare", C.c_int), ("sunPos", C.c_float * 2), ("sunUv", C.c_int * 2)]
+                ("lensFlare", C.c_int), ("sunPos", C.c_float * 2), ("sunUv", C.c_int * 2),
+                ("histW", C.c_uint32), ("histH", C.c_uint32)]
+
+
+def dynamic_resolution(w: int, dt: float, target_fps: float, min_w: int, max_w: int, max_h: int):
+    """UpdateFrame's dynamic-resolution step (kernel.cu:77-100): (next width, next height)."""
+    ow, oh = C.c_int(), C.c_int()
+    lib().orc_dynamic_resolution(w, dt, target_fps, min_w, max_w, max_h, C.byref(ow), C.byref(oh))
+    return ow.value, oh.value
 
 
 class Denoiser:
@@ -360,6 +371,7 @@ class Denoiser:
 
     def __init__(self, W: int, H: int, Ws: int | None = None, Hs: int | None = None):
         self.W, self.H = W, H
+        self.hist_size = (W, H)  # render size the history buffers hold (historyDim)
         self.Ws, self.Hs = Ws or W, Hs or H
         P = W * H
         self.accum = np.zeros((P, 4), np.uint16)
@@ -370,10 +382,14 @@ class Denoiser:
         self.bn = bluenoise_tables()
 
     def draw(self, g: dict, frame_num: int, params=None, delta_time: float = 1000.0 / 60.0,
-             cam: CameraIn | None = None, sun_dir=None) -> dict:
-        """cam / sun_dir: the frame's camera and sun direction, needed only for the lens flare."""
+             cam: CameraIn | None = None, sun_dir=None, size: tuple[int, int] | None = None) -> dict:
+        """cam / sun_dir: the frame's camera and sun direction, needed only for the lens flare.
+        size: this frame's render size when dynamic resolution changed it (at most (W, H)); the
+        history buffers keep the layout of the size they were written at."""
         params = params if params is not None else default_params()
-        W, H, Ws, Hs = self.W, self.H, self.Ws, self.Hs
+        W, H = size or (self.W, self.H)
+        assert W * H <= self.W * self.H
+        Ws, Hs = self.Ws, self.Hs
         d = lambda n: (n + 3) // 4
         W4, H4 = d(W), d(H)
         W16, H16 = d(W4), d(H4)
@@ -401,7 +417,9 @@ class Denoiser:
                                                       su.ctypes.data)
             io.sunPos[:] = sp.tolist()
             io.sunUv[:] = su.tolist()
+        io.histW, io.histH = self.hist_size
         rc = lib().orc_denoise_post(C.byref(io))
+        self.hist_size = (W, H)
         out["lens_flare"] = int(io.lensFlare)
         out["sun_uv"] = (int(io.sunUv[0]), int(io.sunUv[1]))
         if rc < 0:

@@ -247,6 +247,9 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
         ctx->stripRows = (int)strip_row_count((uint32_t)ctx->renderH, (uint32_t)ctx->stripCount, (uint32_t)ctx->stripIndex);
     }
     if (ctx->stripRows < 0) ctx->stripRows = ctx->renderH - ctx->stripY0;
+    ctx->fullFrame = ctx->stripCount == 1 && ctx->stripY0 == 0 && ctx->stripRows == ctx->renderH;
+    ctx->histW = ctx->renderW;
+    ctx->histH = ctx->renderH;
     if (ctx->stripCount < 1 || ctx->stripY0 < 0 || ctx->stripRows < 1 || ctx->stripY0 + ctx->stripRows > ctx->renderH) {
         g_createError = "invalid strip rows";
         delete ctx;

@@ -113,12 +113,15 @@ struct FrameResources {
     uint2* renderColor = nullptr;  // buffer that currently holds RenderColorBuffer
     uint2* scaledColor = nullptr;  // buffer that currently holds ScaledColorBuffer
     double lastDrawTime = -1.0;    // wall clock of the previous rt_draw (s)
+    float drawDt = -1.0f;          // this rt_draw's frame time (ms), taken once by UpdateFrame
 };
 
 struct rt_context {
     // ---- settings (GlobalSettings, globalSettings.h:5-22) + extensions
     int screenW = 1920, screenH = 1080;
     int renderW = 1920, renderH = 1080;
+    int histW = 1920, histH = 1080;   // historyRenderWidth / Height (kernel.cu:83-84): previous frame's size
+    bool fullFrame = true;            // no strip split: dynamic resolution may resize the frame
     bool useDynamicResolution = true;
     float targetFps = 60.0f;
     int maxWidth = 3840, maxHeight = 2160, minWidth = 640, minHeight = 480;

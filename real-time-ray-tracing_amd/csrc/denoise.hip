@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uin
 
 RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, int y) {
     const int W = (int)P.W, H = (int)P.H;
-    const View2 col{in, W, H}, nrm{P.normal, W, H}, acc{P.accum, W, H};
+    const View2 col{in, W, H}, nrm{P.normal, W, H}, acc{P.accum, (int)P.histW, (int)P.histH};
     const View1 dep{P.depth, W, H};
     const size_t p = (size_t)y * W + x;
     const uint2 c0 = in[p];
@@ -229,7 +229,7 @@ RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, 
             cH = ycocg_inv(cHy);
             const float lumaMin = nMin.x, lumaMax = nMax.x, lumaC = ycocg(cV).x;
             float discard = 0.0f;
-            const int hx = (int)floorf(huv.x * (float)W), hy = (int)floorf(huv.y * (float)H);
+            const int hx = (int)floorf(huv.x * (float)acc.W), hy = (int)floorf(huv.y * (float)acc.H);
 #pragma unroll
             for (int i = 0; i < 4; ++i) discard += (mV != mask_of(acc.at(hx + i % 2, hy + i / 2))) ? 1.0f : 0.0f;
             discard /= 4.0f;
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256) void k_temporal2(DenoisePostParams P, const ui
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= W || y >= H) return;
     const size_t p = (size_t)y * W + x;
-    const View2 col{in, W, H}, hc{P.histColor, W, H};
+    const View2 col{in, W, H}, hc{P.histColor, (int)P.histW, (int)P.histH};
     const uint2 c0 = in[p];
     out[p] = c0;
     const F3 cV = ycocg_inv(ycocg(rgb_of(c0)));
@@ -496,7 +496,7 @@ __global__ __launch_bounds__(256) void k_temporal2(DenoisePostParams P, const ui
     cH = ycocg_inv(cHy);
     const float lumaMin = nMin.x, lumaMax = nMax.x, lumaC = ycocg(cV).x;
     float discard = 0.0f;
-    const int hx = (int)floorf(huv.x * (float)W), hy = (int)floorf(huv.y * (float)H);
+    const int hx = (int)floorf(huv.x * (float)hc.W), hy = (int)floorf(huv.y * (float)hc.H);
 #pragma unroll
     for (int i = 0; i < 4; ++i) discard += (mV != (int)mask_of(hc.at(hx + i % 2, hy + i / 2))) ? 1.0f : 0.0f;
     discard /= 4.0f;

@@ -245,6 +245,44 @@ int sync_streams(rt_context* ctx) {
     return RT_OK;
 }
 
+// UpdateFrame's timer (kernel.cu:67-71): the frame time rt_draw already took, the fixed one
+// (rt_set_delta_time) or the wall clock since the previous call.  The 75-fps limiter's busy wait
+// (timer.h) is frame pacing for a window and is not reproduced.
+float frame_delta(rt_context* ctx) {
+    FrameResources& fr = ctx->fr;
+    if (fr.drawDt >= 0.0f) {
+        const float d = fr.drawDt;
+        fr.drawDt = -1.0f;
+        return d;
+    }
+    if (ctx->deltaMs > 0.0f) return ctx->deltaMs;
+    const double now = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    const float dt = fr.lastDrawTime < 0 ? 1000.0f / 60.0f : (float)((now - fr.lastDrawTime) * 1000.0);
+    fr.lastDrawTime = now;
+    return dt;
+}
+
+// UpdateFrame's dynamic resolution (kernel.cu:77-100): outside the targetFps +-2 band the width
+// scales by sqrt(target / frame time), snaps to a multiple of 16, clamps to [minWidth, maxWidth]
+// and the height follows at 16:9.  Every render-size buffer was allocated at the initial (max)
+// size; a height past maxHeight (a config whose max is not 16:9) is clamped to it so it fits.
+void update_dynamic_resolution(rt_context* ctx, float dt) {
+    if (!(dt > 0.0f)) return;
+    const float hi = 1000.0f / (ctx->targetFps - 2), lo = 1000.0f / (ctx->targetFps + 2);
+    int w = ctx->renderW;
+    if (hi < dt || lo > dt) {
+        const float ratio = sqrtf((1000.0f / ctx->targetFps) / dt);
+        w = (int)((float)w * ratio);
+    }
+    w = w + ((w % 16 < 8) ? (-w % 16) : (16 - w % 16));
+    w = w < ctx->minWidth ? ctx->minWidth : w > ctx->maxWidth ? ctx->maxWidth : w;
+    int h = (w / 16) * 9;
+    if (h > ctx->maxHeight) h = ctx->maxHeight;
+    ctx->renderW = w;
+    ctx->renderH = h;
+    ctx->stripRows = h;
+}
+
 int rt_frame_init(rt_context* ctx) {
     FrameResources& fr = ctx->fr;
     std::string err;
@@ -511,13 +549,9 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.Ws = (uint32_t)ctx->screenW;
     p.Hs = (uint32_t)ctx->screenH;
     p.frameNum = frame_num;
-    float dt = ctx->deltaMs;
-    if (dt <= 0.0f) {  // wall clock between draws (UpdateFrame's timer, kernel.cu:67-71)
-        const double now = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-        dt = fr.lastDrawTime < 0 ? 1000.0f / 60.0f : (float)((now - fr.lastDrawTime) * 1000.0);
-        fr.lastDrawTime = now;
-    }
-    p.deltaTime = dt;
+    p.histW = (uint32_t)ctx->histW;
+    p.histH = (uint32_t)ctx->histH;
+    p.deltaTime = frame_delta(ctx);
     p.temporal = ps.enableTemporalDenoising;
     p.localSpatial = ps.enableLocalSpatialFilter;
     p.visualize = ps.enableNoiseLevelVisualize;
@@ -607,6 +641,8 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
         fr.scaledColor = p.finalScaled;
     }
     if (p.temporal2) std::swap(fr.histColor, fr.histColorAlt);
+    ctx->histW = ctx->renderW;  // the history buffers now hold this frame's size
+    ctx->histH = ctx->renderH;
     return RT_OK;
 }
 
@@ -616,6 +652,10 @@ int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
     if (!ctx->inited) { ctx->err = "rt_draw before rt_init"; return RT_ERR_STATE; }
     const int frame = ctx->nextFrame++;
     int rc;
+    ctx->fr.drawDt = -1.0f;
+    const float dt = frame_delta(ctx);  // UpdateFrame's timer, read once per frame
+    if (ctx->useDynamicResolution && frame > 1 && ctx->fullFrame) update_dynamic_resolution(ctx, dt);
+    ctx->fr.drawDt = dt;
     if ((rc = rt_build_bvh(ctx)) != RT_OK) return rc;
     if ((rc = rt_path_trace(ctx, frame, 0)) != RT_OK) return rc;
     if ((rc = rt_denoise_post(ctx, frame, hdr_out != nullptr)) != RT_OK) return rc;

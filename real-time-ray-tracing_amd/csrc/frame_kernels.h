@@ -143,6 +143,8 @@ struct PathTraceParams {
 struct DenoisePostParams {
     uint32_t W, H;              // render size
     uint32_t Ws, Hs;            // screen size
+    uint32_t histW, histH;      // render size of the previous frame (historyDim, kernel.cu:266):
+                                // the accumulation / history colour buffers are read at that size
     int frameNum;
     float deltaTime;            // ms
     int temporal, localSpatial, visualize, wideSpatial, temporal2;   // RenderPassSettings

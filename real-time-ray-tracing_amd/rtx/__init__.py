@@ -148,7 +148,8 @@ class RtError(RuntimeError):
 
 
 def write_config(path: str, width: int, height: int, dynamic: bool = False, chunk_dim: int = 1, spp: int = 1,
-                 extra: str = "", max_size=(3840, 2160), camera_file: str | None = None) -> str:
+                 extra: str = "", max_size=(3840, 2160), camera_file: str | None = None, min_size=(640, 480),
+                 target_fps: float = 60.0) -> str:
     """Write a config.toml with the reference's three tables (resources/config.toml) + extensions."""
     with open(path, "w") as f:
         f.write("[resolution]\nwidth = %d\nheight = %d\n\n" % (width, height))
@@ -157,8 +158,9 @@ def write_config(path: str, width: int, height: int, dynamic: bool = False, chun
                     % (camera_file, camera_file))
         else:
             f.write("[file]\nloadCameraAtInit = false\n\n")
-        f.write("[optimziation]\nuseDynamicResolution = %s\ntargetFps = 60.0\nmaxWidth = %d\nmaxHeight = %d\n"
-                "minWidth = 640\nminHeight = 480\n\n" % ("true" if dynamic else "false", max_size[0], max_size[1]))
+        f.write("[optimziation]\nuseDynamicResolution = %s\ntargetFps = %r\nmaxWidth = %d\nmaxHeight = %d\n"
+                "minWidth = %d\nminHeight = %d\n\n" % ("true" if dynamic else "false", float(target_fps), max_size[0],
+                                                      max_size[1], min_size[0], min_size[1]))
         f.write("[scene]\nchunkDim = %d\n\n[render]\nspp = %d\n" % (chunk_dim, spp))
         f.write(extra)
     return path

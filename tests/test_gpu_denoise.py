@@ -141,6 +141,39 @@ def test_draw_1080p_4spp(rtx, oracle, tmp_path, default_scene):
     rt.cleanup()
 
 
+def test_draw_dynamic_resolution(rtx, oracle, tmp_path, default_scene):
+    """useDynamicResolution through rt_draw (UpdateFrame, kernel.cu:77-100): frame times outside
+    the targetFps band resize the render size frame to frame; the temporal passes read their
+    history at the previous frame's size (historyDim) and BicubicScale resamples to the screen."""
+    maxw, maxh, ws, hs = 192, 108, 160, 90
+    cfg = rtx.write_config(str(tmp_path / "c.toml"), ws, hs, dynamic=True, max_size=(maxw, maxh), min_size=(64, 36))
+    rt = rtx.RayTracer(ws, hs, cfg).init()
+    s, tex = oracle.sky(), oracle.textures()
+    dn = oracle.Denoiser(maxw, maxh, ws, hs)
+    rgba = np.zeros((hs, ws, 4), np.uint8)
+    hdr = np.zeros((maxw * maxh, 4), np.float32)
+    w, h, prev, sizes = maxw, maxh, None, []
+    for f, dt in enumerate((16.667, 40.0, 10.0, 25.0, 16.4), start=1):
+        if f > 1:
+            w, h = oracle.dynamic_resolution(w, dt, 60.0, 64, maxw, maxh)
+        sizes.append((w, h))
+        oc, rc = terrain_camera(rtx, oracle, w, h, pos=(8.0 + 0.15 * f, 15.0, -6.0 + 0.1 * f), yaw=0.02 * f,
+                                pitch=-0.7 + 0.01 * f)
+        rt.camera = rc
+        rt.set_delta_time(dt)
+        rt.draw(rgba, hdr)
+        info = rt.info()
+        assert (info.renderWidth, info.renderHeight) == (w, h)
+        gb = oracle.pathtrace(default_scene["bvh"], w, h, frame_num=f, cam=oc, hist_cam=prev or oc, sky_out=s, tex=tex)
+        o = dn.draw(gb, f, delta_time=dt, size=(w, h))
+        assert np.array_equal(rgba.reshape(-1, 4), o["rgba"]), f
+        ref = o["color"][:, :3].view(np.float16).astype(np.float32)
+        assert np.array_equal(hdr[:w * h, :3], ref), f
+        prev = oc
+    rt.cleanup()
+    assert sizes == [(192, 108), (128, 72), (160, 90), (128, 72), (128, 72)]
+
+
 @pytest.mark.parametrize("tm", [0, 1, 2])
 def test_denoise_post_tone_mappers(rtx, oracle, tmp_path, default_scene, tm):
     """ToneMappingType Uncharted (0, NaN by construction in the reference), ACES1 (1, ACESFitted

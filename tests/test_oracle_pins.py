@@ -146,3 +146,27 @@ def test_sky_model_matches_reference_probe(oracle):
         if best is None or err < best:
             best = err
     assert best < 0.005
+
+
+def test_dynamic_resolution_rule(oracle):
+    """UpdateFrame's dynamic-resolution step (kernel.cu:77-100) restated in float32 arithmetic:
+    outside the targetFps +-2 band the width scales by sqrt(target / dt) (int *= float), snaps
+    to the nearest multiple of 16 (8 rounds up), clamps to [minWidth, maxWidth]; height = w/16*9."""
+    f32 = np.float32
+
+    def rule(w, dt, fps, lo, hi, maxh):
+        high, low = f32(1000.0) / f32(fps - 2), f32(1000.0) / f32(fps + 2)
+        if high < f32(dt) or low > f32(dt):
+            w = int(f32(w) * np.sqrt(f32(1000.0) / f32(fps) / f32(dt)))
+        w = w - w % 16 if w % 16 < 8 else w + 16 - w % 16
+        w = lo if w < lo else (hi if w > hi else w)
+        return w, min((w // 16) * 9, maxh)
+
+    cases = [(192, 40.0), (128, 10.0), (160, 25.0), (128, 16.4), (1920, 16.0), (1920, 13.3), (3840, 5.0),
+             (1000, 1000.0), (647, 16.667), (1288, 17.5)]
+    for w, dt in cases:
+        assert oracle.dynamic_resolution(w, dt, 60.0, 640 if w >= 640 else 64, 3840, 2160) == \
+            rule(w, dt, 60.0, 640 if w >= 640 else 64, 3840, 2160), (w, dt)
+    assert oracle.dynamic_resolution(192, 40.0, 60.0, 64, 192, 108) == (128, 72)
+    assert oracle.dynamic_resolution(1920, 1000.0, 60.0, 640, 3840, 2160) == (640, 360)   # clamped to minWidth
+    assert oracle.dynamic_resolution(3840, 13.3, 60.0, 640, 3840, 2160) == (3840, 2160)   # 75-fps cap: grows, clamped

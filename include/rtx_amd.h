@@ -112,6 +112,19 @@ typedef struct rt_camera {
 int rt_get_camera(const rt_context* ctx, rt_camera* out); /* RayTracer::GetCamera */
 int rt_set_camera(rt_context* ctx, const rt_camera* in);
 
+/* Input (inputControl.cu:29-113): a windowing host forwards GLFW events (key, action and
+ * modifier values are GLFW's).  keyboardUpdate sets the W/S/A/D/C/X movement flags and the
+ * shift slow-down, or with ctrl saves (C) / loads (V) the camera at [file] cameraSaveFileName;
+ * cursorPosUpdate turns the cursor delta into yaw / pitch (the first event after a cursor reset
+ * only records the position); scrollUpdate and mouseButtenUpdate are no-ops as in the
+ * reference.  rt_draw moves the camera by the held keys once per frame (InputControlUpdate,
+ * pos += dir * deltaTime * moveSpeed).  cursorReset (kernel.cuh:465) starts set. */
+int rt_keyboard_update(rt_context* ctx, int key, int scancode, int action, int mods);
+int rt_cursor_pos_update(rt_context* ctx, double xpos, double ypos);
+int rt_scroll_update(rt_context* ctx, double xoffset, double yoffset);
+int rt_mouse_button_update(rt_context* ctx, int button, int action, int mods);
+int rt_set_cursor_reset(rt_context* ctx, int reset);
+
 /* RayTracer::SaveCameraToFile / LoadCameraFromFile (inputControl.cu:115-149): the reference's
  * 176-byte binary Camera record (kernel.cuh:78-100, derived fields included).  Loading takes
  * pos, pitch, yaw, focal, aperture and fov.x from the record; the derived fields are recomputed

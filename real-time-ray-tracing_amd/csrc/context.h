@@ -116,6 +116,15 @@ struct FrameResources {
     float drawDt = -1.0f;          // this rt_draw's frame time (ms), taken once by UpdateFrame
 };
 
+struct InputState {  // InputControl (inputControl.cu:8-25) + RayTracer::cursorReset (kernel.cuh:465)
+    float moveSpeed = 0.01f;
+    float cursorMoveSpeed = 0.001f;
+    double xpos = 0, ypos = 0;
+    bool moveW = false, moveS = false, moveA = false, moveD = false, moveC = false, moveX = false;
+    float deltax = 0, deltay = 0;
+    bool cursorReset = true;
+};
+
 struct rt_context {
     // ---- settings (GlobalSettings, globalSettings.h:5-22) + extensions
     int screenW = 1920, screenH = 1080;
@@ -143,6 +152,7 @@ struct rt_context {
     int nextFrame = 1;     // frameNum of the next draw (kernel.cu:64 starts at 1)
     int lastFrame = 0;
     float deltaMs = 16.667f;
+    InputState input;
 
     // ---- scene
     rtscene::SceneMesh mesh;
@@ -222,4 +232,5 @@ extern "C" void bvh_select(rt_context* ctx, int k);  // context.cpp: point the d
 extern "C" int wait_bvh(rt_context* ctx);  // context.cpp: context stream waits for the LBVH build
 std::string rt_data_dir();
 void rt_camera_update(const rt_camera& in, int renderW, int renderH, HostCamera& c);
+void rt_input_control_update(rt_context* ctx, float deltaTime);  // input.cpp
 TraceCamera rt_trace_camera(const HostCamera& c);

@@ -655,6 +655,7 @@ int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
     ctx->fr.drawDt = -1.0f;
     const float dt = frame_delta(ctx);  // UpdateFrame's timer, read once per frame
     if (ctx->useDynamicResolution && frame > 1 && ctx->fullFrame) update_dynamic_resolution(ctx, dt);
+    rt_input_control_update(ctx, dt);  // UpdateFrame's InputControlUpdate (kernel.cu:117)
     ctx->fr.drawDt = dt;
     if ((rc = rt_build_bvh(ctx)) != RT_OK) return rc;
     if ((rc = rt_path_trace(ctx, frame, 0)) != RT_OK) return rc;

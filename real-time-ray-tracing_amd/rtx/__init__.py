@@ -97,6 +97,11 @@ SIGNATURES = {
     "rt_set_camera": (C.c_int, [C.c_void_p, C.POINTER(Camera)]),
     "rt_set_frame_index": (C.c_int, [C.c_void_p, C.c_int]),
     "rt_set_delta_time": (C.c_int, [C.c_void_p, C.c_float]),
+    "rt_keyboard_update": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "rt_cursor_pos_update": (C.c_int, [C.c_void_p, C.c_double, C.c_double]),
+    "rt_scroll_update": (C.c_int, [C.c_void_p, C.c_double, C.c_double]),
+    "rt_mouse_button_update": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
+    "rt_set_cursor_reset": (C.c_int, [C.c_void_p, C.c_int]),
     "rt_get_info": (C.c_int, [C.c_void_p, C.POINTER(Info)]),
     "rt_get_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     "rt_buffer_bytes": (C.c_size_t, [C.c_void_p, C.c_int]),
@@ -226,6 +231,22 @@ class RayTracer:
 
     def set_delta_time(self, ms: float):
         self._check(self.lib.rt_set_delta_time(self.h, ms), "rt_set_delta_time")
+
+    # ---- input (inputControl.cu): GLFW key / action / modifier values
+    def keyboard_update(self, key: int, scancode: int, action: int, mods: int):
+        self._check(self.lib.rt_keyboard_update(self.h, key, scancode, action, mods), "rt_keyboard_update")
+
+    def cursor_pos_update(self, x: float, y: float):
+        self._check(self.lib.rt_cursor_pos_update(self.h, x, y), "rt_cursor_pos_update")
+
+    def scroll_update(self, dx: float, dy: float):
+        self._check(self.lib.rt_scroll_update(self.h, dx, dy), "rt_scroll_update")
+
+    def mouse_button_update(self, button: int, action: int, mods: int):
+        self._check(self.lib.rt_mouse_button_update(self.h, button, action, mods), "rt_mouse_button_update")
+
+    def set_cursor_reset(self, reset: bool = True):
+        self._check(self.lib.rt_set_cursor_reset(self.h, int(reset)), "rt_set_cursor_reset")
 
     def info(self) -> Info:
         i = Info()

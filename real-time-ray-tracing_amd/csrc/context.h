@@ -174,8 +174,8 @@ struct rt_context {
     // at the next host read / denoise call, whichever comes first
     bool postPending = false;
     int postPendingSet = 0;
-    int overlapAfter = 5;  // after k_pt_resume<4>: measured best with cameraAfter = 2
-    int cameraAfter = 2;   // the next frame's camera rays start after this frame's trace<3>
+    int overlapAfter = 1;  // after k_pt_shade0: measured best with cameraAfter = 3 at 1-8 ranks
+    int cameraAfter = 3;   // the next frame's camera rays start after this frame's resume<3>
     hipEvent_t cameraGate = nullptr;
     bool cameraGated = false;
     DenoisePostParams postParams{};

@@ -140,14 +140,23 @@ def main():
     if pipeline:  # denoise/post of frame f on a second stream, overlapping the trace of frame f+1
         rt.set_post_stream(post.cuda_stream)
     sg = StripGather(W, H, world, rank, dev, rt, sets=rtx.GBUFFER_SETS if pipeline else 1) if world > 1 else None
+    # RCCL gathers on a stream of their own: the next frame's path trace does not wait for the
+    # collective, only the frame's own denoise does (rt_set_gather_stream)
+    gs = torch.cuda.Stream(dev) if (sg is not None and args.dist_backend == "nccl") else None
+    if gs is not None:
+        rt.set_gather_stream(gs.cuda_stream)
 
     def frame(f):
         rt.build_bvh()
         rt.path_trace(f)
         if sg is not None:
-            if args.dist_backend == "gloo":
+            if gs is not None:
+                gs.wait_stream(torch.cuda.current_stream(dev))  # this frame's path trace
+                with torch.cuda.stream(gs):
+                    sg.gather()
+            else:
                 rt.sync()  # gloo copies through the host: the strip must be complete
-            sg.gather()
+                sg.gather()
         rt.denoise_post(f)
 
     for k in range(args.warmup):

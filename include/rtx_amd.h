@@ -229,6 +229,14 @@ int rt_set_stream(rt_context* ctx, void* stream);
 #define RT_BUF_SET2 0x200
 int rt_set_post_stream(rt_context* ctx, void* stream);
 
+/* Multi-GPU gathers off the trace chain (no reference counterpart): each later rt_denoise_post
+ * also waits for the work enqueued on `stream` up to that call, so a host that gathers a
+ * frame's G-buffer rows on its own stream (after the path trace; rtx/dist.py) keeps the next
+ * frame's path trace free of the collective.  The gathers must not write a G-buffer set the
+ * renderer is still using: gather the set rt_info.gbufferSet names, right after its path trace.
+ * NULL (the default) turns it off. */
+int rt_set_gather_stream(rt_context* ctx, void* stream);
+
 /* Use caller-owned device memory (>= rt_buffer_bytes, 16-B aligned) as one of the path-trace
  * G-buffers (RT_BUF_RENDER_COLOR / NORMAL / ALBEDO / DEPTH / MOTION), e.g. so a multi-GPU host
  * can all-gather screen strips in place.  The memory must outlive the context's use of it. */

@@ -371,7 +371,7 @@ void rt_destroy(rt_context* ctx) {
     for (hipEvent_t e : {ctx->overlapEv, ctx->cameraGate, ctx->buildDone[0], ctx->buildDone[1], ctx->bvhFree[0], ctx->bvhFree[1]})
         if (e) (void)hipEventDestroy(e);
     for (int k = 0; k < kGbSets; ++k)
-        for (hipEvent_t e : {ctx->ptDone[k], ctx->postDone[k], ctx->camDone[k], ctx->restDone[k]})
+        for (hipEvent_t e : {ctx->ptDone[k], ctx->postDone[k], ctx->camDone[k], ctx->restDone[k], ctx->gatherDone[k]})
             if (e) (void)hipEventDestroy(e);
     if (ctx->sideStream) (void)hipStreamDestroy(ctx->sideStream);
     for (void* p : ctx->allocations) (void)hipFree(p);

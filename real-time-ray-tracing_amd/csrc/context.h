@@ -165,6 +165,9 @@ struct rt_context {
     hipStream_t postStream = nullptr;  // optional: denoise + post run here (rt_set_post_stream)
     hipStream_t sideStream = nullptr;  // pipelining: LBVH build + camera rays of the next frame
     hipEvent_t ptDone[kGbSets] = {}, postDone[kGbSets] = {}, overlapEv = nullptr;
+    hipStream_t gatherStream = nullptr;  // optional: the caller's G-buffer gathers (rt_set_gather_stream)
+    hipEvent_t gatherDone[kGbSets] = {};
+    bool postGather = false;             // the pending denoise also waits for gatherDone[its set]
     hipEvent_t buildDone[2] = {}, bvhFree[2] = {}, camDone[kGbSets] = {}, restDone[kGbSets] = {};
     bool bvhInFlight[2] = {false, false}, buildOnSide[2] = {false, false};
     BvhBufs bvh[2];

@@ -206,6 +206,7 @@ int issue_pending_post(rt_context* ctx) {
     ctx->postPending = false;
     const int set = ctx->postPendingSet;
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->postStream, ctx->ptDone[set], 0));
+    if (ctx->postGather) HIP_TRY(ctx, hipStreamWaitEvent(ctx->postStream, ctx->gatherDone[set], 0));
     HIP_TRY(ctx, rtk_denoise_post(&ctx->postParams, ctx->postStream));
     HIP_TRY(ctx, hipEventRecord(ctx->postDone[set], ctx->postStream));
     ctx->fr.renderColor = ctx->postParams.finalColor;  // the launcher's buffer plan names them
@@ -631,11 +632,17 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
         int rc = issue_pending_post(ctx);
         if (rc != RT_OK) return rc;
         HIP_TRY(ctx, hipEventRecord(ctx->ptDone[fr.gbSet], ctx->stream));
+        ctx->postGather = ctx->gatherStream != nullptr;
+        if (ctx->postGather) HIP_TRY(ctx, hipEventRecord(ctx->gatherDone[fr.gbSet], ctx->gatherStream));
         ctx->postParams = p;
         ctx->postPendingSet = fr.gbSet;
         ctx->postPending = true;
         fr.setInFlight[fr.gbSet] = true;
     } else {
+        if (ctx->gatherStream) {
+            HIP_TRY(ctx, hipEventRecord(ctx->gatherDone[0], ctx->gatherStream));
+            HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->gatherDone[0], 0));
+        }
         HIP_TRY(ctx, rtk_denoise_post(&p, ctx->stream));
         fr.renderColor = p.finalColor;
         fr.scaledColor = p.finalScaled;
@@ -674,6 +681,17 @@ int rt_set_stream(rt_context* ctx, void* stream) {
     int rc = sync_streams(ctx);
     if (rc != RT_OK) return rc;
     ctx->stream = stream == RT_OWN_STREAM ? ctx->ownStream : (hipStream_t)stream;  // NULL: the null stream
+    return RT_OK;
+}
+
+int rt_set_gather_stream(rt_context* ctx, void* stream) {
+    if (!ctx) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_set_gather_stream before rt_init"; return RT_ERR_STATE; }
+    int rc = sync_streams(ctx);
+    if (rc != RT_OK) return rc;
+    for (int k = 0; k < kGbSets; ++k)
+        if (!ctx->gatherDone[k]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->gatherDone[k], hipEventDisableTiming));
+    ctx->gatherStream = (hipStream_t)stream;
     return RT_OK;
 }
 

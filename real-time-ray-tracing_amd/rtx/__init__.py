@@ -109,6 +109,7 @@ SIGNATURES = {
     "rt_denoise_post": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "rt_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "rt_set_post_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "rt_set_gather_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "rt_bind_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     "rt_get_ray_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "rt_build_bvh": (C.c_int, [C.c_void_p]),
@@ -275,6 +276,10 @@ class RayTracer:
     def set_post_stream(self, stream_ptr: int | None):
         """Run denoise + post on a second stream and alternate two G-buffer sets (frame pipelining)."""
         self._check(self.lib.rt_set_post_stream(self.h, stream_ptr), "rt_set_post_stream")
+
+    def set_gather_stream(self, stream: int | None):
+        """Stream the caller gathers G-buffers on; each later denoise also waits for it."""
+        self._check(self.lib.rt_set_gather_stream(self.h, stream or None), "rt_set_gather_stream")
 
     def bind_buffer(self, name: str, device_ptr: int, nbytes: int, gbuffer_set: int = 0):
         what = BUF[name] | (int(gbuffer_set) << 8)  # RT_BUF_SET1 / RT_BUF_SET2

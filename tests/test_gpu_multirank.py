@@ -21,7 +21,7 @@ def free_port():
     return p
 
 
-def render(rank, world, port, out_dir, pipelined):
+def render(rank, world, port, out_dir, pipelined, gather_stream):
     import torch
     import torch.distributed as dist
 
@@ -43,6 +43,9 @@ def render(rank, world, port, out_dir, pipelined):
         rt.set_post_stream(post.cuda_stream)
     sets = rtx.GBUFFER_SETS if pipelined else 1
     sg = StripGather(W, H, world, rank, dev, rt, sets=sets) if world > 1 else None
+    gs = torch.cuda.Stream(dev) if (gather_stream and sg is not None) else None
+    if gs is not None:
+        rt.set_gather_stream(gs.cuda_stream)
     cam0 = rt.camera
     for f in range(1, FRAMES + 1):
         c = rt.camera
@@ -52,7 +55,12 @@ def render(rank, world, port, out_dir, pipelined):
         rt.path_trace(f)
         if sg is not None:
             rt.sync()  # gloo reads the tensors on the host side: the strip must be complete
-            sg.gather()
+            if gs is not None:  # gathers on their own stream; the denoise waits for it
+                gs.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(gs):
+                    sg.gather()
+            else:
+                sg.gather()
         rt.denoise_post(f)
     rgba = rt.download("RGBA8", np.uint8).copy()
     hdr = rt.get_buffer("RENDER_COLOR").copy()
@@ -62,14 +70,16 @@ def render(rank, world, port, out_dir, pipelined):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pipelined", [True, False])
-def test_two_ranks_one_gpu_match_single_rank(tmp_path, pipelined):
+@pytest.mark.parametrize("pipelined,gather_stream", [(True, False), (False, False), (True, True), (False, True)])
+def test_two_ranks_one_gpu_match_single_rank(tmp_path, pipelined, gather_stream):
     """The renderer runs on torch's default stream (the null stream, handle 0) like the gathers:
-    serial frames exercise exactly that ordering."""
+    serial frames exercise exactly that ordering.  gather_stream: the gathers run on a stream of
+    their own (rt_set_gather_stream), as bench.py does over RCCL."""
     import torch.multiprocessing as mp
 
-    mp.start_processes(render, args=(1, 0, str(tmp_path), pipelined), nprocs=1, start_method="spawn")
-    mp.start_processes(render, args=(2, free_port(), str(tmp_path), pipelined), nprocs=2, start_method="spawn")
+    mp.start_processes(render, args=(1, 0, str(tmp_path), pipelined, gather_stream), nprocs=1, start_method="spawn")
+    mp.start_processes(render, args=(2, free_port(), str(tmp_path), pipelined, gather_stream), nprocs=2,
+                       start_method="spawn")
     ref = np.load(tmp_path / "r0_of1.npz")
     for r in range(2):
         got = np.load(tmp_path / ("r%d_of2.npz" % r))

@@ -16,7 +16,11 @@ def hip_stream():
     import ctypes
     import os
 
-    hip = ctypes.CDLL(os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "libamdhip64.so"))
+    # the HIP runtime the renderer is bound to: whichever libamdhip64 the process loaded first
+    # (torch's bundled copy when torch came first) -- a second copy would not link
+    loaded = [ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln]
+    path = loaded[0] if loaded else os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "libamdhip64.so")
+    hip = ctypes.CDLL(path)
     s = ctypes.c_void_p()
     assert hip.hipStreamCreate(ctypes.byref(s)) == 0
     return hip, s

@@ -140,6 +140,13 @@ def load_library(path: str | None = None) -> C.CDLL:
     path = path or os.environ.get("RTX_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError("librtx.so not found at %s — run `make` (or __graft_entry__.build())" % path)
+    # One HIP runtime per process: torch ships its own libamdhip64 (same soname, different path).
+    # Loaded after librtx it would be a second runtime that finds no GPU, so when torch is
+    # installed it is loaded first and librtx binds to it; streams then pass freely between them.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -10,29 +10,21 @@ pytestmark = pytest.mark.gpu
 W, H, FRAMES = 320, 180, 6
 
 
-def hip_stream():
-    """A HIP stream made through the HIP runtime directly (the renderer has initialised HIP by
-    the time this runs; torch's own lazy init is not needed for the C-ABI)."""
-    import ctypes
-    import os
+def post_stream():
+    """The post stream, made by torch as bench.py makes it: torch and the renderer share one HIP
+    runtime in this process, so torch's stream handle is valid for rt_set_post_stream."""
+    import torch
 
-    # the HIP runtime the renderer is bound to: whichever libamdhip64 the process loaded first
-    # (torch's bundled copy when torch came first) -- a second copy would not link
-    loaded = [ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln]
-    path = loaded[0] if loaded else os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "libamdhip64.so")
-    hip = ctypes.CDLL(path)
-    s = ctypes.c_void_p()
-    assert hip.hipStreamCreate(ctypes.byref(s)) == 0
-    return hip, s
+    return torch.cuda.Stream(device=0)
 
 
 def run(rtx, tmp_path, pipelined, per_frame):
     cfg = rtx.write_config(str(tmp_path / ("p%d%d.toml" % (pipelined, per_frame))), W, H, spp=2)
     rt = rtx.RayTracer(W, H, cfg).init()
     rt.set_delta_time(16.667)
-    hip, post = hip_stream() if pipelined else (None, None)
+    post = post_stream() if pipelined else None
     if pipelined:
-        rt.set_post_stream(post.value)
+        rt.set_post_stream(post.cuda_stream)
     cam0 = rt.camera
     images = []
     for f in range(1, FRAMES + 1):
@@ -50,8 +42,6 @@ def run(rtx, tmp_path, pipelined, per_frame):
         out[b] = rt.get_buffer(b).copy()
     sets = rt.info().gbufferSet
     rt.cleanup()
-    if pipelined:
-        hip.hipStreamDestroy(post)
     return out, images, sets
 
 

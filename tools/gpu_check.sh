@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 step() { echo "[$(date +%T)] $*"; }
 if [[ $WHAT == tests || $WHAT == all ]]; then
   step pytest-gpu
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
   tail -2 "$OUT/pytest_gpu.log"
   step smoke
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -30 "$OUT/smoke.log"; exit 1; }

@@ -1,6 +1,7 @@
 # Build recipe (no cmake in the product path).  `make -j8` builds:
 #   real-time-ray-tracing_amd/lib/librtx.so   the product: HIP kernels for gfx950 + host runtime + C-ABI
 #   oracle/_build/liboracle.so                the CPU restatement (test infrastructure only)
+#   oracle/_build/liboracle_libm.so           the same with host-libm transcendentals (parity metric)
 HIPCC    ?= /opt/rocm/bin/hipcc
 CXX      ?= g++
 PKG      := real-time-ray-tracing_amd
@@ -21,7 +22,7 @@ CPP_OBJS := $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.cpp.o,$(CPP_SRCS))
 ORC_SRCS := $(wildcard oracle/*.cpp)
 ORC_HDRS := $(wildcard oracle/*.h) $(CSRC)/rtmath.h $(CSRC)/scene_gen.h
 
-all: $(LIBDIR)/librtx.so oracle/_build/liboracle.so
+all: $(LIBDIR)/librtx.so oracle/_build/liboracle.so oracle/_build/liboracle_libm.so
 
 $(OBJDIR)/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -37,6 +38,11 @@ $(LIBDIR)/librtx.so: $(HIP_OBJS) $(CPP_OBJS)
 oracle/_build/liboracle.so: $(ORC_SRCS) $(ORC_HDRS) $(CSRC)/scene_gen.cpp
 	@mkdir -p oracle/_build
 	$(CXX) $(CXXFLAGS) -shared -o $@ $(ORC_SRCS) $(CSRC)/scene_gen.cpp -lpthread
+
+# the same restatement with host-libm transcendentals (parity metric, ocommon.h ORC_LIBM)
+oracle/_build/liboracle_libm.so: $(ORC_SRCS) $(ORC_HDRS) $(CSRC)/scene_gen.cpp
+	@mkdir -p oracle/_build
+	$(CXX) $(CXXFLAGS) -DORC_LIBM -shared -o $@ $(ORC_SRCS) $(CSRC)/scene_gen.cpp -lpthread
 
 clean:
 	rm -rf $(LIBDIR) oracle/_build

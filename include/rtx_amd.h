@@ -213,6 +213,7 @@ int rt_get_ray_count(rt_context* ctx, uint64_t* rays, int reset);
  * its collectives order with the renderer).  NULL is the device's null stream (a framework's
  * default stream, e.g. torch's, is that stream); RT_OWN_STREAM restores the context's own. */
 #define RT_OWN_STREAM ((void*)(intptr_t)-1)
+#define RT_STREAM_OFF ((void*)(intptr_t)-2) /* rt_set_gather_stream: no gather stream */
 int rt_set_stream(rt_context* ctx, void* stream);
 
 /* Frame pipelining (no reference counterpart; the reference draws frames strictly one after
@@ -234,10 +235,11 @@ int rt_set_post_stream(rt_context* ctx, void* stream);
  * frame's G-buffer rows on its own stream (after the path trace; rtx/dist.py) keeps the next
  * frame's path trace free of the collective.  The gathers must not write a G-buffer set the
  * renderer is still using: gather the set rt_info.gbufferSet names, right after its path trace.
- * NULL (the default) turns it off. */
+ * NULL is the null stream (as in rt_set_stream); RT_STREAM_OFF (the default) turns it off. */
 int rt_set_gather_stream(rt_context* ctx, void* stream);
 
-/* Use caller-owned device memory (>= rt_buffer_bytes, 16-B aligned) as one of the path-trace
+/* Use caller-owned device memory (>= the buffer's size at the largest render size, i.e.
+ * maxWidth x maxHeight with dynamic resolution, else rt_buffer_bytes; 16-B aligned) as one of the path-trace
  * G-buffers (RT_BUF_RENDER_COLOR / NORMAL / ALBEDO / DEPTH / MOTION), e.g. so a multi-GPU host
  * can all-gather screen strips in place.  The memory must outlive the context's use of it. */
 int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes);
@@ -256,6 +258,12 @@ int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms);
  * (n >= 7: camera, shade, trace bounce queue, resume, trace shadow queue, resume, resolve).
  * Measurement aid for the roofline in bench.py; no reference counterpart. */
 int rt_time_path_trace_kernels(rt_context* ctx, int iters, float* kernel_ms, int n);
+
+/* The same split over `iters` whole frames (LBVH build + path trace + denoise/post of frames
+ * first_frame, first_frame + 1, ...) run exactly as a caller runs them: on a pipelined context
+ * (rt_set_post_stream) each kernel is timed on the stream it runs on, beside the other streams'
+ * work.  Waits for the frames.  Measurement aid for bench.py's per-kernel roofline. */
+int rt_time_frame_kernels(rt_context* ctx, int first_frame, int iters, float* kernel_ms, int n);
 
 /* Copies device arrays to host (debug dumps of bvh.cu:15-96, traversal outputs). */
 enum rt_array_name {
@@ -294,7 +302,11 @@ enum rt_array_name {
                                     deferred at step 3, [1] at step 4, [4] pixels resolved late,
                                     [8]/[9] longest traversal (iterations) of the step-3/4 queues
                                     (detail launches only), [10] internal errors (must be 0),
-                                    [11] pixels with a sample that hit geometry */
+                                    [11] pixels with a sample that hit geometry; detail launches
+                                    also: node visits / triangle tests of [12,13] the camera
+                                    kernel, [14,15] the shade kernel (inline glossy traces),
+                                    [16,17] the step-3 and [18,19] the step-4 queue tracers,
+                                    diffuse events of [20] the shade and [21] the resume<3> kernel */
     RT_ARR_PT_Q3_ORIGINS = 33,   /* float4[cap] step-3 queue rays of the last launch: origin xyz, pixel bits */
     RT_ARR_PT_Q3_DIRS = 34,      /* float4[cap] direction xyz, flags bits ([0] of RT_ARR_PT_QUEUE are valid) */
     RT_ARR_PT_Q4_ORIGINS = 35,   /* float4[cap] step-4 queue, same layout ([1] valid) */

@@ -9,6 +9,7 @@
 // sequenced as BuildBvhLevel1/2 (bvh.cu:7-97).  The per-frame memsets of morton/tlasMorton
 // to 0xFFFFFFFF (kernel.cu:279-280) are part of the contract.
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "oracle.h"
@@ -114,7 +115,13 @@ static void stable_sort_1024(uint32_t* keys, uint32_t* reorder) {
 
 using namespace orc;
 
-extern "C" int orc_build_bvh(const OrcBvhIO* io) {
+extern "C" int orc_build_bvh_mt(const OrcBvhIO* io, int threads);
+
+extern "C" int orc_build_bvh(const OrcBvhIO* io) { return orc_build_bvh_mt(io, 1); }
+
+// threads > 1: the BLAS batches (independent blocks in the reference) spread over host threads;
+// the result does not depend on the split
+extern "C" int orc_build_bvh_mt(const OrcBvhIO* io, int threads) {
     const uint32_t N = io->triCount, NP = io->triCountPadded;
     if (N < 2 || NP < N || NP % 4 != 0) return -1;
     const uint32_t B = (N + 1023) / 1024;
@@ -128,7 +135,7 @@ extern "C" int orc_build_bvh(const OrcBvhIO* io) {
     for (uint32_t k = 0; k < 1024; ++k) io->tlasMortonUnsorted[k] = 0xFFFFFFFFu;
 
     // ---------------- BLAS (one block per batch)
-    for (uint32_t b = 0; b < B; ++b) {
+    auto blas = [&](uint32_t b) {
         const uint32_t start = b * 1024;
         const uint32_t cnt = (b + 1 < B) ? 1024u : N - (B - 1) * 1024u;  // init.cu:129-130
         const uint32_t active = (cnt - 1) / 4 + 1;                       // threads with tid*4 <= cnt-1
@@ -163,6 +170,17 @@ extern "C" int orc_build_bvh(const OrcBvhIO* io) {
         io->batchSceneAabbs[6 * b + 0] = scene.min.x; io->batchSceneAabbs[6 * b + 1] = scene.min.y;
         io->batchSceneAabbs[6 * b + 2] = scene.min.z; io->batchSceneAabbs[6 * b + 3] = scene.max.x;
         io->batchSceneAabbs[6 * b + 4] = scene.max.y; io->batchSceneAabbs[6 * b + 5] = scene.max.z;
+    };
+    if (threads <= 1 || B < 2) {
+        for (uint32_t b = 0; b < B; ++b) blas(b);
+    } else {
+        std::vector<std::thread> pool;
+        const uint32_t T = (uint32_t)threads < B ? (uint32_t)threads : B;
+        for (uint32_t t = 0; t < T; ++t)
+            pool.emplace_back([&, t] {
+                for (uint32_t b = t; b < B; b += T) blas(b);
+            });
+        for (auto& th : pool) th.join();
     }
 
     // ---------------- TLAS (one block)

@@ -31,8 +31,10 @@
 // `x >= W && y >= H` test lets them write a clamped edge texel).  A pixel whose own colour is
 // NaN is left unchanged by the LDS-staged filters (the reference returns before its barrier).
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <thread>
 #include <vector>
 
 #include "../include/rtx_amd.h"
@@ -42,6 +44,25 @@
 
 namespace orc {
 namespace {
+
+// rows of a per-pixel pass over host threads: every pass below writes only its own pixel from
+// read-only inputs, so the split changes nothing in the results (ORC_THREADS caps the count)
+template <typename F>
+void par_rows(int H, F f) {
+    int T = (int)std::thread::hardware_concurrency();
+    if (const char* e = getenv("ORC_THREADS")) T = atoi(e);
+    T = T < 1 ? 1 : (T > 32 ? 32 : T);
+    if (T == 1 || H < 64) {
+        for (int y = 0; y < H; ++y) f(y);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            for (int y = t; y < H; y += T) f(y);
+        });
+    for (auto& x : th) x.join();
+}
 
 const double kG3[9] = {0.0578968, 0.0921378, 0.0584323, 0.0921378, 0.146629, 0.09299, 0.0584322, 0.0929898, 0.0589727};
 const double kG5[25] = {0.00360466, 0.0144464, 0.0229902, 0.01458,   0.0036719,  0.0144464, 0.0578968,
@@ -137,7 +158,7 @@ void temporal_filter(const Ctx& c, const uint16_t* in, uint16_t* out, const uint
     const rt_denoising_params& dp = c.prm->denoise;
     const Img col{c.W, c.H, in, 4}, nrm = c.nrm(), dep = c.dep(), acc{c.hW, c.hH, accum, 4};
     memcpy(out, in, (size_t)c.W * c.H * 8);
-    for (int y = 0; y < c.H; ++y)
+    par_rows(c.H, [&](int y) {
         for (int x = 0; x < c.W; ++x) {
             const size_t p = (size_t)y * c.W + x;
             F3 cV = col.rgb(x, y);
@@ -206,6 +227,7 @@ void temporal_filter(const Ctx& c, const uint16_t* in, uint16_t* out, const uint
             if (isnan3(o)) o = f3(0.0f);
             store_color(out, p, o, mV);
         }
+    });
 }
 
 void tile_noise(const Ctx& c, const uint16_t* color, uint16_t* noise8, uint16_t* noise16) {
@@ -267,7 +289,7 @@ void spatial7x7(const Ctx& c, const uint16_t* in, uint16_t* out, const uint16_t*
     const Img col{c.W, c.H, in, 4}, nrm = c.nrm(), dep = c.dep();
     const int W16 = (c.W + 15) / 16;
     memcpy(out, in, (size_t)c.W * c.H * 8);
-    for (int y = 0; y < c.H; ++y)
+    par_rows(c.H, [&](int y) {
         for (int x = 0; x < c.W; ++x) {
             if (h2f(noise16[(size_t)(y / 16) * W16 + x / 16]) < dp.noise_threshold_local) continue;
             F3 cV = col.rgb(x, y);
@@ -307,6 +329,7 @@ void spatial7x7(const Ctx& c, const uint16_t* in, uint16_t* out, const uint16_t*
             if (isnan3(fin)) fin = f3(0.0f);
             store_color(out, (size_t)y * c.W + x, fin, mV);
         }
+    });
 }
 
 void spatial5x5(const Ctx& c, const uint16_t* in, uint16_t* out, const uint16_t* noise16, int S) {
@@ -314,7 +337,7 @@ void spatial5x5(const Ctx& c, const uint16_t* in, uint16_t* out, const uint16_t*
     const Img col{c.W, c.H, in, 4}, nrm = c.nrm(), dep = c.dep();
     const int W16 = (c.W + 15) / 16;
     memcpy(out, in, (size_t)c.W * c.H * 8);
-    for (int y = 0; y < c.H; ++y)
+    par_rows(c.H, [&](int y) {
         for (int x = 0; x < c.W; ++x) {
             if (h2f(noise16[(size_t)(y / 16) * W16 + x / 16]) < dp.noise_threshold_large) continue;
             F3 nV = nrm.rgb(x, y);
@@ -350,6 +373,7 @@ void spatial5x5(const Ctx& c, const uint16_t* in, uint16_t* out, const uint16_t*
             if (isnan3(fin)) fin = f3(0.0f);
             store_color(out, (size_t)y * c.W + x, fin, mV);
         }
+    });
 }
 
 void apply_albedo(const Ctx& c, uint16_t* color) {
@@ -365,7 +389,7 @@ void temporal_filter2(const Ctx& c, const uint16_t* in, uint16_t* out, const uin
     const Img col{c.W, c.H, in, 4}, hc{c.hW, c.hH, hist, 4};
     memcpy(out, in, (size_t)c.W * c.H * 8);
     const float FLTMIN = 1.17549435e-38f, FLTMAX = 3.402823466e+38f;
-    for (int y = 0; y < c.H; ++y)
+    par_rows(c.H, [&](int y) {
         for (int x = 0; x < c.W; ++x) {
             const size_t p = (size_t)y * c.W + x;
             const F3 cV = ycocg_inv(ycocg(col.rgb(x, y)));
@@ -415,6 +439,7 @@ void temporal_filter2(const Ctx& c, const uint16_t* in, uint16_t* out, const uin
             if (isnan3(o)) o = f3(0.0f);
             store_color(out, p, o, (uint16_t)mV);
         }
+    });
 }
 
 // ------------------------------------------------------------------ post
@@ -507,7 +532,7 @@ void auto_exposure(float* e, const uint32_t* hist, float area, float deltaTime, 
 }
 
 void bicubic_scale(const uint16_t* in, int W, int H, uint16_t* out, int Ws, int Hs) {
-    for (int y = 0; y < Hs; ++y)
+    par_rows(Hs, [&](int y) {
         for (int x = 0; x < Ws; ++x) {
             const F2 uv = {(float)x / Ws, (float)y / Hs};
             const F2 UV = {uv.x * (float)W, uv.y * (float)H};
@@ -534,10 +559,11 @@ void bicubic_scale(const uint16_t* in, int W, int H, uint16_t* out, int Ws, int 
             uint16_t* q = out + ((size_t)y * Ws + x) * 4;
             q[0] = f2h(o.x); q[1] = f2h(o.y); q[2] = f2h(o.z); q[3] = f2h(1.0f);
         }
+    });
 }
 
 void sharpen(const uint16_t* in, uint16_t* out, int W, int H) {
-    for (int y = 0; y < H; ++y)
+    par_rows(H, [&](int y) {
         for (int x = 0; x < W; ++x) {
             F3 c[3][3];
             for (int i = 0; i < 3; ++i)
@@ -567,6 +593,7 @@ void sharpen(const uint16_t* in, uint16_t* out, int W, int H) {
             uint16_t* q = out + ((size_t)y * W + x) * 4;
             q[0] = f2h(o.x); q[1] = f2h(o.y); q[2] = f2h(o.z); q[3] = f2h(1.0f);
         }
+    });
 }
 
 float luminance(F3 v) { return dot(v, f3(0.2126f, 0.7152f, 0.0722f)); }

@@ -6,6 +6,7 @@ See oracle/ocommon.h for what it restates and how it is pinned.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 
@@ -13,6 +14,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+# the same restatement with host-libm transcendentals (ocommon.h ORC_LIBM): the parity-metric
+# reference that shares no transcendental code with the product
+LIBM_PATH = os.path.join(HERE, "_build", "liboracle_libm.so")
 DATA_DIR = os.path.join(os.path.dirname(HERE), "real-time-ray-tracing_amd", "data")
 
 NODE_DTYPE = np.dtype([("lmin", "<f4", 3), ("lmax", "<f4", 3), ("rmin", "<f4", 3), ("rmax", "<f4", 3),
@@ -45,17 +49,31 @@ class CameraIn(C.Structure):
                 ("aperture", C.c_float), ("fovX", C.c_float), ("resolution", C.c_float * 2)]
 
 
-_lib = None
+_libs: dict = {}
+_variant = "rtmath"
+
+
+@contextlib.contextmanager
+def libm():
+    """Run the oracle calls inside the block on the host-libm build (liboracle_libm.so)."""
+    global _variant
+    old, _variant = _variant, "libm"
+    try:
+        yield
+    finally:
+        _variant = old
 
 
 def lib() -> C.CDLL:
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError("oracle not built: %s (run make)" % LIB_PATH)
-        L = C.CDLL(LIB_PATH)
+    path = LIBM_PATH if _variant == "libm" else LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise RuntimeError("oracle not built: %s (run make)" % path)
+        L = C.CDLL(path)
         L.orc_build_bvh.argtypes = [C.POINTER(BvhIO)]
         L.orc_build_bvh.restype = C.c_int
+        L.orc_build_bvh_mt.argtypes = [C.POINTER(BvhIO), C.c_int]
+        L.orc_build_bvh_mt.restype = C.c_int
         L.orc_morton3.argtypes = [C.c_uint32] * 3
         L.orc_morton3.restype = C.c_uint32
         L.orc_smooth_normals.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
@@ -75,8 +93,8 @@ def lib() -> C.CDLL:
         L.orc_scene_copy.argtypes = [C.c_void_p, C.c_void_p]
         L.orc_scene_copy.restype = None
         _bind_frame_api(L)
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def scene(chunk_dim: int = 1):
@@ -100,7 +118,7 @@ def smooth_normals(vertices: np.ndarray, indices: np.ndarray) -> np.ndarray:
     return out
 
 
-def build_bvh(vertices, indices, tri_count, normals=None) -> dict:
+def build_bvh(vertices, indices, tri_count, normals=None, threads: int = 1) -> dict:
     NP = indices.shape[0]
     B = (tri_count + 1023) // 1024
     out = dict(
@@ -117,7 +135,7 @@ def build_bvh(vertices, indices, tri_count, normals=None) -> dict:
                out["nodes"].ctypes.data, out["batch_scene_aabbs"].ctypes.data, out["tlas_aabbs"].ctypes.data,
                out["tlas_scene_aabb"].ctypes.data, out["tlas_morton_unsorted"].ctypes.data,
                out["tlas_morton"].ctypes.data, out["tlas_reorder"].ctypes.data, out["tlas_nodes"].ctypes.data)
-    rc = lib().orc_build_bvh(C.byref(io))
+    rc = lib().orc_build_bvh_mt(C.byref(io), threads)
     if rc < 0:
         raise RuntimeError("orc_build_bvh failed (%d)" % rc)
     out["batch_count"] = rc

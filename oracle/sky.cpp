@@ -90,7 +90,7 @@ static F3 sky_radiance(F3 raydir, F3 sunDir, const SkyState& st) {
                            rt_powf((1.0f + c[8] * c[8] - 2.0f * c[8] * rt_cosf(gamma)), 1.5f);
         const float zenith = sqrtf(rt_cosf(theta));
         // (cos(theta) + 0.01) promotes to double; so does the left factor and the product
-        double left = 1.0 + (double)c[0] * rtm::expd((double)c[1] / ((double)rt_cosf(theta) + 0.01));
+        double left = 1.0 + (double)c[0] * ORC_EXPD((double)c[1] / ((double)rt_cosf(theta) + 0.01));
         float right = c[2] + c[3] * expM + c[5] * rayM + c[6] * mieM + c[7] * zenith;
         float radianceInternal = (float)(left * (double)right);
         float radiance = radianceInternal * st.radiances[ch];

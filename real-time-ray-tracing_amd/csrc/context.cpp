@@ -250,6 +250,9 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
     ctx->fullFrame = ctx->stripCount == 1 && ctx->stripY0 == 0 && ctx->stripRows == ctx->renderH;
     ctx->histW = ctx->renderW;
     ctx->histH = ctx->renderH;
+    ctx->allocW = ctx->renderW;  // the largest frame: dynamic resolution only shrinks from here
+    ctx->allocH = ctx->renderH;
+    ctx->allocStripRows = ctx->stripRows;
     if (ctx->stripCount < 1 || ctx->stripY0 < 0 || ctx->stripRows < 1 || ctx->stripY0 + ctx->stripRows > ctx->renderH) {
         g_createError = "invalid strip rows";
         delete ctx;
@@ -367,7 +370,7 @@ int rt_init(rt_context* ctx) {
 
 void rt_destroy(rt_context* ctx) {
     if (!ctx) return;
-    if (ctx->stream) (void)sync_streams(ctx);
+    if (ctx->inited) (void)sync_streams(ctx);  // also when the context stream is the null stream
     for (hipEvent_t e : {ctx->overlapEv, ctx->cameraGate, ctx->buildDone[0], ctx->buildDone[1], ctx->bvhFree[0], ctx->bvhFree[1]})
         if (e) (void)hipEventDestroy(e);
     for (int k = 0; k < kGbSets; ++k)
@@ -530,7 +533,7 @@ int rt_trace_primary(rt_context* ctx, int frame_num, int with_detail) {
 
 int rt_sync(rt_context* ctx) {
     if (!ctx) return RT_ERR_ARG;
-    if (!ctx->stream) return RT_OK;
+    if (!ctx->inited) return RT_OK;  // NULL is a valid stream (the null stream): test the init state
     return sync_streams(ctx);
 }
 
@@ -566,36 +569,53 @@ int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms) {
     return RT_OK;
 }
 
+// per-kernel HIP-event split of `iters` path traces: serial ones (stage 2 of rt_time_stage) or,
+// with `frames` set, whole frames (BVH + path trace + denoise/post) as the caller runs them, so
+// on a pipelined context each kernel is timed beside the other streams' work (bench.py)
+static int time_kernels(rt_context* ctx, int first_frame, int iters, float* kernel_ms, int n, bool frames) {
+    if (!ctx || !kernel_ms || iters < 1 || n < kPtKernels || first_frame < 1) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_time_*_kernels before rt_init"; return RT_ERR_STATE; }
+    std::vector<hipEvent_t> marks((size_t)iters * 2 * kPtKernels, nullptr);
+    int rc = RT_OK;
+    for (auto& m : marks)
+        if (hipEventCreate(&m) != hipSuccess) { rc = RT_ERR_HIP; ctx->err = "hipEventCreate failed"; break; }
+    for (int k = 0; k < kPtKernels; ++k) kernel_ms[k] = 0.0f;
+    for (int i = 0; i < iters && rc == RT_OK; ++i) {
+        const int f = first_frame + i;
+        if (frames) rc = rt_build_bvh(ctx);
+        ctx->ptMarks = marks.data() + (size_t)i * 2 * kPtKernels;
+        if (rc == RT_OK) rc = rt_path_trace(ctx, f, 0);
+        ctx->ptMarks = nullptr;
+        if (rc == RT_OK && frames) rc = rt_denoise_post(ctx, f, 0);
+        if (rc == RT_OK && !frames && hipEventSynchronize(marks[(size_t)i * 2 * kPtKernels + 2 * kPtKernels - 1]) != hipSuccess)
+            rc = RT_ERR_HIP;
+    }
+    if (rc == RT_OK) rc = sync_streams(ctx);
+    for (int i = 0; i < iters && rc == RT_OK; ++i)
+        for (int k = 0; k < kPtKernels && rc == RT_OK; ++k) {
+            float ms = 0.0f;
+            hipEvent_t* m = marks.data() + (size_t)i * 2 * kPtKernels;
+            if (hipEventElapsedTime(&ms, m[2 * k], m[2 * k + 1]) != hipSuccess) { rc = RT_ERR_HIP; ctx->err = "HIP event timing failed"; }
+            kernel_ms[k] += ms / (float)iters;
+        }
+    for (auto& m : marks)
+        if (m) (void)hipEventDestroy(m);
+    return rc;
+}
+
 int rt_time_path_trace_kernels(rt_context* ctx, int iters, float* kernel_ms, int n) {
-    if (!ctx || !kernel_ms || iters < 1 || n < kPtKernels) return RT_ERR_ARG;
-    if (!ctx->inited) { ctx->err = "rt_time_path_trace_kernels before rt_init"; return RT_ERR_STATE; }
-    if (ctx->postStream) {  // kernels are timed serially on the context stream
+    if (ctx && ctx->inited && ctx->postStream) {  // kernels are timed serially on the context stream
         void* post = ctx->postStream;
         int rc = rt_set_post_stream(ctx, nullptr);
         if (rc == RT_OK) rc = rt_time_path_trace_kernels(ctx, iters, kernel_ms, n);
         const int rc2 = rt_set_post_stream(ctx, post);
         return rc != RT_OK ? rc : rc2;
     }
-    hipEvent_t marks[kPtKernels + 1] = {};
-    int rc = RT_OK;
-    for (auto& m : marks)
-        if (hipEventCreate(&m) != hipSuccess) { rc = RT_ERR_HIP; break; }
-    for (int k = 0; k < kPtKernels; ++k) kernel_ms[k] = 0.0f;
-    for (int i = 0; i < iters && rc == RT_OK; ++i) {
-        ctx->ptMarks = marks;
-        rc = rt_path_trace(ctx, 1 + i, 0);
-        ctx->ptMarks = nullptr;
-        if (rc == RT_OK && hipEventSynchronize(marks[kPtKernels]) != hipSuccess) rc = RT_ERR_HIP;
-        for (int k = 0; k < kPtKernels && rc == RT_OK; ++k) {
-            float ms = 0.0f;
-            if (hipEventElapsedTime(&ms, marks[k], marks[k + 1]) != hipSuccess) rc = RT_ERR_HIP;
-            kernel_ms[k] += ms / (float)iters;
-        }
-    }
-    for (auto& m : marks)
-        if (m) (void)hipEventDestroy(m);
-    if (rc == RT_ERR_HIP) ctx->err = "HIP event timing failed";
-    return rc;
+    return time_kernels(ctx, 1, iters, kernel_ms, n, false);
+}
+
+int rt_time_frame_kernels(rt_context* ctx, int first_frame, int iters, float* kernel_ms, int n) {
+    return time_kernels(ctx, first_frame, iters, kernel_ms, n, true);
 }
 
 size_t rt_array_bytes(const rt_context* ctx, int what) {

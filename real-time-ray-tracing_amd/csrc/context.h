@@ -130,6 +130,8 @@ struct rt_context {
     int screenW = 1920, screenH = 1080;
     int renderW = 1920, renderH = 1080;
     int histW = 1920, histH = 1080;   // historyRenderWidth / Height (kernel.cu:83-84): previous frame's size
+    int allocW = 1920, allocH = 1080; // render size every render-size buffer is allocated for (the max)
+    int allocStripRows = 1080;        // strip rows the path-trace workspace is allocated for
     bool fullFrame = true;            // no strip split: dynamic resolution may resize the frame
     bool useDynamicResolution = true;
     float targetFps = 60.0f;
@@ -166,6 +168,7 @@ struct rt_context {
     hipStream_t sideStream = nullptr;  // pipelining: LBVH build + camera rays of the next frame
     hipEvent_t ptDone[kGbSets] = {}, postDone[kGbSets] = {}, overlapEv = nullptr;
     hipStream_t gatherStream = nullptr;  // optional: the caller's G-buffer gathers (rt_set_gather_stream)
+    bool gatherOn = false;               // gatherStream is set (it may be the null stream)
     hipEvent_t gatherDone[kGbSets] = {};
     bool postGather = false;             // the pending denoise also waits for gatherDone[its set]
     hipEvent_t buildDone[2] = {}, bvhFree[2] = {}, camDone[kGbSets] = {}, restDone[kGbSets] = {};
@@ -231,6 +234,7 @@ int dalloc(rt_context* ctx, T** p, size_t bytes) {
 }
 int rt_frame_init(rt_context* ctx);  // frame.cpp: sky tables, textures, G-buffers
 int sync_streams(rt_context* ctx);   // frame.cpp: context, post and side streams
+extern "C" size_t rt_alloc_bytes(const rt_context* ctx, int name);  // frame.cpp: allocated size of a render buffer
 extern "C" void bvh_select(rt_context* ctx, int k);  // context.cpp: point the dTriPos.. views at bvh[k]
 extern "C" int wait_bvh(rt_context* ctx);  // context.cpp: context stream waits for the LBVH build
 std::string rt_data_dir();

@@ -632,14 +632,14 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
         int rc = issue_pending_post(ctx);
         if (rc != RT_OK) return rc;
         HIP_TRY(ctx, hipEventRecord(ctx->ptDone[fr.gbSet], ctx->stream));
-        ctx->postGather = ctx->gatherStream != nullptr;
+        ctx->postGather = ctx->gatherOn;
         if (ctx->postGather) HIP_TRY(ctx, hipEventRecord(ctx->gatherDone[fr.gbSet], ctx->gatherStream));
         ctx->postParams = p;
         ctx->postPendingSet = fr.gbSet;
         ctx->postPending = true;
         fr.setInFlight[fr.gbSet] = true;
     } else {
-        if (ctx->gatherStream) {
+        if (ctx->gatherOn) {
             HIP_TRY(ctx, hipEventRecord(ctx->gatherDone[0], ctx->gatherStream));
             HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->gatherDone[0], 0));
         }
@@ -691,7 +691,8 @@ int rt_set_gather_stream(rt_context* ctx, void* stream) {
     if (rc != RT_OK) return rc;
     for (int k = 0; k < kGbSets; ++k)
         if (!ctx->gatherDone[k]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->gatherDone[k], hipEventDisableTiming));
-    ctx->gatherStream = (hipStream_t)stream;
+    ctx->gatherOn = stream != RT_STREAM_OFF;  // NULL is the null stream, as in rt_set_stream
+    ctx->gatherStream = ctx->gatherOn ? (hipStream_t)stream : nullptr;
     return RT_OK;
 }
 
@@ -706,10 +707,12 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
         ctx->postStream = nullptr;
         return RT_OK;
     }
-    const size_t P = (size_t)ctx->renderW * ctx->renderH;
+    // sized for the largest frame: with dynamic resolution the current size may be smaller and
+    // grow back later
+    const size_t P = (size_t)ctx->allocW * ctx->allocH;
 #define ALLOC(p, bytes) if (!(p) && (rc = dalloc(ctx, &(p), (bytes))) != RT_OK) return rc
     for (int k = 1; k < kGbSets; ++k) {  // further G-buffer sets and camera-output slots
-        const size_t cap = fr.ws.cap, strip = (size_t)ctx->renderW * ctx->stripRows;
+        const size_t cap = fr.ws.cap, strip = (size_t)ctx->allocW * ctx->allocStripRows;
         ALLOC(fr.gColor[k], P * 8);
         ALLOC(fr.gNormal[k], P * 8);
         ALLOC(fr.gAlbedo[k], P * 8);
@@ -774,7 +777,7 @@ int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
     const int set = (name >> 8) & 3;  // RT_BUF_SET1 / RT_BUF_SET2
     name &= 0xFF;
     if (set >= kGbSets) { ctx->err = "rt_bind_buffer: no such G-buffer set"; return RT_ERR_ARG; }
-    const size_t need = rt_buffer_bytes(ctx, name);
+    const size_t need = rt_alloc_bytes(ctx, name);  // later frames may be larger than the current one
     if (need == 0 || bytes < need) { ctx->err = "rt_bind_buffer: unknown buffer or too small"; return RT_ERR_ARG; }
     if (((uintptr_t)device_ptr & 15u) != 0) { ctx->err = "rt_bind_buffer: pointer must be 16-byte aligned"; return RT_ERR_ARG; }
     int rc = sync_streams(ctx);
@@ -790,6 +793,17 @@ int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
     }
     if (set == fr.gbSet) select_gbuffers(fr);
     return RT_OK;
+}
+
+// bytes a render-size buffer has at the allocation (maximum) size
+size_t rt_alloc_bytes(const rt_context* ctx, int name) {
+    const size_t P = (size_t)ctx->allocW * ctx->allocH;
+    switch (name) {
+        case RT_BUF_RENDER_COLOR: case RT_BUF_NORMAL: case RT_BUF_ALBEDO: return P * 8;
+        case RT_BUF_DEPTH: return P * 2;
+        case RT_BUF_MOTION: return P * 4;
+        default: return 0;
+    }
 }
 
 size_t rt_buffer_bytes(const rt_context* ctx, int name) {

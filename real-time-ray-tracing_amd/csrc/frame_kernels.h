@@ -69,9 +69,15 @@ struct PtQueue {
 };
 
 // counters[] slots (zeroed before every path-trace launch sequence)
+// [12..21]: per-kernel traversal / shading work of detail launches (statsOut set), for the
+// per-kernel roofline (bench.py): node visits and triangle tests of the camera kernel, the
+// shade kernel's inline (glossy) traces and the two queue tracers; diffuse events of the shade
+// and resume<3> kernels
 enum PtCounter : int { kCntQ3 = 0, kCntQ4 = 1, kCntFetch3 = 2, kCntFetch4 = 3, kCntPending = 4, kCntResume3 = 5,
                        kCntResume4 = 6, kCntResolve = 7, kCntMaxIter3 = 8, kCntMaxIter4 = 9, kCntError = 10,
-                       kCntSurface = 11, kCntSlots = 12 };
+                       kCntSurface = 11, kCntVisCam = 12, kCntTstCam = 13, kCntVisShade = 14, kCntTstShade = 15,
+                       kCntVisQ3 = 16, kCntTstQ3 = 17, kCntVisQ4 = 18, kCntTstQ4 = 19, kCntDiffShade = 20,
+                       kCntDiffRes3 = 21, kCntSlots = 22 };
 constexpr int kWsCounterWords = 64 + 2 * 8 * 16;  // counters | fetch, zeroed together
 
 struct PtWorkspace {
@@ -196,8 +202,9 @@ struct PtLaunchHook {
 };
 // The camera kernel (writes the hit records, the surface list and the sky pixels' G-buffer) and
 // the rest (shade .. resolve) can go to different streams: the frame pipeline runs the camera
-// rays of frame f+1 beside the trace tails of frame f (frame.cpp).  marks: kPtKernels + 1 events,
-// [0..1] recorded by the camera launcher, [1..7] by the rest (rt_time_path_trace_kernels).
+// rays of frame f+1 beside the trace tails of frame f (frame.cpp).  marks: 2 * kPtKernels events,
+// marks[2k] / marks[2k + 1] recorded right before / after kernel k on the stream it runs on
+// (k = 0 by the camera launcher, 1..6 by the rest; rt_time_path_trace_kernels, rt_time_frame_kernels).
 extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks);
 extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
                                          const PtLaunchHook* hook);

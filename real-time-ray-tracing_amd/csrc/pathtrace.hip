@@ -331,6 +331,13 @@ RT_DEV uint2 pack_h4(float a, float b, float c, uint32_t d16) {
     return make_uint2((uint32_t)rt_f2h(a) | ((uint32_t)rt_f2h(b) << 16), (uint32_t)rt_f2h(c) | (d16 << 16));
 }
 
+// wave sum of a per-lane count into a counter: one atomic per wave (every lane of the wave calls)
+RT_DEV void wave_add(uint32_t v, uint32_t* dst) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (__lane_id() == 0 && v) atomicAdd(dst, v);
+}
+
 // wave-aggregated append: one atomic per wave, slots in lane order
 RT_DEV uint32_t wave_append(bool want, uint32_t* counter) {
     const unsigned long long m = __ballot(want);
@@ -444,7 +451,7 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
     bool anyHit = false;
     float4 rec = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float recErr = 0.0f;
-    uint32_t rays = 0;
+    uint32_t rays = 0, camV = 0, camT = 0;
 #pragma unroll 1
     for (int r = 0; r < rounds; ++r) {  // uniform trip count: every thread reaches the barriers
         const int s = r * nSW + sw;
@@ -465,6 +472,8 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
             if (P.statsOut) {
                 atomicAdd(&P.statsOut[p].y, st.visits);
                 atomicAdd(&P.statsOut[p].z, st.tests);
+                camV += st.visits;
+                camT += st.tests;
             }
             rec = make_float4(st.t, __uint_as_float((uint32_t)st.hitIdx), st.hitU, st.hitV);
             recErr = st.hitErrT;
@@ -518,6 +527,10 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
         if (P.raysOut) atomicAdd(&P.raysOut[p], rays);
         if (P.statsOut) atomicAdd(&P.statsOut[p].x, rays);
     }
+    if (P.statsOut) {
+        wave_add(camV, &P.ws.counters[kCntVisCam]);
+        wave_add(camT, &P.ws.counters[kCntTstCam]);
+    }
     const uint32_t slot = wave_append(sw == 0 && surface, &P.ws.counters[kCntSurface]);
     if (sw == 0 && active) {
         if (surface) {
@@ -566,7 +579,7 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
     const int rounds = ((int)P.spp + nSW - 1) / nSW;
     const SceneView sc = scene_of(P);
     const size_t plane = (size_t)P.rows * P.width;
-    uint32_t raysWg = 0;
+    uint32_t raysWg = 0, shV = 0, shT = 0, shD = 0;
 #pragma unroll 1
     for (uint32_t base = blockIdx.x * perWg; base < n; base += gridDim.x * perWg) {  // block-uniform
         const uint32_t i = base + (uint32_t)g * 64u + (uint32_t)lane;
@@ -689,8 +702,16 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
             if (c.visits) atomicAdd(&P.statsOut[p].y, c.visits);
             if (c.tests) atomicAdd(&P.statsOut[p].z, c.tests);
             if (c.diffuse) atomicAdd(&P.statsOut[p].w, c.diffuse);
+            shV += c.visits;
+            shT += c.tests;
+            shD += c.diffuse;
         }
         raysWg += c.rays;
+    }
+    if (P.statsOut) {
+        wave_add(shV, &P.ws.counters[kCntVisShade]);
+        wave_add(shT, &P.ws.counters[kCntTstShade]);
+        wave_add(shD, &P.ws.counters[kCntDiffShade]);
     }
     add_rays(P, wgRays, raysWg);
 }
@@ -710,7 +731,7 @@ __global__ __launch_bounds__(256) void k_pt_resume(PathTraceParams P) {
     const PtQueue& q = kStep == 3 ? P.ws.q3 : P.ws.q4;
     const uint32_t n = P.ws.counters[kStep == 3 ? kCntQ3 : kCntQ4];
     const SceneView sc = scene_of(P);
-    uint32_t rays = 0;
+    uint32_t rays = 0, rsD = 0;
 #pragma unroll 1
     for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {  // block-uniform
         const uint32_t i = base + (uint32_t)tid;
@@ -766,10 +787,12 @@ __global__ __launch_bounds__(256) void k_pt_resume(PathTraceParams P) {
             if (P.statsOut) {
                 if (c.rays) atomicAdd(&P.statsOut[p].x, c.rays);
                 if (c.diffuse) atomicAdd(&P.statsOut[p].w, c.diffuse);
+                rsD += c.diffuse;
             }
             rays += c.rays;
         }
     }
+    if (kStep == 3 && P.statsOut) wave_add(rsD, &P.ws.counters[kCntDiffRes3]);
     add_rays(P, wgRays, rays);
 }
 
@@ -802,7 +825,7 @@ extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t
     if ((size_t)p->rows * p->width >= (1u << 26) || (size_t)p->rows * p->width * p->spp > p->ws.cap)
         return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
-    if (e == hipSuccess && marks) e = hipEventRecord(marks[0], stream);
+    if (e == hipSuccess && marks) e = hipEventRecord(marks[0], stream);  // begin / end of kernel 0
     if (e != hipSuccess) return e;
     const int nSW = cam_sample_waves(p->spp);
     const int BW = nSW == 4 ? 8 : 16, BH = nSW == 1 ? 16 : 8;
@@ -817,25 +840,30 @@ extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t
 extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
                                          const PtLaunchHook* hook) {
     hipError_t e = hipSuccess;  // the counters were zeroed before the camera kernel (rtk_launch_pt_camera)
-    int k = 2;  // marks[2] = end of the shade kernel
-    auto mark = [&]() {
+    int k = 1;  // kernel 1 = shade; marks[2k] / marks[2k + 1] bracket kernel k on this stream
+    auto begin = [&]() { return marks ? hipEventRecord(marks[2 * k], stream) : hipSuccess; };
+    auto end = [&]() {
         if (hook && hook->fn) {
-            const hipError_t he = hook->fn(hook->arg, k - 1);
+            const hipError_t he = hook->fn(hook->arg, k);
             if (he != hipSuccess) return he;
         }
-        if (!marks) { ++k; return hipSuccess; }
-        return hipEventRecord(marks[k++], stream);
+        const hipError_t me = marks ? hipEventRecord(marks[2 * k + 1], stream) : hipSuccess;
+        ++k;
+        return me;
     };
+    if ((e = begin()) != hipSuccess) return e;
     if (p->ws.glossy) hipLaunchKernelGGL(k_pt_shade0<true>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
     else hipLaunchKernelGGL(k_pt_shade0<false>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
-    if ((e = mark()) != hipSuccess) return e;
-    if ((e = rtk_launch_trace_queue(p, 3, stream)) != hipSuccess || (e = mark()) != hipSuccess) return e;
+    if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
+    if ((e = rtk_launch_trace_queue(p, 3, stream)) != hipSuccess || (e = end()) != hipSuccess) return e;
+    if ((e = begin()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_pt_resume<3>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
-    if ((e = mark()) != hipSuccess) return e;
-    if ((e = rtk_launch_trace_queue(p, 4, stream)) != hipSuccess || (e = mark()) != hipSuccess) return e;
+    if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
+    if ((e = rtk_launch_trace_queue(p, 4, stream)) != hipSuccess || (e = end()) != hipSuccess) return e;
+    if ((e = begin()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_pt_resume<4>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
-    if ((e = mark()) != hipSuccess) return e;
+    if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_pt_resolve, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
-    if ((e = mark()) != hipSuccess) return e;
+    if ((e = end()) != hipSuccess) return e;
     return hipGetLastError();
 }

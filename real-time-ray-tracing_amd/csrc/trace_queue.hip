@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
     fetch_init(f, n, gridDim.x * wavesPerBlock, blockIdx.x * wavesPerBlock + (uint32_t)(tid >> 6));
 
     bool active = false, exhausted = false;
-    uint32_t idx = 0;
+    uint32_t idx = 0, accV = 0, accT = 0;
     TravRay r;
     TravState s;
     r.org = f3(0.0f);
@@ -130,9 +130,23 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
                     atomicAdd(&P.statsOut[p].y, s.visits);
                     atomicAdd(&P.statsOut[p].z, s.tests);
                     atomicMax(&P.ws.counters[kStep == 3 ? kCntMaxIter3 : kCntMaxIter4], s.iters);
+                    accV += s.visits;
+                    accT += s.tests;
                 }
                 active = false;
             }
+        }
+    }
+    if (P.statsOut) {  // every lane left the loop together (the wave-uniform break above)
+        uint32_t v = accV, t = accT;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            v += __shfl_xor(v, o);
+            t += __shfl_xor(t, o);
+        }
+        if (lane == 0) {
+            if (v) atomicAdd(&P.ws.counters[kStep == 3 ? kCntVisQ3 : kCntVisQ4], v);
+            if (t) atomicAdd(&P.ws.counters[kStep == 3 ? kCntTstQ3 : kCntTstQ4], t);
         }
     }
 }

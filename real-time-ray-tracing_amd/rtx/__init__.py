@@ -117,6 +117,7 @@ SIGNATURES = {
     "rt_sync": (C.c_int, [C.c_void_p]),
     "rt_time_stage": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float)]),
     "rt_time_path_trace_kernels": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float), C.c_int]),
+    "rt_time_frame_kernels": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float), C.c_int]),
     "rt_trace_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]),
     "rt_download": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     "rt_array_bytes": (C.c_size_t, [C.c_void_p, C.c_int]),
@@ -162,7 +163,7 @@ class RtError(RuntimeError):
 
 def write_config(path: str, width: int, height: int, dynamic: bool = False, chunk_dim: int = 1, spp: int = 1,
                  extra: str = "", max_size=(3840, 2160), camera_file: str | None = None, min_size=(640, 480),
-                 target_fps: float = 60.0) -> str:
+                 target_fps: float = 60.0, mesh_file: str | None = None) -> str:
     """Write a config.toml with the reference's three tables (resources/config.toml) + extensions."""
     with open(path, "w") as f:
         f.write("[resolution]\nwidth = %d\nheight = %d\n\n" % (width, height))
@@ -174,7 +175,10 @@ def write_config(path: str, width: int, height: int, dynamic: bool = False, chun
         f.write("[optimziation]\nuseDynamicResolution = %s\ntargetFps = %r\nmaxWidth = %d\nmaxHeight = %d\n"
                 "minWidth = %d\nminHeight = %d\n\n" % ("true" if dynamic else "false", float(target_fps), max_size[0],
                                                       max_size[1], min_size[0], min_size[1]))
-        f.write("[scene]\nchunkDim = %d\n\n[render]\nspp = %d\n" % (chunk_dim, spp))
+        f.write("[scene]\nchunkDim = %d\n" % chunk_dim)
+        if mesh_file:  # a meshProcessor .bin instead of the procedural terrain (init.cu:28-50)
+            f.write('meshFile = "%s"\n' % mesh_file)
+        f.write("\n[render]\nspp = %d\n" % spp)
         f.write(extra)
     return path
 
@@ -285,8 +289,10 @@ class RayTracer:
         self._check(self.lib.rt_set_post_stream(self.h, stream_ptr), "rt_set_post_stream")
 
     def set_gather_stream(self, stream: int | None):
-        """Stream the caller gathers G-buffers on; each later denoise also waits for it."""
-        self._check(self.lib.rt_set_gather_stream(self.h, stream or None), "rt_set_gather_stream")
+        """Stream the caller gathers G-buffers on; each later denoise also waits for it.
+        0 is the null stream (torch's default stream), as in set_stream; None turns it off."""
+        ptr = C.c_void_p(-2) if stream is None else C.c_void_p(stream)  # RT_STREAM_OFF
+        self._check(self.lib.rt_set_gather_stream(self.h, ptr), "rt_set_gather_stream")
 
     def bind_buffer(self, name: str, device_ptr: int, nbytes: int, gbuffer_set: int = 0):
         what = BUF[name] | (int(gbuffer_set) << 8)  # RT_BUF_SET1 / RT_BUF_SET2
@@ -315,6 +321,13 @@ class RayTracer:
         """Average ms of each path-trace kernel (HIP events on the context stream)."""
         ms = (C.c_float * len(self.PT_KERNELS))()
         self._check(self.lib.rt_time_path_trace_kernels(self.h, iters, ms, len(ms)), "rt_time_path_trace_kernels")
+        return dict(zip(self.PT_KERNELS, (float(v) for v in ms)))
+
+    def time_frame_kernels(self, first_frame: int, iters: int = 10):
+        """Average ms of each path-trace kernel over `iters` whole frames run as the caller runs
+        them (pipelined when a post stream is set); waits for the frames."""
+        ms = (C.c_float * len(self.PT_KERNELS))()
+        self._check(self.lib.rt_time_frame_kernels(self.h, first_frame, iters, ms, len(ms)), "rt_time_frame_kernels")
         return dict(zip(self.PT_KERNELS, (float(v) for v in ms)))
 
     # ---- camera file I/O and offscreen image dumps

@@ -47,6 +47,11 @@ def main():
             "chunk4": {"triCount": 958720, "batchCount": 937, "lastBatch": 256, "dupKeys": 0,
                        "blasDepthMinMedMax": [9, 16, 19], "tlasDepth": 16,
                        "quirkBoxMaxXY": [62.5, 13.0], "trueBoxMaxXY": [64.5, 14.0], "tlasCentresOutside": 28},
+            # the reference's own TraverseBvh on a 2-triangle BLAS + 1-leaf TLAS
+            # (the B == 1 special case, buildBVH.cuh:31-38) and its RayTriangleIntersect probe
+            # (geometry.cuh:474-495), as printed there
+            "traverse_probe": {"objectIdx": 1, "t": 2.99999952, "u": 0.6, "v": 0.2, "geometricNormal": [0, 0, 1]},
+            "triangle_probe": {"t": 1.0, "u": 0.6, "v": 0.2},
         },
         "oracle": {},
     }

@@ -1,0 +1,82 @@
+"""meshProcessor .bin scenes through the GPU renderer ([scene] meshFile, init.cu:28-50): the
+loader, the one-batch BLAS with padding triangles and the B == 1 TLAS special case
+(buildBVH.cuh:31-38), traversal, and a full frame, against the oracle fed by the test's own
+numpy reader of the same file (tests/scene_bin.py)."""
+import numpy as np
+import pytest
+
+from scene_bin import bin_bvh, probe_triangles, terrain_patch, write_bin
+
+pytestmark = pytest.mark.gpu
+
+
+def make(rtx, tmp_path, path, w=64, h=48, spp=1):
+    cfg = rtx.write_config(str(tmp_path / "b.toml"), w, h, spp=spp, mesh_file=path)
+    rt = rtx.RayTracer(w, h, cfg).init()
+    rt.set_delta_time(16.667)
+    return rt
+
+
+def gpu_nodes(rt, rtx, n):
+    return rt.download("NODES").view(rtx.NODE_DTYPE)[:n - 1], rt.download("TLAS_NODES").view(rtx.NODE_DTYPE)[:1]
+
+
+def test_probe_scene_traversal(rtx, oracle, tmp_path):
+    """SURVEY §8c's two-triangle probe (tests/test_oracle_pins.py) traced by the GPU queue tracer."""
+    for z0, z1, bits, obj in ((5.0, 3.0, 0x403FFFFE, 1), (5.0, 1.0, 0x3F800000, 1), (1.0, 5.0, None, -1)):
+        path = write_bin(str(tmp_path / ("p%g_%g.bin" % (z0, z1))), probe_triangles(z0, z1))
+        rt = make(rtx, tmp_path, path)
+        info = rt.info()
+        assert (info.triCount, info.triCountPadded, info.batchCount) == (2, 4, 1)
+        rt.build_bvh()
+        b, _, _, _ = bin_bvh(oracle, path)
+        g, gt = gpu_nodes(rt, rtx, 2)
+        assert g.tobytes() == b["nodes"][:1].tobytes()
+        assert gt.tobytes() == b["tlas_nodes"][:1].tobytes()
+        t, tri, u, v, ms = rt.trace_rays([[0.2, 0.2, 0.0]], [[0.0, 0.0, 1.0]])
+        assert int(tri[0]) == obj
+        if bits is not None:
+            assert t[0].view(np.uint32) == bits
+            assert (u[0], v[0]) == (np.float32(0.59999996), np.float32(0.19999999))
+        rt.cleanup()
+
+
+@pytest.mark.parametrize("ntri", [1012, 1010])
+def test_bin_terrain_frame(rtx, oracle, tmp_path, ntri):
+    """A 1,012 / 1,010-triangle height field (one batch; 1,010 adds two padding triangles):
+    LBVH, primary hits and a 2-frame path trace + denoise + post, bit-exact vs the oracle."""
+    tris = terrain_patch()[:ntri]
+    path = write_bin(str(tmp_path / "t.bin"), tris)
+    w, h = 96, 64
+    rt = make(rtx, tmp_path, path, w, h, spp=2)
+    b, _, _, n = bin_bvh(oracle, path)
+    assert rt.info().triCount == n == ntri and rt.info().batchCount == 1
+    cam = rtx.Camera()
+    cam.pos[:] = (5.5, 4.0, -3.0)
+    cam.yaw, cam.pitch, cam.focal, cam.aperture, cam.fovX = 0.0, -0.55, 5.0, 0.001, np.float32(90.0) * np.float32(0.01745329251)
+    rt.camera = cam
+    rt.build_bvh()
+    g, gt = gpu_nodes(rt, rtx, n)
+    assert g.tobytes() == b["nodes"][:n - 1].tobytes()
+    assert gt.tobytes() == b["tlas_nodes"][:1].tobytes()
+    assert np.array_equal(rt.download("MORTON", np.uint32)[:1024], b["morton"])
+    assert np.array_equal(rt.download("REORDER", np.uint32)[:1024], b["reorder"])
+    oc = oracle.default_camera(w, h)
+    oc.pos[:] = (5.5, 4.0, -3.0)
+    oc.pitch = -0.55
+    rt.trace_primary(1)
+    hits = rt.download("HITS", np.float32).reshape(-1, 4)
+    rays, _ = oracle.primary_rays(w, h, 1, cam=oc)
+    oh = oracle.intersect(b, rays)
+    assert 0.3 < oh["hit"].mean() and np.array_equal(hits[:, 0].view(np.uint32), oh["t"].view(np.uint32))
+    assert np.array_equal(hits[:, 1].view(np.int32), oh["objectIdx"])
+    s, tex = oracle.sky(), oracle.textures()
+    dn = oracle.Denoiser(w, h)
+    rgba = np.zeros((h, w, 4), np.uint8)
+    for f in (1, 2):
+        rt.draw(rgba)
+        gb = oracle.pathtrace(b, w, h, frame_num=f, spp=2, cam=oc, hist_cam=oc, sky_out=s, tex=tex)
+        o = dn.draw(gb, f, delta_time=16.667)
+        assert np.array_equal(rgba.reshape(-1, 4), o["rgba"]), f
+        assert np.array_equal(rt.get_buffer("RENDER_COLOR", (w * h, 4), np.uint16), o["color"]), f
+    rt.cleanup()

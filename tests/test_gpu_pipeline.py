@@ -54,3 +54,68 @@ def test_pipelined_frames_match_serial(rtx, tmp_path):
     _, imgs, _ = run(rtx, tmp_path, True, True)
     for f, (a, b) in enumerate(zip(ref_imgs, imgs)):
         assert np.array_equal(a, b), "frame %d" % (f + 1)
+
+
+def test_sync_on_null_stream_then_other_stream(rtx, oracle, tmp_path, default_scene):
+    """rt_sync with the renderer on the null stream (set_stream(0), torch's default stream) must
+    still issue the deferred denoise and wait for every renderer stream: G-buffers bound as torch
+    tensors and read on an unrelated stream right after it hold the finished frame."""
+    import torch
+
+    w, h = 160, 96
+    cfg = rtx.write_config(str(tmp_path / "ns.toml"), w, h)
+    rt = rtx.RayTracer(w, h, cfg).init()
+    rt.set_delta_time(16.667)
+    rt.set_stream(0)
+    post = post_stream()
+    rt.set_post_stream(post.cuda_stream)
+    bufs = [{k: torch.zeros(rt.buffer_bytes(k), dtype=torch.uint8, device="cuda:0") for k in ("NORMAL", "DEPTH")}
+            for _ in range(rtx.GBUFFER_SETS)]
+    for s, d in enumerate(bufs):
+        for k, t in d.items():
+            rt.bind_buffer(k, t.data_ptr(), t.numel(), gbuffer_set=s)
+    torch.cuda.synchronize()
+    other = torch.cuda.Stream(device=0)
+    s, tex = oracle.sky(), oracle.textures()
+    cam = oracle.default_camera(w, h)
+    for f in range(1, 4):
+        rt.build_bvh()
+        rt.path_trace(f)
+        rt.denoise_post(f)
+        rt.sync()
+        k = rt.info().gbufferSet
+        with torch.cuda.stream(other):
+            got = {n: t.to("cpu", non_blocking=True) for n, t in bufs[k].items()}
+        other.synchronize()
+        g = oracle.pathtrace(default_scene["bvh"], w, h, frame_num=f, cam=cam, sky_out=s, tex=tex)
+        assert np.array_equal(got["NORMAL"].numpy().view(np.uint16).reshape(-1, 4), g["normal"]), f
+        assert np.array_equal(got["DEPTH"].numpy().view(np.uint16), g["depth"]), f
+    rt.cleanup()
+
+
+def test_post_stream_after_dynamic_resolution_shrink(rtx, oracle, tmp_path, default_scene):
+    """rt_set_post_stream after dynamic resolution has shrunk the frame sizes its extra G-buffer
+    sets for the largest frame: the sequence grows back and stays bit-exact vs the oracle."""
+    maxw, maxh, ws, hs = 192, 108, 160, 90
+    cfg = rtx.write_config(str(tmp_path / "dr.toml"), ws, hs, dynamic=True, max_size=(maxw, maxh),
+                           min_size=(64, 36))
+    rt = rtx.RayTracer(ws, hs, cfg).init()
+    s, tex = oracle.sky(), oracle.textures()
+    dn = oracle.Denoiser(maxw, maxh, ws, hs)
+    rgba = np.zeros((hs, ws, 4), np.uint8)
+    w, h, cam = maxw, maxh, None
+    for f, dt in enumerate((16.667, 40.0, 16.667, 10.0, 5.0), start=1):
+        if f > 1:
+            w, h = oracle.dynamic_resolution(w, dt, 60.0, 64, maxw, maxh)
+        if f == 3:  # the frame is 128x72 now: pipelining turned on at the shrunk size
+            rt.set_post_stream(post_stream().cuda_stream)
+        rt.set_delta_time(dt)
+        rt.draw(rgba)
+        assert (rt.info().renderWidth, rt.info().renderHeight) == (w, h)
+        oc = oracle.default_camera(w, h)
+        gb = oracle.pathtrace(default_scene["bvh"], w, h, frame_num=f, cam=oc, hist_cam=cam or oc, sky_out=s, tex=tex)
+        o = dn.draw(gb, f, delta_time=dt, size=(w, h))
+        assert np.array_equal(rgba.reshape(-1, 4), o["rgba"]), f
+        cam = oc
+    assert (w, h) == (192, 108)  # grew back to the maximum
+    rt.cleanup()

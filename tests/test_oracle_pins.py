@@ -170,3 +170,53 @@ def test_dynamic_resolution_rule(oracle):
     assert oracle.dynamic_resolution(192, 40.0, 60.0, 64, 192, 108) == (128, 72)
     assert oracle.dynamic_resolution(1920, 1000.0, 60.0, 640, 3840, 2160) == (640, 360)   # clamped to minWidth
     assert oracle.dynamic_resolution(3840, 13.3, 60.0, 640, 3840, 2160) == (3840, 2160)   # 75-fps cap: grows, clamped
+
+
+def _probe_hit(oracle, tmp_path, z0, z1):
+    """closest hit of the ray (0.2, 0.2, 0) + t (0, 0, 1) on the two-triangle probe scene, built as
+    a meshProcessor .bin through the oracle's LBVH (1 BLAS batch of 2 + padding, the B == 1 TLAS)"""
+    from scene_bin import bin_bvh, probe_triangles, write_bin
+
+    path = write_bin(str(tmp_path / "probe.bin"), probe_triangles(z0, z1))
+    b, _, _, _ = bin_bvh(oracle, path)
+    assert b["batch_count"] == 1
+    tl = b["tlas_nodes"][0]  # buildBVH.cuh:31-38: {aabbs[0], AABB(0, 0)}, both children leaf 0
+    assert (tl["isLeftLeaf"], tl["isRightLeaf"], tl["idxLeft"], tl["idxRight"]) == (1, 1, 0, 0)
+    assert (tl["rmin"] == 0).all() and (tl["rmax"] == 0).all()
+    return oracle.intersect(b, np.array([[0.2, 0.2, 0.0, 0.0, 0.0, 1.0]], np.float32))[0]
+
+
+def test_traverse_probe_two_triangles(oracle, tmp_path):
+    """SURVEY.md §8c ran the reference's TraverseBvh on a hand-built 2-triangle BLAS under a
+    1-leaf TLAS and printed obj=1, t=2.99999952 (two ulps below 3: the watertight test's
+    T * (1/det) rounding), geometric normal (0,0,1), uv (0.6, 0.2).  The geometry was not recorded;
+    this reconstruction (unit right triangles in z = 5 and z = 3, the nearer one object 1, a +z
+    ray through (0.2, 0.2)) reproduces every printed value bit for bit (t) or to the printed digits."""
+    pin = PINS["traverse_probe"]
+    h = _probe_hit(oracle, tmp_path, 5.0, 3.0)
+    assert int(h["objectIdx"]) == pin["objectIdx"]
+    assert np.float32(h["t"]).view(np.uint32) == np.float32(pin["t"]).view(np.uint32) == 0x403FFFFE
+    assert round(float(h["u"]), 6) == pin["u"] and round(float(h["v"]), 6) == pin["v"]
+    # RaySceneIntersect flips the geometric normal (0,0,1) to face the +z ray (traverse.cuh:192-217)
+    assert list(np.abs(h["normal"])) == pin["geometricNormal"] and h["normal"][2] == -1.0
+
+
+def test_triangle_probe(oracle, tmp_path):
+    """RayTriangleIntersect -> t=1, u=0.6, v=0.2 (the same unit triangle at z = 1)."""
+    pin = PINS["triangle_probe"]
+    h = _probe_hit(oracle, tmp_path, 5.0, 1.0)
+    assert float(h["t"]) == pin["t"] and int(h["objectIdx"]) == 1
+    assert round(float(h["u"]), 6) == pin["u"] and round(float(h["v"]), 6) == pin["v"]
+
+
+def test_padding_triangles_displace_real_ones(oracle, tmp_path):
+    """the padding triangles (index 0 repeated up to a multiple of 4, init.cu:104-115)
+    are Morton-coded with the rest and only the first triCount sorted keys are built, so a padding
+    key can take a real triangle's place.  Two triangles at z = 1 and 5: both pads sit on vertex 0
+    (the box minimum, Morton 0) and sort first, so the tree holds the two pads and the ray misses."""
+    from scene_bin import bin_bvh, probe_triangles, write_bin
+
+    b, _, _, _ = bin_bvh(oracle, write_bin(str(tmp_path / "pad.bin"), probe_triangles(1.0, 5.0)))
+    assert list(b["reorder"][:2]) == [2, 3] and list(b["morton"][:2]) == [0, 0]
+    h = oracle.intersect(b, np.array([[0.2, 0.2, 0.0, 0.0, 0.0, 1.0]], np.float32))[0]
+    assert int(h["objectIdx"]) == -1

@@ -47,6 +47,17 @@ int rt_init(rt_context* ctx);
  * maxWidth x maxHeight. */
 int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out);
 
+/* RayTracer::draw(SurfObj* renderTarget), kernel.cu:259-398 (CopyToOutput kernel.cu:26-59 writes
+ * the caller's surface): one frame whose screen-size RGBA8 image is written straight into
+ * caller-owned DEVICE memory (row pitch in bytes, 0 = width * 4; 4-byte aligned).  flags 0: returns
+ * when the frame is complete, as the reference's draw does (it ends with a device sync).
+ * RT_DRAW_ASYNC: returns once the frame is enqueued; frames are pipelined (the denoise/post of
+ * frame f overlaps the trace of f+1 on an internal low-priority stream unless rt_set_post_stream
+ * named one) and each frame's target must stay valid until rt_sync (or a later synchronous
+ * call) has returned.  rt_download(RT_ARR_RGBA8) reads the last frame's target. */
+#define RT_DRAW_ASYNC 1
+int rt_draw_device(rt_context* ctx, void* rgba8_device, size_t pitch_bytes, int flags);
+
 /* RayTracer::cleanup + ~RayTracer, init.cu:601-663, kernel.cuh:443-446 */
 void rt_destroy(rt_context* ctx);
 
@@ -139,6 +150,18 @@ int rt_load_camera(rt_context* ctx, const char* path);
 #define RT_IMAGE_PPM_RGBA8 0
 #define RT_IMAGE_PFM_HDR 1
 int rt_save_image(rt_context* ctx, const char* path, int kind);
+
+/* Texture path, init.cu:524-580 + MipmapGen (mipgen.cu:121-182): a 16-bit texture of the atlas
+ * (MipmapTextureName, texture.h:5-12) — its level 0 as stbi_load_16 returns it, rows of
+ * width * channels ushorts — is copied to the device and its 11-level mip chain is generated there
+ * (2x2 mean in float, min 65535, truncated to ushort).  The atlas is 1024 x 1024: 4 channels for
+ * the albedo/AO and normal/roughness maps the diffuse shading samples, 1 for the height map.
+ * rt_init uploads a deterministic synthetic pair (the PNGs are missing from the reference tree).
+ * Synchronous. */
+#define RT_TEX_SOIL_ALBEDO_AO 0
+#define RT_TEX_SOIL_NORMAL_ROUGHNESS 1
+#define RT_TEX_SOIL_HEIGHT 2
+int rt_upload_texture(rt_context* ctx, int which, const uint16_t* texels, int width, int height, int channels);
 
 /* Determinism hooks the reference lacks: the frame counter is a function static
  * (kernel.cu:64) and AutoExposure reads wall-clock deltaTime (postprocessing.cu:46-51). */
@@ -311,8 +334,11 @@ enum rt_array_name {
     RT_ARR_PT_Q3_DIRS = 34,      /* float4[cap] direction xyz, flags bits ([0] of RT_ARR_PT_QUEUE are valid) */
     RT_ARR_PT_Q4_ORIGINS = 35,   /* float4[cap] step-4 queue, same layout ([1] valid) */
     RT_ARR_PT_Q4_DIRS = 36,
-    RT_ARR_PT_STATS = 31         /* uint32[W*H][4] rays, node visits, triangle tests, diffuse events
+    RT_ARR_PT_STATS = 31,        /* uint32[W*H][4] rays, node visits, triangle tests, diffuse events
                                     (rt_path_trace with_detail) */
+    RT_ARR_TEX_ALBEDO_AO = 37,   /* ushort4, 11-level mip chain of 1024^2 (levels concatenated, 1024 -> 1) */
+    RT_ARR_TEX_NORMAL_ROUGHNESS = 38, /* ushort4, same layout */
+    RT_ARR_TEX_HEIGHT = 39       /* ushort, same layout (zero unless uploaded) */
 };
 int rt_download(const rt_context* ctx, int what, void* dst, size_t bytes);
 

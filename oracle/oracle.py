@@ -228,6 +228,8 @@ def _bind_frame_api(L):
     L.orc_scan.restype = None
     L.orc_textures.argtypes = [C.c_void_p, C.c_void_p]
     L.orc_textures.restype = None
+    L.orc_mip_chain.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+    L.orc_mip_chain.restype = None
     L.orc_pathtrace.argtypes = [C.POINTER(Frame), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                 C.POINTER(GBuffer), C.c_int]
     L.orc_pathtrace.restype = None
@@ -295,6 +297,15 @@ def textures():
     n = np.zeros((TEX_TEXELS, 4), np.uint16)
     lib().orc_textures(a.ctypes.data, n.ctypes.data)
     return a, n
+
+
+def mip_chain(level0: np.ndarray) -> np.ndarray:
+    """MipmapGen chain (11 levels, 1024 -> 1, concatenated) of a 1024x1024 16-bit image (H, W[, C])."""
+    c = 1 if level0.ndim == 2 else level0.shape[2]
+    chain = np.zeros((TEX_TEXELS, c), np.uint16)
+    chain[:1024 * 1024] = np.asarray(level0, np.uint16).reshape(-1, c)
+    lib().orc_mip_chain(chain.ctypes.data, 1024, 11, c)
+    return chain
 
 
 def pathtrace(bvh: dict, width: int, height: int, frame_num: int = 1, spp: int = 1, cam: CameraIn | None = None,

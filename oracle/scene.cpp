@@ -29,11 +29,3 @@ extern "C" void orc_scene_copy(float* vertices, uint32_t* indices) {
     memcpy(vertices, g_mesh.vertices.data(), g_mesh.vertices.size() * 4);
     memcpy(indices, g_mesh.indices.data(), g_mesh.indices.size() * 4);
 }
-
-// Synthetic soil texture pair (input data; see scene_gen.h TexturePair).
-extern "C" void orc_textures(uint16_t* albedoAo, uint16_t* normalRough) {
-    rtscene::TexturePair t;
-    rtscene::make_textures(t);
-    memcpy(albedoAo, t.albedoAo.data(), t.albedoAo.size() * 2);
-    memcpy(normalRough, t.normalRough.data(), t.normalRough.size() * 2);
-}

@@ -1,0 +1,59 @@
+// ORACLE (test infrastructure only; see ocommon.h) — texture atlas mip chains.
+//
+// Restates MipmapGen (mipgen.cu:121-146) as GenerateMipmap runs it level by level
+// (mipgen.cu:148-178): output texel (x, y) = the 2x2 input texels (2x, 2x+1) x (2y, 2y+1) of the
+// level above, read with the surface's clamp boundary, converted to float, summed in order,
+// divided by 4.0f, fminf'd with 65535 and truncated to ushort (toType<ushort4, float4>).  The
+// synthetic soil pair's level 0 comes from the scene-input generator (scene_gen.cpp); the chain
+// above it is built here, independently of the renderer's device kernel (texture.hip).
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../real-time-ray-tracing_amd/csrc/scene_gen.h"
+
+namespace {
+
+void mip_chain(uint16_t* chain, int size, int levels, int C) {
+    size_t off = 0;
+    int w = size;
+    for (int l = 1; l < levels && w > 1; ++l) {
+        const int n = w / 2 > 1 ? w / 2 : 1;
+        const uint16_t* in = chain + off * C;
+        uint16_t* out = chain + (off + (size_t)w * w) * C;
+        for (int y = 0; y < n; ++y)
+            for (int x = 0; x < n; ++x) {
+                const int xs[2] = {2 * x < w - 1 ? 2 * x : w - 1, 2 * x + 1 < w - 1 ? 2 * x + 1 : w - 1};
+                const int ys[2] = {2 * y < w - 1 ? 2 * y : w - 1, 2 * y + 1 < w - 1 ? 2 * y + 1 : w - 1};
+                for (int k = 0; k < C; ++k) {
+                    const float v0 = in[((size_t)ys[0] * w + xs[0]) * C + k];
+                    const float v1 = in[((size_t)ys[0] * w + xs[1]) * C + k];
+                    const float v2 = in[((size_t)ys[1] * w + xs[0]) * C + k];
+                    const float v3 = in[((size_t)ys[1] * w + xs[1]) * C + k];
+                    float v = (((v0 + v1) + v2) + v3) / 4.0f;
+                    v = v < 65535.0f ? v : 65535.0f;  // fminf (no NaN can arise)
+                    out[((size_t)y * n + x) * C + k] = (uint16_t)v;
+                }
+            }
+        off += (size_t)w * w;
+        w = n;
+    }
+}
+
+}  // namespace
+
+// levels 1..levels-1 of a square chain (size x size at level 0, C channels) in place
+extern "C" void orc_mip_chain(uint16_t* chain, int size, int levels, int channels) {
+    mip_chain(chain, size, levels, channels);
+}
+
+// the synthetic soil pair (input level 0, scene_gen.h TexturePair) with its mip chains
+extern "C" void orc_textures(uint16_t* albedoAo, uint16_t* normalRough) {
+    rtscene::TexturePair t;
+    rtscene::make_textures(t);
+    memcpy(albedoAo, t.albedoAo.data(), t.albedoAo.size() * 2);
+    memcpy(normalRough, t.normalRough.data(), t.normalRough.size() * 2);
+    mip_chain(albedoAo, 1024, rtscene::TexturePair::kLevels, 4);
+    mip_chain(normalRough, 1024, rtscene::TexturePair::kLevels, 4);
+}

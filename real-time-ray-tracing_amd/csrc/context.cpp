@@ -377,6 +377,7 @@ void rt_destroy(rt_context* ctx) {
         for (hipEvent_t e : {ctx->ptDone[k], ctx->postDone[k], ctx->camDone[k], ctx->restDone[k], ctx->gatherDone[k]})
             if (e) (void)hipEventDestroy(e);
     if (ctx->sideStream) (void)hipStreamDestroy(ctx->sideStream);
+    if (ctx->ownPostStream) (void)hipStreamDestroy(ctx->ownPostStream);
     for (void* p : ctx->allocations) (void)hipFree(p);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -655,6 +656,8 @@ size_t rt_array_bytes(const rt_context* ctx, int what) {
         }
         case RT_ARR_RGBA8: return (size_t)ctx->screenW * ctx->screenH * 4;
         case RT_ARR_PT_STATS: return P * 16;
+        case RT_ARR_TEX_ALBEDO_AO: case RT_ARR_TEX_NORMAL_ROUGHNESS: return (size_t)kTexTexels * 8;
+        case RT_ARR_TEX_HEIGHT: return (size_t)kTexTexels * 2;
         case RT_ARR_PT_QUEUE: return 64 * 4;
         case RT_ARR_PT_Q3_ORIGINS:
         case RT_ARR_PT_Q3_DIRS:
@@ -699,8 +702,13 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
         case RT_ARR_COLOR4: src = ctx->fr.c4; break;
         case RT_ARR_COLOR16: src = ctx->fr.c16; break;
         case RT_ARR_COLOR64: src = ctx->fr.c64; break;
-        case RT_ARR_RGBA8: src = ctx->fr.rgba; break;
+        case RT_ARR_RGBA8:  // the last frame's output, wherever it was drawn (rt_draw_device)
+            if (bytes < rt_array_bytes(ctx, what)) { ctx->err = "destination too small"; return RT_ERR_ARG; }
+            return copy_rgba_out(ctx, dst);
         case RT_ARR_PT_STATS: src = ctx->fr.ptStats; break;
+        case RT_ARR_TEX_ALBEDO_AO: src = ctx->fr.texAlbedo; break;
+        case RT_ARR_TEX_NORMAL_ROUGHNESS: src = ctx->fr.texNormal; break;
+        case RT_ARR_TEX_HEIGHT: src = ctx->fr.texHeight; break;
         case RT_ARR_PT_QUEUE: src = ctx->fr.lastCounters ? ctx->fr.lastCounters : ctx->fr.ws.counters; break;
         case RT_ARR_PT_Q3_ORIGINS: src = ctx->fr.ws.q3.rayO; break;
         case RT_ARR_PT_Q3_DIRS: src = ctx->fr.ws.q3.rayD; break;

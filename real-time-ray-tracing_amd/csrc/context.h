@@ -61,6 +61,7 @@ struct FrameResources {
     // soil textures (init.cu:524-577)
     uint2* texAlbedo = nullptr;
     uint2* texNormal = nullptr;
+    uint16_t* texHeight = nullptr;  // SoilHeight (ushort chain; feeds only the reference's disabled displacement)
     // path-trace G-buffer (pathtrace.cuh:11-128): the set the last path trace wrote.  With a
     // post stream (rt_set_post_stream) the path tracer cycles through kGbSets sets, so the
     // camera rays of frame f+1 and the rest of frame f are traced while frame f-1 is denoised;
@@ -109,6 +110,10 @@ struct FrameResources {
     uint2* scaledA = nullptr;
     uint2* scaledB = nullptr;
     uint32_t* rgba = nullptr;
+    uint32_t* outRgba = nullptr;   // where the last rt_denoise_post wrote RGBA8 (rgba or a draw target)
+    uint32_t outPitch = 0;         // its row pitch in pixels
+    uint32_t* drawTarget = nullptr;  // set by rt_draw_device for the frame it enqueues
+    uint32_t drawPitch = 0;
     float4* hdr = nullptr;
     uint2* renderColor = nullptr;  // buffer that currently holds RenderColorBuffer
     uint2* scaledColor = nullptr;  // buffer that currently holds ScaledColorBuffer
@@ -165,6 +170,7 @@ struct rt_context {
     hipStream_t ownStream = nullptr;   // the one rt_init created (destroyed by rt_destroy)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t postStream = nullptr;  // optional: denoise + post run here (rt_set_post_stream)
+    hipStream_t ownPostStream = nullptr;  // created by an asynchronous rt_draw_device (destroyed by rt_destroy)
     hipStream_t sideStream = nullptr;  // pipelining: LBVH build + camera rays of the next frame
     hipEvent_t ptDone[kGbSets] = {}, postDone[kGbSets] = {}, overlapEv = nullptr;
     hipStream_t gatherStream = nullptr;  // optional: the caller's G-buffer gathers (rt_set_gather_stream)
@@ -234,6 +240,7 @@ int dalloc(rt_context* ctx, T** p, size_t bytes) {
 }
 int rt_frame_init(rt_context* ctx);  // frame.cpp: sky tables, textures, G-buffers
 int sync_streams(rt_context* ctx);   // frame.cpp: context, post and side streams
+extern "C" int copy_rgba_out(rt_context* ctx, void* dst);  // frame.cpp: the last frame's RGBA8 to host memory
 extern "C" size_t rt_alloc_bytes(const rt_context* ctx, int name);  // frame.cpp: allocated size of a render buffer
 extern "C" void bvh_select(rt_context* ctx, int k);  // context.cpp: point the dTriPos.. views at bvh[k]
 extern "C" int wait_bvh(rt_context* ctx);  // context.cpp: context stream waits for the LBVH build

@@ -933,7 +933,7 @@ __global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const u
                             bluenoise(P.bluenoise, x, y, s, 2) / 256);
     const float hi = 1.0f - 1.1920928955078125e-07f;
     c = clamp3(c, f3(0.0f), f3(hi));
-    P.rgba[p] = (uint32_t)(uint8_t)(c.x * 256) | ((uint32_t)(uint8_t)(c.y * 256) << 8) |
+    P.rgba[(size_t)y * P.rgbaPitch + x] = (uint32_t)(uint8_t)(c.x * 256) | ((uint32_t)(uint8_t)(c.y * 256) << 8) |
                 ((uint32_t)(uint8_t)(c.z * 256) << 16) | (1u << 24);
 }
 

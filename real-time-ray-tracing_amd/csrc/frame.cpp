@@ -308,6 +308,8 @@ int rt_frame_init(rt_context* ctx) {
     ALLOC(fr.sunTree, (size_t)kSunTreeNodes * 4);
     ALLOC(fr.texAlbedo, (size_t)kTexTexels * 8);
     ALLOC(fr.texNormal, (size_t)kTexTexels * 8);
+    ALLOC(fr.texHeight, (size_t)kTexTexels * 2);
+    HIP_TRY(ctx, hipMemset(fr.texHeight, 0, (size_t)kTexTexels * 2));
     const size_t P = (size_t)ctx->renderW * ctx->renderH;
     ALLOC(fr.color, P * 8);
     ALLOC(fr.normal, P * 8);
@@ -373,6 +375,8 @@ int rt_frame_init(rt_context* ctx) {
     ALLOC(fr.scaledA, Ps * 8);
     ALLOC(fr.scaledB, Ps * 8);
     ALLOC(fr.rgba, Ps * 4);
+    fr.outRgba = fr.rgba;
+    fr.outPitch = (uint32_t)ctx->screenW;
     ALLOC(fr.hdr, P * 16);
 #undef ALLOC
     HIP_TRY(ctx, hipMemcpy(fr.solar, g_tables.solar.data(), 1800 * 4, hipMemcpyHostToDevice));
@@ -382,13 +386,16 @@ int rt_frame_init(rt_context* ctx) {
     memcpy(cie.data() + 10, g_tables.cieY.data(), 40);
     memcpy(cie.data() + 20, g_tables.cieZ.data(), 40);
     HIP_TRY(ctx, hipMemcpy(fr.cie, cie.data(), 30 * 4, hipMemcpyHostToDevice));
-    // soil texture pair (synthetic stand-in for the missing blobs, scene_gen.h)
+    // soil texture pair (synthetic stand-in for the missing blobs, scene_gen.h): level 0 uploaded,
+    // the mip chain built by MipmapGen on the device, as init.cu:524-580 does for the PNGs
     {
         rtscene::TexturePair t;
         rtscene::make_textures(t);
         if (t.albedoAo.size() != (size_t)kTexTexels * 4) { ctx->err = "texture chain size mismatch"; return RT_ERR_STATE; }
-        HIP_TRY(ctx, hipMemcpy(fr.texAlbedo, t.albedoAo.data(), (size_t)kTexTexels * 8, hipMemcpyHostToDevice));
-        HIP_TRY(ctx, hipMemcpy(fr.texNormal, t.normalRough.data(), (size_t)kTexTexels * 8, hipMemcpyHostToDevice));
+        int rc2;
+        if ((rc2 = rt_upload_texture(ctx, RT_TEX_SOIL_ALBEDO_AO, t.albedoAo.data(), kTexSize, kTexSize, 4)) != RT_OK ||
+            (rc2 = rt_upload_texture(ctx, RT_TEX_SOIL_NORMAL_ROUGHNESS, t.normalRough.data(), kTexSize, kTexSize, 4)) != RT_OK)
+            return rc2;
     }
     HIP_TRY(ctx, hipMemset(fr.color, 0, P * 8));
     HIP_TRY(ctx, hipMemset(fr.normal, 0, P * 8));
@@ -413,6 +420,35 @@ int rt_frame_init(rt_context* ctx) {
 }
 
 extern "C" {
+
+// init.cu:524-580 for one texture of the atlas: its 16-bit level 0 (stbi_load_16 output, rows of
+// width * channels ushorts) to the device, then GenerateMipmap (mipgen.cu:148-178) on the device
+int rt_upload_texture(rt_context* ctx, int which, const uint16_t* texels, int width, int height, int channels) {
+    if (!ctx || !texels) return RT_ERR_ARG;
+    FrameResources& fr = ctx->fr;
+    if (!fr.texAlbedo) { ctx->err = "rt_upload_texture before rt_init"; return RT_ERR_STATE; }
+    uint16_t* chain = nullptr;
+    int want = 4;
+    switch (which) {
+        case RT_TEX_SOIL_ALBEDO_AO: chain = (uint16_t*)fr.texAlbedo; break;
+        case RT_TEX_SOIL_NORMAL_ROUGHNESS: chain = (uint16_t*)fr.texNormal; break;
+        case RT_TEX_SOIL_HEIGHT: chain = fr.texHeight; want = 1; break;
+        default: ctx->err = "rt_upload_texture: unknown texture"; return RT_ERR_ARG;
+    }
+    // the atlas is BUFFER_2D_1024x1024 with 11 levels (init.cu:526-528, texture.h:14-17), asserted there
+    if (width != kTexSize || height != kTexSize || channels != want) {
+        ctx->err = "rt_upload_texture: the soil textures are 1024 x 1024, 4 channels (height: 1)";
+        return RT_ERR_ARG;
+    }
+    if (ctx->inited) {  // frames in flight may be sampling the old chain
+        const int rc = sync_streams(ctx);
+        if (rc != RT_OK) return rc;
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(chain, texels, (size_t)width * height * channels * 2, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, rtk_launch_mipgen(chain, kTexSize, kTexLevels, channels, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
 
 int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     if (!ctx || frame_num < 1) return RT_ERR_ARG;
@@ -588,7 +624,10 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.exposure = fr.exposure;
     p.scaledA = fr.scaledA;
     p.scaledB = fr.scaledB;
-    p.rgba = fr.rgba;
+    p.rgba = fr.drawTarget ? fr.drawTarget : fr.rgba;  // rt_draw_device: the caller's device target
+    p.rgbaPitch = fr.drawTarget ? fr.drawPitch : (uint32_t)ctx->screenW;
+    fr.outRgba = p.rgba;
+    fr.outPitch = p.rgbaPitch;
     p.bluenoise = ctx->dBlueNoise;
     p.hdrOut = with_hdr ? fr.hdr : nullptr;
     p.bloom = ps.enablePostProcess && ps.enableBloomEffect;
@@ -653,10 +692,21 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     return RT_OK;
 }
 
-// RayTracer::draw (kernel.cu:259-398): BVH rebuild, path trace, denoise, post, output
-int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
-    if (!ctx) return RT_ERR_ARG;
-    if (!ctx->inited) { ctx->err = "rt_draw before rt_init"; return RT_ERR_STATE; }
+// the last frame's RGBA8 (screen size) into tightly packed host memory; waits for the frame
+int copy_rgba_out(rt_context* ctx, void* dst) {
+    if (int rc = sync_streams(ctx)) return rc;
+    const FrameResources& fr = ctx->fr;
+    const size_t row = (size_t)ctx->screenW * 4;
+    HIP_TRY(ctx, hipMemcpy2D(dst, row, fr.outRgba, (size_t)fr.outPitch * 4, row, (size_t)ctx->screenH,
+                             hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+namespace {
+// UpdateFrame (kernel.cu:61-137) + BuildBvhLevel1/2 + PathTrace + TemporalSpatialDenoising +
+// PostProcessing + CopyToOutput of one frame, enqueued (draw, kernel.cu:259-398); the RGBA8 image
+// goes to `target` (pitch in pixels) or, when NULL, to the context's own buffer
+int enqueue_frame(rt_context* ctx, uint32_t* target, uint32_t pitch, bool hdr) {
     const int frame = ctx->nextFrame++;
     int rc;
     ctx->fr.drawDt = -1.0f;
@@ -666,12 +716,52 @@ int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
     ctx->fr.drawDt = dt;
     if ((rc = rt_build_bvh(ctx)) != RT_OK) return rc;
     if ((rc = rt_path_trace(ctx, frame, 0)) != RT_OK) return rc;
-    if ((rc = rt_denoise_post(ctx, frame, hdr_out != nullptr)) != RT_OK) return rc;
+    ctx->fr.drawTarget = target;
+    ctx->fr.drawPitch = pitch;
+    rc = rt_denoise_post(ctx, frame, hdr ? 1 : 0);
+    ctx->fr.drawTarget = nullptr;
+    return rc;
+}
+}  // namespace
+
+// RayTracer::draw (kernel.cu:259-398) with host outputs: BVH rebuild, path trace, denoise, post,
+// output, then the copies to the caller's host buffers
+int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
+    if (!ctx) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_draw before rt_init"; return RT_ERR_STATE; }
+    int rc;
+    if ((rc = enqueue_frame(ctx, nullptr, 0, hdr_out != nullptr)) != RT_OK) return rc;
     if ((rc = sync_streams(ctx)) != RT_OK) return rc;
-    if (rgba8_out)
-        HIP_TRY(ctx, hipMemcpy(rgba8_out, ctx->fr.rgba, (size_t)ctx->screenW * ctx->screenH * 4, hipMemcpyDeviceToHost));
+    if (rgba8_out && (rc = copy_rgba_out(ctx, rgba8_out)) != RT_OK) return rc;
     if (hdr_out)
         HIP_TRY(ctx, hipMemcpy(hdr_out, ctx->fr.hdr, (size_t)ctx->renderW * ctx->renderH * 16, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+// RayTracer::draw(SurfObj* renderTarget) (kernel.cu:259, CopyToOutput kernel.cu:26-59): the frame's
+// RGBA8 image is written straight into caller-owned device memory.  RT_DRAW_ASYNC returns once the
+// frame is enqueued and runs the frame pipeline (an internal post stream unless the caller set one).
+int rt_draw_device(rt_context* ctx, void* rgba8_device, size_t pitch_bytes, int flags) {
+    if (!ctx || !rgba8_device) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_draw_device before rt_init"; return RT_ERR_STATE; }
+    const size_t row = (size_t)ctx->screenW * 4;
+    if (pitch_bytes == 0) pitch_bytes = row;
+    if (pitch_bytes < row || pitch_bytes % 4 != 0 || ((uintptr_t)rgba8_device & 3u) != 0) {
+        ctx->err = "rt_draw_device: pitch must be >= screen width * 4 and a multiple of 4, target 4-byte aligned";
+        return RT_ERR_ARG;
+    }
+    if ((flags & ~RT_DRAW_ASYNC) != 0) { ctx->err = "rt_draw_device: unknown flags"; return RT_ERR_ARG; }
+    int rc;
+    if ((flags & RT_DRAW_ASYNC) && !ctx->postStream) {  // pipelined frames on an internal low-priority stream
+        if (!ctx->ownPostStream) {
+            int least = 0, greatest = 0;
+            HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+            HIP_TRY(ctx, hipStreamCreateWithPriority(&ctx->ownPostStream, hipStreamNonBlocking, least));
+        }
+        if ((rc = rt_set_post_stream(ctx, ctx->ownPostStream)) != RT_OK) return rc;
+    }
+    if ((rc = enqueue_frame(ctx, (uint32_t*)rgba8_device, (uint32_t)(pitch_bytes / 4), false)) != RT_OK) return rc;
+    if (!(flags & RT_DRAW_ASYNC)) return sync_streams(ctx);  // draw ends with a device sync (kernel.cu:393-397)
     return RT_OK;
 }
 
@@ -929,7 +1019,7 @@ extern "C" int rt_save_image(rt_context* ctx, const char* path, int kind) {
     if (kind == RT_IMAGE_PPM_RGBA8) {
         const size_t n = (size_t)ctx->screenW * ctx->screenH;
         std::vector<uint8_t> rgba(n * 4), rgb(n * 3);
-        HIP_TRY(ctx, hipMemcpy(rgba.data(), ctx->fr.rgba, n * 4, hipMemcpyDeviceToHost));
+        if (int rc = copy_rgba_out(ctx, rgba.data())) return rc;
         for (size_t i = 0; i < n; ++i) memcpy(&rgb[3 * i], &rgba[4 * i], 3);
         f << "P6\n" << ctx->screenW << " " << ctx->screenH << "\n255\n";
         f.write(reinterpret_cast<const char*>(rgb.data()), (std::streamsize)rgb.size());

@@ -182,7 +182,8 @@ struct DenoisePostParams {
     float* exposure;            // [4], persistent
     uint2* scaledA;             // screen-size pair
     uint2* scaledB;
-    uint32_t* rgba;             // screen-size RGBA8
+    uint32_t* rgba;             // screen-size RGBA8 (the context's own buffer or a caller's device target)
+    uint32_t rgbaPitch;         // row pitch of rgba in pixels (>= Ws)
     const uint8_t* bluenoise;
     float4* hdrOut;             // optional render-size float4 copy of the denoised HDR colour
     uint2* finalColor;          // out: buffer holding RenderColorBuffer after denoising
@@ -192,6 +193,8 @@ struct DenoisePostParams {
 extern "C" hipError_t rtk_denoise_post(DenoisePostParams* p, hipStream_t stream);
 
 extern "C" hipError_t rtk_launch_sky(const SkyGenParams* p, hipStream_t stream);
+// MipmapGen (texture.hip): levels 1.. of a square 16-bit chain whose level 0 is in place
+extern "C" hipError_t rtk_launch_mipgen(uint16_t* chain, int size, int levels, int channels, hipStream_t stream);
 extern "C" hipError_t rtk_launch_scan(const float* in, float* out, float* sums, int size, int blockSize,
                                       hipStream_t stream);
 // kernels of one path-trace launch: camera, shade, trace<3>, resume<3>, trace<4>, resume<4>, resolve

@@ -416,24 +416,9 @@ void make_textures(TexturePair& t) {
             t.normalRough[p + 2] = 65535;
             t.normalRough[p + 3] = to16(0.4 + 0.4 * unit(hash3(x >> 4, y >> 4, 53u)));
         }
-    for (int l = 1; l < TexturePair::kLevels; ++l) {
-        const int n = t.size[l], m = t.size[l - 1];
-        for (std::vector<uint16_t>* tex : {&t.albedoAo, &t.normalRough}) {
-            uint16_t* dst = tex->data() + t.offset[l] * 4;
-            const uint16_t* src = tex->data() + t.offset[l - 1] * 4;
-            for (int y = 0; y < n; ++y)
-                for (int x = 0; x < n; ++x)
-                    for (int c = 0; c < 4; ++c) {
-                        const float v0 = src[((size_t)(2 * y) * m + 2 * x) * 4 + c];
-                        const float v1 = src[((size_t)(2 * y) * m + 2 * x + 1) * 4 + c];
-                        const float v2 = src[((size_t)(2 * y + 1) * m + 2 * x) * 4 + c];
-                        const float v3 = src[((size_t)(2 * y + 1) * m + 2 * x + 1) * 4 + c];
-                        float v = (v0 + v1 + v2 + v3) / 4.0f;
-                        v = v < 65535.0f ? v : 65535.0f;
-                        dst[((size_t)y * n + x) * 4 + c] = (uint16_t)v;
-                    }
-        }
-    }
+    // levels 1..10 are left to MipmapGen: the renderer's device kernel (texture.hip) and the
+    // oracle's own restatement (oracle/texture.cpp) each build them from this level 0
+
 }
 
 }  // namespace rtscene

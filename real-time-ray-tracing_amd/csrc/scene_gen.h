@@ -30,8 +30,9 @@ bool generate(int chunkDim, const std::vector<std::vector<float>>& tiles, SceneM
 
 // Synthetic stand-in for the soil texture pair the reference loads but does not ship
 // (init.cu:524-549, .MISSING_LARGE_BLOBS): SoilAlbedoAo and SoilNormalRoughness, 1024^2
-// ushort4, with the reference's 11-level mip chain (MipmapGen, mipgen.cu:144-163:
-// mean of 4 texels in float, min 65535, truncated to ushort).  Deterministic integer hash.
+// ushort4, laid out as the reference's 11-level mip chain; make_textures fills level 0 only
+// (deterministic integer hash): the mips are MipmapGen's (mipgen.cu:121-182), built on the device
+// by the renderer (texture.hip) and restated by the oracle (oracle/texture.cpp).
 struct TexturePair {
     static constexpr int kLevels = 11;
     int size[kLevels];                 // 1024 >> level

@@ -26,7 +26,8 @@ ARR = dict(VERTICES=0, INDICES=1, NORMALS=2, TRI_POS=3, AABBS=4, MORTON=5, REORD
            HIT_NORMALS=15, HIT_FAKE_NORMALS=16, HIT_STATS=17, TRI_NRM=18, RAYS=19, SKY_PDF=20, SKY_CDF=21,
            SUN_PDF=22, SUN_CDF=23, SUN_DIR=24, HISTOGRAM=25, EXPOSURE=26, COLOR4=27, COLOR16=28, COLOR64=29,
            RGBA8=30, PT_STATS=31, PT_QUEUE=32, PT_Q3_ORIGINS=33, PT_Q3_DIRS=34,
-           PT_Q4_ORIGINS=35, PT_Q4_DIRS=36)
+           PT_Q4_ORIGINS=35, PT_Q4_DIRS=36, TEX_ALBEDO_AO=37, TEX_NORMAL_ROUGHNESS=38, TEX_HEIGHT=39)
+TEX = dict(SOIL_ALBEDO_AO=0, SOIL_NORMAL_ROUGHNESS=1, SOIL_HEIGHT=2)  # MipmapTextureName (texture.h:5-12)
 # rt_buffer_name (Buffer2DName, kernel.cuh:286-315)
 BUF = dict(RENDER_COLOR=0, ACCUMULATION=1, HISTORY_COLOR=2, SCALED_COLOR=3, NORMAL=10, DEPTH=11, HISTORY_DEPTH=12,
            MOTION=13, NOISE_LEVEL=14, NOISE_LEVEL16=15, SKY=16, SUN=17, ALBEDO=18)
@@ -89,6 +90,7 @@ SIGNATURES = {
     "rt_create": (C.c_int, [C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_void_p)]),
     "rt_init": (C.c_int, [C.c_void_p]),
     "rt_draw": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_draw_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),
     "rt_destroy": (None, [C.c_void_p]),
     "rt_last_error": (C.c_char_p, [C.c_void_p]),
     "rt_get_params": (C.c_int, [C.c_void_p, C.POINTER(Params)]),
@@ -124,8 +126,10 @@ SIGNATURES = {
     "rt_save_camera": (C.c_int, [C.c_void_p, C.c_char_p]),
     "rt_load_camera": (C.c_int, [C.c_void_p, C.c_char_p]),
     "rt_save_image": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
+    "rt_upload_texture": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]),
 }
 IMAGE_PPM_RGBA8, IMAGE_PFM_HDR = 0, 1
+DRAW_ASYNC = 1  # rt_draw_device flag
 BUF_SET1, BUF_SET2 = 0x100, 0x200  # rt_bind_buffer: further G-buffer sets (frame pipelining)
 GBUFFER_SETS = 3  # G-buffer sets a pipelined context cycles through (rt_set_post_stream)
 
@@ -205,6 +209,12 @@ class RayTracer:
 
     def draw(self, rgba8: np.ndarray | None = None, hdr: np.ndarray | None = None):
         self._check(self.lib.rt_draw(self.h, _ptr(rgba8), _ptr(hdr)), "rt_draw")
+
+    def draw_device(self, device_ptr: int, pitch_bytes: int = 0, asynchronous: bool = False):
+        """draw(SurfObj*): the RGBA8 frame into caller-owned device memory (e.g. a torch uint8
+        tensor's data_ptr()); asynchronous=True enqueues the frame and pipelines frames."""
+        self._check(self.lib.rt_draw_device(self.h, device_ptr, pitch_bytes, DRAW_ASYNC if asynchronous else 0),
+                    "rt_draw_device")
 
     def cleanup(self):
         if getattr(self, "h", None):
@@ -339,6 +349,13 @@ class RayTracer:
 
     def save_image(self, path: str, kind: int = IMAGE_PPM_RGBA8):
         self._check(self.lib.rt_save_image(self.h, path.encode(), kind), "rt_save_image")
+
+    def upload_texture(self, name: str, texels: np.ndarray):
+        """init.cu:524-580: a 16-bit (H, W, C) level-0 image into the atlas; mips built on the device."""
+        t = np.ascontiguousarray(texels, np.uint16)
+        h, w = t.shape[:2]
+        c = 1 if t.ndim == 2 else t.shape[2]
+        self._check(self.lib.rt_upload_texture(self.h, TEX[name], t.ctypes.data, w, h, c), "rt_upload_texture")
 
     # ---- downloads
     def download(self, name: str, dtype=np.uint8) -> np.ndarray:

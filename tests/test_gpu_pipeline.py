@@ -119,3 +119,34 @@ def test_post_stream_after_dynamic_resolution_shrink(rtx, oracle, tmp_path, defa
         cam = oc
     assert (w, h) == (192, 108)  # grew back to the maximum
     rt.cleanup()
+
+
+def test_draw_device_target_sync_and_async(rtx, oracle, tmp_path, default_scene):
+    """draw(SurfObj*) (kernel.cu:259, CopyToOutput kernel.cu:26-59): the RGBA8 frame written into a
+    caller-owned device buffer with a row pitch, synchronously and asynchronously (pipelined, one
+    target per frame), each frame bit-exact vs the oracle; rt_download(RGBA8) reads the last target."""
+    import torch
+
+    w, h = 160, 96
+    pitch = (w + 16) * 4  # padded rows: the pad bytes must stay untouched
+    s, tex = oracle.sky(), oracle.textures()
+    cam = oracle.default_camera(w, h)
+    for asynchronous in (False, True):
+        cfg = rtx.write_config(str(tmp_path / ("dd%d.toml" % asynchronous)), w, h, spp=2)
+        rt = rtx.RayTracer(w, h, cfg).init()
+        rt.set_delta_time(16.667)
+        dn = oracle.Denoiser(w, h)
+        targets = [torch.full((h * pitch,), 7, dtype=torch.uint8, device="cuda:0") for _ in range(4)]
+        torch.cuda.synchronize()
+        for f, t in enumerate(targets, start=1):
+            rt.draw_device(t.data_ptr(), pitch, asynchronous=asynchronous)
+        rt.sync()
+        last = rt.download("RGBA8", np.uint8).reshape(-1, 4)
+        for f, t in enumerate(targets, start=1):
+            g = oracle.pathtrace(default_scene["bvh"], w, h, frame_num=f, spp=2, cam=cam, sky_out=s, tex=tex)
+            o = dn.draw(g, f, delta_time=16.667)
+            img = t.cpu().numpy().reshape(h, pitch)
+            assert np.array_equal(img[:, :w * 4].reshape(-1, 4), o["rgba"]), (asynchronous, f)
+            assert (img[:, w * 4:] == 7).all()
+        assert np.array_equal(last, o["rgba"])
+        rt.cleanup()

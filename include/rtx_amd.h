@@ -180,6 +180,7 @@ typedef struct rt_info {
     int32_t deviceId;
     uint32_t spp;               /* samples (reference PathTrace evaluations) per frame */
     int32_t gbufferSet;         /* G-buffer set the last rt_path_trace wrote (0..2, see rt_set_post_stream) */
+    int32_t denoiseRowBegin, denoiseRowEnd; /* rows of a strip-local denoise (rt_set_collective_hook) */
 } rt_info;
 
 int rt_get_info(const rt_context* ctx, rt_info* out);
@@ -199,7 +200,9 @@ enum rt_buffer_name {
     RT_BUF_NOISE_LEVEL16 = 15, /* half, 16x16-tile grid */
     RT_BUF_SKY = 16,           /* float4 512x256 */
     RT_BUF_SUN = 17,           /* float4 32x32 */
-    RT_BUF_ALBEDO = 18         /* half4 */
+    RT_BUF_ALBEDO = 18,        /* half4 */
+    RT_BUF_RGBA8 = 19,         /* uint8 x4, screen res: the last frame's output (CopyToOutput) */
+    RT_BUF_HISTOGRAM = 20      /* uint32[64] luminance histogram (Histogram2) */
 };
 int rt_get_buffer(const rt_context* ctx, int name, void* dst, size_t bytes);
 size_t rt_buffer_bytes(const rt_context* ctx, int name); /* 0 for names not available */
@@ -261,10 +264,38 @@ int rt_set_post_stream(rt_context* ctx, void* stream);
  * NULL is the null stream (as in rt_set_stream); RT_STREAM_OFF (the default) turns it off. */
 int rt_set_gather_stream(rt_context* ctx, void* stream);
 
+/* Multi-GPU strip-local denoise (no reference counterpart, the reference runs on one
+ * GPU).  With stripCount > 1 and a hook set, each rank runs the denoise/post chain only for its own
+ * contiguous rows [rowBegin, rowEnd) — the frame's 64-row blocks split evenly over the ranks — plus
+ * the halo rows its passes read (the summed stencil radius, ~64 rows each side), instead of the
+ * whole frame.  Two exchanges per frame make the result identical to one GPU; the renderer asks the
+ * host to enqueue them on `stream` (the stream the denoise runs on) through the hook:
+ *   RT_HOOK_HISTOGRAM  sum the ranks' 64-bin histograms (RT_BUF_HISTOGRAM) in place (all-reduce)
+ *                      before AutoExposure reads them;
+ *   RT_HOOK_ROWS       give every rank every rank's rows [rowBegin, rowEnd) of the accumulation
+ *                      buffer, of history buffer `historySet` (the final HDR of the frame) and of the
+ *                      RGBA8 output (all-gather), before the next frame's temporal passes read them.
+ * The host binds those buffers to its own device memory (rt_bind_buffer: RT_BUF_ACCUMULATION,
+ * RT_BUF_HISTORY_COLOR sets 0 and 1, RT_BUF_HISTOGRAM, RT_BUF_RGBA8) so its collectives move them
+ * in place (rtx/dist.py StripDenoise).  The hook returns 0 on success.  Without a hook (or with the
+ * noise visualisation, bloom or lens flare on) every rank denoises the whole frame. */
+typedef struct rt_strip_exchange {
+    int32_t frameNum;
+    int32_t rowBegin, rowEnd;   /* this rank's rows */
+    int32_t historySet;         /* history buffer (0 / 1) TemporalFilter2 wrote this frame */
+} rt_strip_exchange;
+#define RT_HOOK_HISTOGRAM 0
+#define RT_HOOK_ROWS 1
+typedef int (*rt_collective_fn)(void* arg, int stage, void* stream, const rt_strip_exchange* x);
+int rt_set_collective_hook(rt_context* ctx, rt_collective_fn fn, void* arg);
+
 /* Use caller-owned device memory (>= the buffer's size at the largest render size, i.e.
  * maxWidth x maxHeight with dynamic resolution, else rt_buffer_bytes; 16-B aligned) as one of the path-trace
  * G-buffers (RT_BUF_RENDER_COLOR / NORMAL / ALBEDO / DEPTH / MOTION), e.g. so a multi-GPU host
- * can all-gather screen strips in place.  The memory must outlive the context's use of it. */
+ * can all-gather screen strips in place; and the strip-local denoise's exchanged buffers
+ * (RT_BUF_ACCUMULATION, RT_BUF_HISTORY_COLOR | RT_BUF_SET1 for the second of the pair,
+ * RT_BUF_HISTOGRAM, RT_BUF_RGBA8), whose current contents are copied over.  The memory must
+ * outlive the context's use of it. */
 int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes);
 
 /* wait for all work on the context stream */

@@ -55,6 +55,19 @@ inline uint32_t strip_row_count(uint32_t height, uint32_t nStrips, uint32_t stri
     return n;
 }
 
+// The rows one rank denoises in a strip-local (multi-GPU) denoise: the frame's 64-row blocks
+// (kDenoiseBlock: one texel row of the 1/64 DownScale4 level) split into nStrips contiguous runs
+// as evenly as whole blocks allow; false when there are fewer blocks than strips.
+constexpr uint32_t kDenoiseBlock = 64;
+inline bool denoise_rows(uint32_t height, uint32_t nStrips, uint32_t strip, uint32_t& a, uint32_t& b) {
+    const uint32_t nb = (height + kDenoiseBlock - 1) / kDenoiseBlock;
+    if (nStrips < 1 || strip >= nStrips || nb < nStrips) return false;
+    const uint32_t b0 = (uint32_t)((uint64_t)strip * nb / nStrips), b1 = (uint32_t)((uint64_t)(strip + 1) * nb / nStrips);
+    a = b0 * kDenoiseBlock;
+    b = b1 * kDenoiseBlock < height ? b1 * kDenoiseBlock : height;
+    return true;
+}
+
 struct TracePrimaryParams {
     TraceCamera cam;
     uint32_t width, height;

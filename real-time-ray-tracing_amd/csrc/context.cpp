@@ -438,6 +438,10 @@ int rt_get_info(const rt_context* ctx, rt_info* out) {
     out->deviceId = ctx->device;
     out->spp = (uint32_t)ctx->spp;
     out->gbufferSet = ctx->fr.gbSet;
+    uint32_t a = 0, b = (uint32_t)ctx->renderH;
+    if (ctx->stripCount > 1) denoise_rows((uint32_t)ctx->renderH, (uint32_t)ctx->stripCount, (uint32_t)ctx->stripIndex, a, b);
+    out->denoiseRowBegin = (int32_t)a;
+    out->denoiseRowEnd = (int32_t)b;
     return RT_OK;
 }
 

@@ -95,8 +95,8 @@ struct FrameResources {
     // denoise + post (denoising.cu, postprocessing.cu)
     uint2* colorB = nullptr;       // ping-pong partner of color
     uint2* accum = nullptr;        // AccumulationColorBuffer
-    uint2* histColor = nullptr;    // HistoryColorBuffer (latest)
-    uint2* histColorAlt = nullptr; // its partner: TemporalFilter2 writes here, then they swap
+    uint2* histBuf[2] = {};        // HistoryColorBuffer pair: histBuf[histIdx] is the latest, TemporalFilter2
+    int histIdx = 0;               // writes the other one, then they swap roles
     uint16_t* histDepth = nullptr; // HistoryDepthBuffer
     uint16_t* noise8 = nullptr;
     uint16_t* noise16 = nullptr;
@@ -173,6 +173,8 @@ struct rt_context {
     hipStream_t ownPostStream = nullptr;  // created by an asynchronous rt_draw_device (destroyed by rt_destroy)
     hipStream_t sideStream = nullptr;  // pipelining: LBVH build + camera rays of the next frame
     hipEvent_t ptDone[kGbSets] = {}, postDone[kGbSets] = {}, overlapEv = nullptr;
+    rt_collective_fn hook = nullptr;     // multi-GPU strip-local denoise exchanges (rt_set_collective_hook)
+    void* hookArg = nullptr;
     hipStream_t gatherStream = nullptr;  // optional: the caller's G-buffer gathers (rt_set_gather_stream)
     bool gatherOn = false;               // gatherStream is set (it may be the null stream)
     hipEvent_t gatherDone[kGbSets] = {};

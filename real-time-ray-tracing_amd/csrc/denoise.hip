@@ -100,6 +100,9 @@ RT_DEV F3 bicubic_smooth(const View2& im, F2 uv) {
     return o / sw;
 }
 
+// 16-row tile row of this workgroup: launches may cover tile rows [P.ty0, P.ty1) only
+RT_DEV int tile_y(const DenoisePostParams& P) { return (int)blockIdx.y + P.ty0; }
+
 template <typename T>
 RT_DEV T tree_sum32(T v) {
 #pragma unroll
@@ -116,14 +119,15 @@ RT_DEV void noise_epilogue(const DenoisePostParams& P, const uint2* sOut, uint16
     const int W = (int)P.W, H = (int)P.H;
     const int W8 = (W + 7) / 8, H8 = (H + 7) / 8, W16 = (W + 15) / 16, H16 = (H + 15) / 16;
     const int tid = threadIdx.x;
-    const int x0 = blockIdx.x * 16, y0 = blockIdx.y * 16;
+    const int TY = tile_y(P);
+    const int x0 = blockIdx.x * 16, y0 = TY * 16;
     if (tid < 128) {
         const int t = tid >> 5, lane = tid & 31;
-        const int tx8 = 2 * blockIdx.x + (t & 1), ty8 = 2 * blockIdx.y + (t >> 1);
+        const int tx8 = 2 * blockIdx.x + (t & 1), ty8 = 2 * TY + (t >> 1);
         const bool valid = tx8 < W8 && ty8 < H8;
         const int x = clampi((valid ? tx8 : 2 * (int)blockIdx.x) * 8 + (lane & 7), 0, W - 1);
-        const int ya = clampi((valid ? ty8 : 2 * (int)blockIdx.y) * 8 + 2 * (lane >> 3), 0, H - 1);
-        const int yb = clampi((valid ? ty8 : 2 * (int)blockIdx.y) * 8 + 2 * (lane >> 3) + 1, 0, H - 1);
+        const int ya = clampi((valid ? ty8 : 2 * TY) * 8 + 2 * (lane >> 3), 0, H - 1);
+        const int yb = clampi((valid ? ty8 : 2 * TY) * 8 + 2 * (lane >> 3) + 1, 0, H - 1);
         const F3 ca = rgb_of(sOut[(ya - y0) * 16 + (x - x0)]), cb = rgb_of(sOut[(yb - y0) * 16 + (x - x0)]);
         const uint32_t bg = (h2f(P.depth[(size_t)ya * W + x]) >= kRayMaxF ? 1u : 0u);
         const uint32_t bg2 = (h2f(P.depth[(size_t)yb * W + x]) >= kRayMaxF ? 1u : 0u);
@@ -147,11 +151,11 @@ RT_DEV void noise_epilogue(const DenoisePostParams& P, const uint2* sOut, uint16
         }
     }
     __syncthreads();
-    if (tid == 0 && (int)blockIdx.x < W16 && (int)blockIdx.y < H16) {
+    if (tid == 0 && (int)blockIdx.x < W16 && TY < H16) {
         // n8.at(2x + i, 2y + j) clamped to the tile grid: tile i/j falls back to 0 past its edge
-        const int i1 = 2 * (int)blockIdx.x + 1 < W8 ? 1 : 0, j1 = 2 * (int)blockIdx.y + 1 < H8 ? 2 : 0;
+        const int i1 = 2 * (int)blockIdx.x + 1 < W8 ? 1 : 0, j1 = 2 * TY + 1 < H8 ? 2 : 0;
         const float v1 = h2f(sN8[0]), v2 = h2f(sN8[i1]), v3 = h2f(sN8[j1]), v4 = h2f(sN8[i1 + j1]);
-        P.noise16[blockIdx.y * W16 + blockIdx.x] = (uint16_t)f2h((v1 + v2 + v3 + v4) / 4);
+        P.noise16[TY * W16 + blockIdx.x] = (uint16_t)f2h((v1 + v2 + v3 + v4) / 4);
     }
 }
 
@@ -163,7 +167,7 @@ template <bool kNoise>
 __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uint2* in, uint2* out) {
     __shared__ uint2 sOut[kNoise ? 256 : 1];
     __shared__ uint16_t sN8[4];
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     const int W = (int)P.W, H = (int)P.H;
     if (x < W && y < H) {
         const uint2 res = temporal_pixel(P, in, x, y);
@@ -295,7 +299,7 @@ __global__ __launch_bounds__(256) void k_noise16(DenoisePostParams P) {
 
 // TileNoiseLevelVisualize (debug pass): outline 16x16 tiles above the noise threshold
 __global__ __launch_bounds__(256) void k_noise_visualize(DenoisePostParams P, uint2* color, int level) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= (int)P.W || y >= (int)P.H) return;
     const int tx = x & 15, ty = y & 15;
     if (!(tx == 0 || tx == 15 || ty == 0 || ty == 15)) return;
@@ -324,14 +328,15 @@ __global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uin
     __shared__ uint16_t sN8[4];
     const int W = (int)P.W, H = (int)P.H;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    const int x = blockIdx.x * 16 + tx, y = blockIdx.y * 16 + ty;
+    const int TY = tile_y(P);
+    const int x = blockIdx.x * 16 + tx, y = TY * 16 + ty;
     const int W16 = (W + 15) / 16;
-    const bool gated = h2f(P.noise16[blockIdx.y * W16 + blockIdx.x]) < P.dn.noise_threshold_local;
+    const bool gated = h2f(P.noise16[TY * W16 + blockIdx.x]) < P.dn.noise_threshold_local;
     const View2 col{in, W, H}, nrm{P.normal, W, H};
     const View1 dep{P.depth, W, H};
     if (!gated) {
         for (int i = threadIdx.x; i < 22 * 22; i += 256) {
-            const int lx = blockIdx.x * 16 - 3 + i % 22, ly = blockIdx.y * 16 - 3 + i / 22;
+            const int lx = blockIdx.x * 16 - 3 + i % 22, ly = TY * 16 - 3 + i / 22;
             sC[i] = col.at(lx, ly);
             sN[i] = nrm.at(lx, ly);
             sD[i] = dep.at(lx, ly);
@@ -399,13 +404,13 @@ RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const u
 template <int S, bool kAlbedo>
 __global__ __launch_bounds__(256) void k_spatial5(DenoisePostParams P, const uint2* in, uint2* out) {
     const int W = (int)P.W, H = (int)P.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= W || y >= H) return;
     const size_t p = (size_t)y * W + x;
     const int W16 = (W + 15) / 16;
     const uint2 c0 = in[p];
     uint2 res = c0;
-    if (!(h2f(P.noise16[blockIdx.y * W16 + blockIdx.x]) < P.dn.noise_threshold_large)) {
+    if (!(h2f(P.noise16[tile_y(P) * W16 + blockIdx.x]) < P.dn.noise_threshold_large)) {
         const View2 col{in, W, H}, nrm{P.normal, W, H};
         const View1 dep{P.depth, W, H};
         F3 nV = rgb_of(P.normal[p]);
@@ -449,8 +454,8 @@ __global__ __launch_bounds__(256) void k_spatial5(DenoisePostParams P, const uin
 
 // ------------------------------------------------------------------ ApplyAlbedo (in place, pointwise)
 __global__ __launch_bounds__(256) void k_apply_albedo(DenoisePostParams P, const uint2* in, uint2* out) {
-    const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= (size_t)P.W * P.H) return;
+    const size_t p = (size_t)P.ty0 * 16 * P.W + (size_t)blockIdx.x * 256 + threadIdx.x;  // rows of tiles ty0..
+    if (p >= (size_t)P.W * P.H || p >= (size_t)P.ty1 * 16 * P.W) return;
     const F3 c = rgb_of(in[p]);
     const F3 a = rgb_of(P.albedo[p]);
     out[p] = pack_color(c * a, 0x3C00u);  // w = half(1.0)
@@ -459,7 +464,7 @@ __global__ __launch_bounds__(256) void k_apply_albedo(DenoisePostParams P, const
 // ------------------------------------------------------------------ TemporalFilter2
 __global__ __launch_bounds__(256) void k_temporal2(DenoisePostParams P, const uint2* in, uint2* out) {
     const int W = (int)P.W, H = (int)P.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= W || y >= H) return;
     const size_t p = (size_t)y * W + x;
     const View2 col{in, W, H}, hc{P.histColor, (int)P.histW, (int)P.histH};
@@ -523,10 +528,14 @@ RT_DEV H4 add4(H4 a, H4 b) { return H4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.
 RT_DEV uint2 pack_h4(H4 v) { return make_uint2(f2h(v.x) | (f2h(v.y) << 16), f2h(v.z) | (f2h(v.w) << 16)); }
 
 // DownScale4: output texel = 4x4 box of inputs, summed as the reference's 2x2-of-2x2 tree
-__global__ __launch_bounds__(256) void k_downscale4(const uint2* in, int Wi, int Hi, uint2* out, int Wo, int Ho) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= Wo * Ho) return;
-    const int ox = i % Wo, oy = i / Wo;
+// output rows [oy0, oy1) only (a strip-local denoise computes its own rows)
+__global__ __launch_bounds__(256) void k_downscale4(const uint2* in, int Wi, int Hi, uint2* out, int Wo, int Ho,
+                                                    int oy0, int oy1) {
+    int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= Wo * (oy1 - oy0)) return;
+    const int ox = i % Wo, oy = oy0 + i / Wo;
+    if (oy >= Ho) return;
+    i = oy * Wo + ox;
     const View2 im{in, Wi, Hi};
     H4 q[2][2];
 #pragma unroll
@@ -547,13 +556,14 @@ __global__ __launch_bounds__(256) void k_downscale4(const uint2* in, int Wi, int
 }
 
 // Histogram2: one 32x32 workgroup over the top-left min(W64,32) x min(H64,32) texels
-__global__ __launch_bounds__(1024) void k_histogram(const uint2* c64, int W64, int H64, uint32_t* hist) {
+// y0 / y1: the texel rows of this (strip-local) count; the ranks' counts are summed afterwards
+__global__ __launch_bounds__(1024) void k_histogram(const uint2* c64, int W64, int H64, uint32_t* hist, int y0, int y1) {
     __shared__ uint32_t h[64];
     if (threadIdx.x < 64) h[threadIdx.x] = 0u;
     __syncthreads();
     const int x = threadIdx.x & 31, y = threadIdx.x >> 5;
     const int tw = W64 < 32 ? W64 : 32, th = H64 < 32 ? H64 : 32;
-    if (x < tw && y < th) {
+    if (x < tw && y < th && y >= y0 && y < y1) {
         const H4 v = h4_of(c64[y * W64 + x]);
         const float lum = dot(f3(v.x, v.y, v.z), f3((float)0.3, (float)0.6, (float)0.1));
         const float logL = (float)((double)rt_log2f(lum) * 0.1 + 0.75);
@@ -748,7 +758,7 @@ RT_DEV F3 catmull_rom(const View2& im, F2 uv) {
 // Bloom (postprocessing.cuh:390-408), out of place: `in` may be the next frame's history
 __global__ __launch_bounds__(256) void k_bloom_apply(DenoisePostParams P, const uint2* in, uint2* out) {
     const int W = (int)P.W, H = (int)P.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= W || y >= H) return;
     const int W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16 = (W4 + 3) / 4, H16 = (H4 + 3) / 4;
     const F2 uv = {(float)x / W, (float)y / H};
@@ -792,7 +802,7 @@ RT_DEV F3 lf_circle(F2 p, float size, float dist, F2 m) {
 
 __global__ __launch_bounds__(256) void k_lens_flare(DenoisePostParams P, const uint2* in, uint2* out) {
     const int W = (int)P.W, H = (int)P.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= W || y >= H) return;
     const size_t p = (size_t)y * W + x;
     const float sunDepth = h2f(P.depth[(size_t)P.sunUv[1] * W + P.sunUv[0]]);
@@ -830,7 +840,7 @@ __global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const u
     __shared__ uint2 sIn[kScaleLds];
     __shared__ uint2 sS[18 * 18];
     const int W = (int)P.W, H = (int)P.H, Ws = (int)P.Ws, Hs = (int)P.Hs;
-    const int X0 = blockIdx.x * 16 - 1, Y0 = blockIdx.y * 16 - 1;
+    const int X0 = blockIdx.x * 16 - 1, Y0 = tile_y(P) * 16 - 1;
     // render texels the 18x18 output apron reads (t1 is monotone in x and y)
     const int ix0 = clampi(scale_t1(clampi(X0, 0, Ws - 1), Ws, W) - 1, 0, W - 1);
     const int ix1 = clampi(scale_t1(clampi(X0 + 17, 0, Ws - 1), Ws, W) + 2, 0, W - 1);
@@ -887,7 +897,7 @@ __global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const u
         }
     }
     __syncthreads();
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= Ws || y >= Hs) return;
     const size_t p = (size_t)y * Ws + x;
     struct {  // clamped reads of the scaled image, from the LDS tile
@@ -952,10 +962,92 @@ __global__ __launch_bounds__(256) void k_hdr_out(const uint2* color, float4* hdr
         if (e__ != hipSuccess) return e__;      \
     } while (0)
 
-extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
+// Tile rows of each pass.  The full frame computes every tile; a strip-local denoise (multi-GPU,
+// rows [rowA, rowB) in 64-row blocks) computes each pass only on the rows the passes after it
+// read for the strip: the stencil radii of the chain summed backwards from the strip — 3 rows for
+// the bicubic scale + sharpen, 1 for TemporalFilter2, 24, 12 and 6 for the a-trous passes, 3 for
+// SpatialFilter7x7 (which also reads the tile-noise levels of its own tiles), 1 for
+// TemporalFilter — rounded out to 16-row tiles (A, B: the strip in tiles):
+//   scale / sharpen / tone map  [A, B)         TemporalFilter2, S5<12>, albedo   [A-1, B+1)
+//   S5<6>                       [A-2, B+2)     S5<3>, SpatialFilter7x7           [A-3, B+3)
+//   TemporalFilter (+ noise)    [A-4, B+4)
+// The accumulation / history rows of the strip itself and the histogram counts are exchanged
+// between the ranks afterwards (rt_set_collective_hook).
+namespace {
+void tile_range(const DenoisePostParams* P, int halo, int& t0, int& t1) {
+    const int H16 = ((int)P->H + 15) / 16;
+    if (!P->stripLocal) { t0 = 0; t1 = H16; return; }
+    t0 = (int)P->rowA / 16 - halo;
+    t1 = ((int)P->rowB + 15) / 16 + halo;
+    t0 = t0 < 0 ? 0 : t0;
+    t1 = t1 > H16 ? H16 : t1;
+}
+}  // namespace
+
+// phase 0: TemporalSpatialDenoising + DownScale4 + Histogram2 (the histogram is this strip's share
+// when strip-local); phase 1: AutoExposure onwards.  A multi-GPU host sums the histograms between
+// the phases.
+extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int phase) {
     const int W = (int)P->W, H = (int)P->H, Ws = (int)P->Ws, Hs = (int)P->Hs;
     const size_t Pn = (size_t)W * H;
-    const dim3 g16((W + 15) / 16, (H + 15) / 16), b256(256);
+    const dim3 b256(256);
+    const int W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16b = (W4 + 3) / 4, H16b = (H4 + 3) / 4, W64 = (W16b + 3) / 4,
+              H64 = (H16b + 3) / 4;
+    hipError_t e;
+    // a copy of the parameters for the launch of tile rows [t0, t1) (halo tiles around the strip)
+    auto tiles = [&](int halo, DenoisePostParams& Q, dim3& g) {
+        int t0, t1;
+        tile_range(P, halo, t0, t1);
+        Q = *P;
+        Q.ty0 = t0;
+        Q.ty1 = t1;
+        g = dim3((W + 15) / 16, (unsigned)(t1 > t0 ? t1 - t0 : 0));
+        return t1 > t0;
+    };
+    DenoisePostParams Q;
+    dim3 g;
+    if (phase == 1) {
+        uint2* cur = P->finalColor;
+        if (P->postProcess) {
+            hipLaunchKernelGGL(k_auto_exposure, dim3(1), dim3(64), 0, s, P->exposure, (const uint32_t*)P->histogram,
+                               (float)(W64 * H64), P->deltaTime, P->gain, P->autoExposure, P->fixedExposure);
+            LAUNCH_CHECK();
+            // Bloom and LensFlare modify RenderColorBuffer, which here may be the next frame's
+            // history (TemporalFilter2's output): both write a colour buffer instead (full frame only).
+            uint2* post = cur == P->colorA ? P->colorB : P->colorA;
+            const dim3 g16((W + 15) / 16, (H + 15) / 16);
+            if (P->bloom) {
+                hipLaunchKernelGGL(k_bloom_gauss, dim3((W4 + 11) / 12, (H4 + 11) / 12), b256, 0, s, (const uint2*)P->c4,
+                                   W4, H4, P->bloom4, (const float*)P->exposure);
+                LAUNCH_CHECK();
+                hipLaunchKernelGGL(k_bloom_gauss, dim3((W16b + 11) / 12, (H16b + 11) / 12), b256, 0, s,
+                                   (const uint2*)P->c16, W16b, H16b, P->bloom16, (const float*)P->exposure);
+                LAUNCH_CHECK();
+                hipLaunchKernelGGL(k_bloom_apply, g16, b256, 0, s, *P, (const uint2*)cur, post);
+                LAUNCH_CHECK();
+                cur = post;
+            }
+            if (P->lensFlare) {
+                hipLaunchKernelGGL(k_lens_flare, g16, b256, 0, s, *P, (const uint2*)cur, post);
+                LAUNCH_CHECK();
+                cur = post;
+            }
+            P->finalColor = cur;
+        }
+        Q = *P;
+        Q.sharpen = P->postProcess && P->sharpen;
+        Q.tonemap = P->postProcess && P->tonemap;
+        int t0 = 0, t1 = (Hs + 15) / 16;
+        if (P->stripLocal) tile_range(P, 0, t0, t1);  // screen = render size for strips
+        Q.ty0 = t0;
+        Q.ty1 = t1;
+        if (t1 > t0) {
+            hipLaunchKernelGGL(k_scale_post, dim3((Ws + 15) / 16, (unsigned)(t1 - t0)), b256, 0, s, Q, (const uint2*)cur);
+            LAUNCH_CHECK();
+        }
+        P->finalScaled = P->scaledB;
+        return hipSuccess;
+    }
     // Buffer plan: the path-trace colour (colorA) and colorB ping-pong; SpatialFilter7x7 writes
     // AccumulationColorBuffer directly and TemporalFilter2 the next history buffer, so neither
     // needs the reference's copy (denoising.cu:110-112, 178-183).  The tile noise levels are
@@ -965,14 +1057,16 @@ extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
     uint2* spare = P->colorB;
     auto next_from = [&](uint2* dst) { if (cur == P->colorA || cur == P->colorB) spare = cur; cur = dst; };
     const int W8 = (W + 7) / 8, H8 = (H + 7) / 8, W16 = (W + 15) / 16, H16 = (H + 15) / 16;
-    hipError_t e;
     auto noise = [&](int level) -> hipError_t {
         hipLaunchKernelGGL(k_tile_noise, dim3((W8 * H8 + 7) / 8), b256, 0, s, *P, (const uint2*)cur);
         LAUNCH_CHECK();
         hipLaunchKernelGGL(k_noise16, dim3((W16 * H16 + 255) / 256), b256, 0, s, *P);
         LAUNCH_CHECK();
         if (P->visualize) {
-            hipLaunchKernelGGL(k_noise_visualize, g16, b256, 0, s, *P, cur, level);
+            DenoisePostParams V = *P;
+            V.ty0 = 0;
+            V.ty1 = H16;
+            hipLaunchKernelGGL(k_noise_visualize, dim3(W16, H16), b256, 0, s, V, cur, level);
             LAUNCH_CHECK();
         }
         return hipSuccess;
@@ -982,9 +1076,11 @@ extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
     if (P->temporal && P->frameNum != 1) {
         noise1 = P->localSpatial && !P->visualize;
         uint2* dst = spare;
-        if (noise1) hipLaunchKernelGGL(k_temporal<true>, g16, b256, 0, s, *P, (const uint2*)cur, dst);
-        else hipLaunchKernelGGL(k_temporal<false>, g16, b256, 0, s, *P, (const uint2*)cur, dst);
-        LAUNCH_CHECK();
+        if (tiles(4, Q, g)) {
+            if (noise1) hipLaunchKernelGGL(k_temporal<true>, g, b256, 0, s, Q, (const uint2*)cur, dst);
+            else hipLaunchKernelGGL(k_temporal<false>, g, b256, 0, s, Q, (const uint2*)cur, dst);
+            LAUNCH_CHECK();
+        }
         next_from(dst);
     }
     bool noise2 = false;
@@ -992,9 +1088,11 @@ extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
         if (!noise1 && (e = noise(1)) != hipSuccess) return e;
         noise2 = P->wideSpatial && !P->visualize;
         uint2* dst = P->temporal ? P->accum : spare;
-        if (noise2) hipLaunchKernelGGL(k_spatial7<true>, g16, b256, 0, s, *P, (const uint2*)cur, dst);
-        else hipLaunchKernelGGL(k_spatial7<false>, g16, b256, 0, s, *P, (const uint2*)cur, dst);
-        LAUNCH_CHECK();
+        if (tiles(3, Q, g)) {
+            if (noise2) hipLaunchKernelGGL(k_spatial7<true>, g, b256, 0, s, Q, (const uint2*)cur, dst);
+            else hipLaunchKernelGGL(k_spatial7<false>, g, b256, 0, s, Q, (const uint2*)cur, dst);
+            LAUNCH_CHECK();
+        }
         next_from(dst);
     } else if (P->temporal) {
         if ((e = hipMemcpyAsync(P->accum, cur, Pn * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
@@ -1008,24 +1106,35 @@ extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
         // a: a colour buffer other than the one being read; b: the other colour buffer
         uint2* a = cur == P->colorA ? P->colorB : cur == P->colorB ? P->colorA : spare;
         uint2* b = a == P->colorA ? P->colorB : P->colorA;
-        hipLaunchKernelGGL((k_spatial5<3, false>), g16, b256, 0, s, *P, (const uint2*)cur, a);
-        LAUNCH_CHECK();
-        hipLaunchKernelGGL((k_spatial5<6, false>), g16, b256, 0, s, *P, (const uint2*)a, b);
-        LAUNCH_CHECK();
-        hipLaunchKernelGGL((k_spatial5<12, true>), g16, b256, 0, s, *P, (const uint2*)b, a);
-        LAUNCH_CHECK();
+        if (tiles(3, Q, g)) {
+            hipLaunchKernelGGL((k_spatial5<3, false>), g, b256, 0, s, Q, (const uint2*)cur, a);
+            LAUNCH_CHECK();
+        }
+        if (tiles(2, Q, g)) {
+            hipLaunchKernelGGL((k_spatial5<6, false>), g, b256, 0, s, Q, (const uint2*)a, b);
+            LAUNCH_CHECK();
+        }
+        if (tiles(1, Q, g)) {
+            hipLaunchKernelGGL((k_spatial5<12, true>), g, b256, 0, s, Q, (const uint2*)b, a);
+            LAUNCH_CHECK();
+        }
         cur = a;
         spare = b;
     } else {  // out of place when cur is the accumulation buffer (the next frame's history)
         uint2* dst = cur == P->accum ? spare : cur;
-        hipLaunchKernelGGL(k_apply_albedo, dim3((unsigned)((Pn + 255) / 256)), b256, 0, s, *P, (const uint2*)cur, dst);
-        LAUNCH_CHECK();
+        if (tiles(1, Q, g)) {
+            const size_t rows = (size_t)(Q.ty1 - Q.ty0) * 16 * W;
+            hipLaunchKernelGGL(k_apply_albedo, dim3((unsigned)((rows + 255) / 256)), b256, 0, s, Q, (const uint2*)cur, dst);
+            LAUNCH_CHECK();
+        }
         cur = dst;
     }
     if (P->temporal2) {
         if (P->frameNum != 1) {
-            hipLaunchKernelGGL(k_temporal2, g16, b256, 0, s, *P, (const uint2*)cur, P->histColorOut);
-            LAUNCH_CHECK();
+            if (tiles(1, Q, g)) {
+                hipLaunchKernelGGL(k_temporal2, g, b256, 0, s, Q, (const uint2*)cur, P->histColorOut);
+                LAUNCH_CHECK();
+            }
         } else if ((e = hipMemcpyAsync(P->histColorOut, cur, Pn * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) {
             return e;
         }
@@ -1037,55 +1146,43 @@ extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
         hipLaunchKernelGGL(k_hdr_out, dim3((unsigned)((Pn + 255) / 256)), b256, 0, s, (const uint2*)cur, P->hdrOut, Pn);
         LAUNCH_CHECK();
     }
-    // ---- PostProcessing (postprocessing.cu:5-161)
-    const int W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16b = (W4 + 3) / 4, H16b = (H4 + 3) / 4, W64 = (W16b + 3) / 4,
-              H64 = (H16b + 3) / 4;
+    // ---- PostProcessing (postprocessing.cu:5-161) up to the histogram: the DownScale4 chain and
+    // the histogram over this context's rows (64-row aligned strips keep each level's texels local)
     if (P->postProcess) {
+        const int ra = P->stripLocal ? (int)P->rowA : 0, rb = P->stripLocal ? (int)P->rowB : H;
+        auto span = [](int a, int b, int f, int n, int& o0, int& o1) {
+            o0 = a / f;
+            o1 = (b + f - 1) / f;
+            o1 = o1 > n ? n : o1;
+        };
         if (P->downScale) {
-            hipLaunchKernelGGL(k_downscale4, dim3((W4 * H4 + 255) / 256), b256, 0, s, (const uint2*)cur, W, H, P->c4, W4, H4);
+            int o0, o1;
+            span(ra, rb, 4, H4, o0, o1);
+            hipLaunchKernelGGL(k_downscale4, dim3((W4 * (o1 - o0) + 255) / 256), b256, 0, s, (const uint2*)cur, W, H,
+                               P->c4, W4, H4, o0, o1);
             LAUNCH_CHECK();
-            hipLaunchKernelGGL(k_downscale4, dim3((W16b * H16b + 255) / 256), b256, 0, s, (const uint2*)P->c4, W4, H4,
-                               P->c16, W16b, H16b);
+            span(ra, rb, 16, H16b, o0, o1);
+            hipLaunchKernelGGL(k_downscale4, dim3((W16b * (o1 - o0) + 255) / 256), b256, 0, s, (const uint2*)P->c4, W4,
+                               H4, P->c16, W16b, H16b, o0, o1);
             LAUNCH_CHECK();
-            hipLaunchKernelGGL(k_downscale4, dim3((W64 * H64 + 255) / 256), b256, 0, s, (const uint2*)P->c16, W16b,
-                               H16b, P->c64, W64, H64);
+            span(ra, rb, 64, H64, o0, o1);
+            hipLaunchKernelGGL(k_downscale4, dim3((W64 * (o1 - o0) + 255) / 256), b256, 0, s, (const uint2*)P->c16,
+                               W16b, H16b, P->c64, W64, H64, o0, o1);
             LAUNCH_CHECK();
         }
         if (P->histogramOn) {
-            hipLaunchKernelGGL(k_histogram, dim3(1), dim3(1024), 0, s, (const uint2*)P->c64, W64, H64, P->histogram);
+            int o0, o1;
+            span(ra, rb, 64, H64, o0, o1);
+            hipLaunchKernelGGL(k_histogram, dim3(1), dim3(1024), 0, s, (const uint2*)P->c64, W64, H64, P->histogram, o0, o1);
             LAUNCH_CHECK();
         } else if ((e = hipMemsetAsync(P->histogram, 0, 256, s)) != hipSuccess) {
             return e;
         }
-        hipLaunchKernelGGL(k_auto_exposure, dim3(1), dim3(64), 0, s, P->exposure, (const uint32_t*)P->histogram,
-                           (float)(W64 * H64), P->deltaTime, P->gain, P->autoExposure, P->fixedExposure);
-        LAUNCH_CHECK();
-        // Bloom and LensFlare modify RenderColorBuffer, which here may be the next frame's
-        // history (TemporalFilter2's output): both write a colour buffer instead.
-        uint2* post = cur == P->colorA ? P->colorB : P->colorA;
-        if (P->bloom) {
-            hipLaunchKernelGGL(k_bloom_gauss, dim3((W4 + 11) / 12, (H4 + 11) / 12), b256, 0, s, (const uint2*)P->c4, W4,
-                               H4, P->bloom4, (const float*)P->exposure);
-            LAUNCH_CHECK();
-            hipLaunchKernelGGL(k_bloom_gauss, dim3((W16b + 11) / 12, (H16b + 11) / 12), b256, 0, s,
-                               (const uint2*)P->c16, W16b, H16b, P->bloom16, (const float*)P->exposure);
-            LAUNCH_CHECK();
-            hipLaunchKernelGGL(k_bloom_apply, g16, b256, 0, s, *P, (const uint2*)cur, post);
-            LAUNCH_CHECK();
-            cur = post;
-        }
-        if (P->lensFlare) {
-            hipLaunchKernelGGL(k_lens_flare, g16, b256, 0, s, *P, (const uint2*)cur, post);
-            LAUNCH_CHECK();
-            cur = post;
-        }
-        P->finalColor = cur;
     }
-    DenoisePostParams Q = *P;
-    Q.sharpen = P->postProcess && P->sharpen;
-    Q.tonemap = P->postProcess && P->tonemap;
-    hipLaunchKernelGGL(k_scale_post, dim3((Ws + 15) / 16, (Hs + 15) / 16), b256, 0, s, Q, (const uint2*)cur);
-    LAUNCH_CHECK();
-    P->finalScaled = P->scaledB;
     return hipSuccess;
+}
+
+extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {
+    hipError_t e = rtk_denoise_phase(P, s, 0);
+    return e == hipSuccess ? rtk_denoise_phase(P, s, 1) : e;
 }

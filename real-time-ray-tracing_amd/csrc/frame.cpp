@@ -200,6 +200,23 @@ void select_gbuffers(FrameResources& fr) {
     fr.motion = fr.gMotion[k];
 }
 
+// the denoise/post chain of one frame on stream s: phase 0, the histogram exchange, phase 1, the
+// rows exchange (the exchanges only for a strip-local denoise, through the caller's hook)
+int run_denoise(rt_context* ctx, DenoisePostParams& p, hipStream_t s) {
+    rt_strip_exchange x{p.frameNum, (int32_t)p.rowA, (int32_t)p.rowB, p.histOutSet};
+    HIP_TRY(ctx, rtk_denoise_phase(&p, s, 0));
+    if (p.stripLocal && ctx->hook(ctx->hookArg, RT_HOOK_HISTOGRAM, (void*)s, &x) != 0) {
+        ctx->err = "collective hook failed (histogram)";
+        return RT_ERR_STATE;
+    }
+    HIP_TRY(ctx, rtk_denoise_phase(&p, s, 1));
+    if (p.stripLocal && ctx->hook(ctx->hookArg, RT_HOOK_ROWS, (void*)s, &x) != 0) {
+        ctx->err = "collective hook failed (rows)";
+        return RT_ERR_STATE;
+    }
+    return RT_OK;
+}
+
 // enqueue a deferred rt_denoise_post on the post stream (frame pipelining)
 int issue_pending_post(rt_context* ctx) {
     if (!ctx->postPending) return RT_OK;
@@ -207,7 +224,7 @@ int issue_pending_post(rt_context* ctx) {
     const int set = ctx->postPendingSet;
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->postStream, ctx->ptDone[set], 0));
     if (ctx->postGather) HIP_TRY(ctx, hipStreamWaitEvent(ctx->postStream, ctx->gatherDone[set], 0));
-    HIP_TRY(ctx, rtk_denoise_post(&ctx->postParams, ctx->postStream));
+    if (int rc = run_denoise(ctx, ctx->postParams, ctx->postStream)) return rc;
     HIP_TRY(ctx, hipEventRecord(ctx->postDone[set], ctx->postStream));
     ctx->fr.renderColor = ctx->postParams.finalColor;  // the launcher's buffer plan names them
     ctx->fr.scaledColor = ctx->postParams.finalScaled;
@@ -357,8 +374,8 @@ int rt_frame_init(rt_context* ctx) {
     }
     ALLOC(fr.colorB, P * 8);
     ALLOC(fr.accum, P * 8);
-    ALLOC(fr.histColor, P * 8);
-    ALLOC(fr.histColorAlt, P * 8);
+    ALLOC(fr.histBuf[0], P * 8);
+    ALLOC(fr.histBuf[1], P * 8);
     ALLOC(fr.histDepth, P * 2);
     const size_t W = (size_t)ctx->renderW, H = (size_t)ctx->renderH;
     const size_t W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16 = (W4 + 3) / 4, H16 = (H4 + 3) / 4;
@@ -407,8 +424,8 @@ int rt_frame_init(rt_context* ctx) {
     HIP_TRY(ctx, hipMemset(fr.rayCounter, 0, (size_t)kRayCounterSlots * kRayCounterStride * 8));
     HIP_TRY(ctx, hipMemset(fr.colorB, 0, P * 8));
     HIP_TRY(ctx, hipMemset(fr.accum, 0, P * 8));
-    HIP_TRY(ctx, hipMemset(fr.histColor, 0, P * 8));
-    HIP_TRY(ctx, hipMemset(fr.histColorAlt, 0, P * 8));
+    HIP_TRY(ctx, hipMemset(fr.histBuf[0], 0, P * 8));
+    HIP_TRY(ctx, hipMemset(fr.histBuf[1], 0, P * 8));
     HIP_TRY(ctx, hipMemset(fr.histDepth, 0, P * 2));
     HIP_TRY(ctx, hipMemset(fr.histogram, 0, 256));
     const float exposure0[4] = {1.0f, 1.0f, 1.0f, 1.0f};  // init.cu:331-333
@@ -612,8 +629,20 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.depth = fr.depth;
     p.motion = fr.motion;
     p.accum = fr.accum;
-    p.histColor = fr.histColor;
-    p.histColorOut = fr.histColorAlt;
+    p.histColor = fr.histBuf[fr.histIdx];
+    p.histColorOut = fr.histBuf[fr.histIdx ^ 1];
+    p.histOutSet = fr.histIdx ^ 1;
+    p.ty0 = 0;
+    p.ty1 = (int)((p.H + 15) / 16);
+    {  // multi-GPU strip-local denoise: only with a collective hook, and for the passes it covers
+        const bool strip = ctx->stripCount > 1 && ctx->hook != nullptr && !ps.enableNoiseLevelVisualize &&
+                           !(ps.enablePostProcess && (ps.enableBloomEffect || ps.enableLensFlare)) &&
+                           ctx->screenW == ctx->renderW && ctx->screenH == ctx->renderH;
+        uint32_t a = 0, b = p.H;
+        p.stripLocal = strip && denoise_rows(p.H, (uint32_t)ctx->stripCount, (uint32_t)ctx->stripIndex, a, b) ? 1 : 0;
+        p.rowA = p.stripLocal ? a : 0;
+        p.rowB = p.stripLocal ? b : p.H;
+    }
     p.histDepth = fr.histDepth;
     p.noise8 = fr.noise8;
     p.noise16 = fr.noise16;
@@ -682,11 +711,11 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
             HIP_TRY(ctx, hipEventRecord(ctx->gatherDone[0], ctx->gatherStream));
             HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->gatherDone[0], 0));
         }
-        HIP_TRY(ctx, rtk_denoise_post(&p, ctx->stream));
+        if (int rc = run_denoise(ctx, p, ctx->stream)) return rc;
         fr.renderColor = p.finalColor;
         fr.scaledColor = p.finalScaled;
     }
-    if (p.temporal2) std::swap(fr.histColor, fr.histColorAlt);
+    if (p.temporal2) fr.histIdx ^= 1;
     ctx->histW = ctx->renderW;  // the history buffers now hold this frame's size
     ctx->histH = ctx->renderH;
     return RT_OK;
@@ -771,6 +800,16 @@ int rt_set_stream(rt_context* ctx, void* stream) {
     int rc = sync_streams(ctx);
     if (rc != RT_OK) return rc;
     ctx->stream = stream == RT_OWN_STREAM ? ctx->ownStream : (hipStream_t)stream;  // NULL: the null stream
+    return RT_OK;
+}
+
+int rt_set_collective_hook(rt_context* ctx, rt_collective_fn fn, void* arg) {
+    if (!ctx) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_set_collective_hook before rt_init"; return RT_ERR_STATE; }
+    int rc = sync_streams(ctx);
+    if (rc != RT_OK) return rc;
+    ctx->hook = fn;
+    ctx->hookArg = arg;
     return RT_OK;
 }
 
@@ -879,7 +918,22 @@ int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
         case RT_BUF_ALBEDO: fr.gAlbedo[set] = (uint2*)device_ptr; break;
         case RT_BUF_DEPTH: fr.gDepth[set] = (uint16_t*)device_ptr; break;
         case RT_BUF_MOTION: fr.gMotion[set] = (uint32_t*)device_ptr; break;
-        default: ctx->err = "rt_bind_buffer: only the path-trace G-buffers can be bound"; return RT_ERR_ARG;
+        // the strip-local denoise's exchanged buffers (set 0 only, except the history pair 0 / 1);
+        // the new memory takes over the old contents (a frame-persistent state)
+        case RT_BUF_ACCUMULATION:
+        case RT_BUF_HISTORY_COLOR:
+        case RT_BUF_HISTOGRAM:
+        case RT_BUF_RGBA8: {
+            if (set > (name == RT_BUF_HISTORY_COLOR ? 1 : 0)) { ctx->err = "rt_bind_buffer: no such set"; return RT_ERR_ARG; }
+            void** slot = name == RT_BUF_ACCUMULATION ? (void**)&fr.accum
+                          : name == RT_BUF_HISTORY_COLOR ? (void**)&fr.histBuf[set]
+                          : name == RT_BUF_HISTOGRAM ? (void**)&fr.histogram : (void**)&fr.rgba;
+            HIP_TRY(ctx, hipMemcpy(device_ptr, *slot, need, hipMemcpyDeviceToDevice));
+            if (name == RT_BUF_RGBA8 && fr.outRgba == fr.rgba) fr.outRgba = (uint32_t*)device_ptr;
+            *slot = device_ptr;
+            return RT_OK;
+        }
+        default: ctx->err = "rt_bind_buffer: this buffer cannot be bound"; return RT_ERR_ARG;
     }
     if (set == fr.gbSet) select_gbuffers(fr);
     return RT_OK;
@@ -889,7 +943,10 @@ int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
 size_t rt_alloc_bytes(const rt_context* ctx, int name) {
     const size_t P = (size_t)ctx->allocW * ctx->allocH;
     switch (name) {
-        case RT_BUF_RENDER_COLOR: case RT_BUF_NORMAL: case RT_BUF_ALBEDO: return P * 8;
+        case RT_BUF_RENDER_COLOR: case RT_BUF_NORMAL: case RT_BUF_ALBEDO: case RT_BUF_ACCUMULATION:
+        case RT_BUF_HISTORY_COLOR: return P * 8;
+        case RT_BUF_HISTOGRAM: return 256;
+        case RT_BUF_RGBA8: return (size_t)ctx->screenW * ctx->screenH * 4;
         case RT_BUF_DEPTH: return P * 2;
         case RT_BUF_MOTION: return P * 4;
         default: return 0;
@@ -909,6 +966,8 @@ size_t rt_buffer_bytes(const rt_context* ctx, int name) {
         case RT_BUF_MOTION: return P * 4;
         case RT_BUF_SKY: return (size_t)kSkySize * 16;
         case RT_BUF_SUN: return (size_t)kSunSize * 16;
+        case RT_BUF_HISTOGRAM: return 256;
+        case RT_BUF_RGBA8: return (size_t)ctx->screenW * ctx->screenH * 4;
         default: return 0;
     }
 }
@@ -923,7 +982,7 @@ int rt_get_buffer(const rt_context* cctx, int name, void* dst, size_t bytes) {
     switch (name) {
         case RT_BUF_RENDER_COLOR: src = fr.renderColor; break;
         case RT_BUF_ACCUMULATION: src = fr.accum; break;
-        case RT_BUF_HISTORY_COLOR: src = fr.histColor; break;
+        case RT_BUF_HISTORY_COLOR: src = fr.histBuf[fr.histIdx]; break;
         case RT_BUF_HISTORY_DEPTH: src = fr.histDepth; break;
         case RT_BUF_SCALED_COLOR: src = fr.scaledColor; break;
         case RT_BUF_NOISE_LEVEL: src = fr.noise8; break;
@@ -934,6 +993,10 @@ int rt_get_buffer(const rt_context* cctx, int name, void* dst, size_t bytes) {
         case RT_BUF_MOTION: src = fr.motion; break;
         case RT_BUF_SKY: src = fr.sky; break;
         case RT_BUF_SUN: src = fr.sun; break;
+        case RT_BUF_HISTOGRAM: src = fr.histogram; break;
+        case RT_BUF_RGBA8:
+            if (bytes < rt_buffer_bytes(ctx, name)) { ctx->err = "destination too small"; return RT_ERR_ARG; }
+            return copy_rgba_out(ctx, dst);
         default: ctx->err = "buffer not available in this revision"; return RT_ERR_ARG;
     }
     const size_t need = rt_buffer_bytes(ctx, name);

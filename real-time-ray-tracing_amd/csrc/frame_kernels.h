@@ -188,9 +188,15 @@ struct DenoisePostParams {
     float4* hdrOut;             // optional render-size float4 copy of the denoised HDR colour
     uint2* finalColor;          // out: buffer holding RenderColorBuffer after denoising
     uint2* finalScaled;         // out: buffer holding ScaledColorBuffer after tone mapping
+    int stripLocal;             // multi-GPU: compute only what rows [rowA, rowB) need (rtk_denoise_phase)
+    uint32_t rowA, rowB;        // this context's output rows (64-row aligned; [0, H) when not strip-local)
+    int histOutSet;             // which buffer of the history pair histColorOut is (the hook reports it)
+    int ty0, ty1;               // per launch (set by the launcher): tile rows of the 16x16-tile kernels
 };
 
 extern "C" hipError_t rtk_denoise_post(DenoisePostParams* p, hipStream_t stream);
+// phase 0: denoise .. DownScale4 + Histogram2; phase 1: AutoExposure .. RGBA8 (finalColor of phase 0 in)
+extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* p, hipStream_t stream, int phase);
 
 extern "C" hipError_t rtk_launch_sky(const SkyGenParams* p, hipStream_t stream);
 // MipmapGen (texture.hip): levels 1.. of a square 16-bit chain whose level 0 is in place

@@ -30,7 +30,7 @@ ARR = dict(VERTICES=0, INDICES=1, NORMALS=2, TRI_POS=3, AABBS=4, MORTON=5, REORD
 TEX = dict(SOIL_ALBEDO_AO=0, SOIL_NORMAL_ROUGHNESS=1, SOIL_HEIGHT=2)  # MipmapTextureName (texture.h:5-12)
 # rt_buffer_name (Buffer2DName, kernel.cuh:286-315)
 BUF = dict(RENDER_COLOR=0, ACCUMULATION=1, HISTORY_COLOR=2, SCALED_COLOR=3, NORMAL=10, DEPTH=11, HISTORY_DEPTH=12,
-           MOTION=13, NOISE_LEVEL=14, NOISE_LEVEL16=15, SKY=16, SUN=17, ALBEDO=18)
+           MOTION=13, NOISE_LEVEL=14, NOISE_LEVEL16=15, SKY=16, SUN=17, ALBEDO=18, RGBA8=19, HISTOGRAM=20)
 
 # canonical 64-byte BVH node as a numpy record (see RT_ARR_NODES)
 NODE_DTYPE = np.dtype([("lmin", "<f4", 3), ("lmax", "<f4", 3), ("rmin", "<f4", 3), ("rmax", "<f4", 3),
@@ -82,7 +82,17 @@ class Info(C.Structure):
     _fields_ = [("triCount", C.c_uint32), ("triCountPadded", C.c_uint32), ("batchCount", C.c_uint32),
                 ("vertexCount", C.c_uint32), ("renderWidth", C.c_int32), ("renderHeight", C.c_int32),
                 ("screenWidth", C.c_int32), ("screenHeight", C.c_int32), ("frameNum", C.c_int32),
-                ("deviceId", C.c_int32), ("spp", C.c_uint32), ("gbufferSet", C.c_int32)]
+                ("deviceId", C.c_int32), ("spp", C.c_uint32), ("gbufferSet", C.c_int32),
+                ("denoiseRowBegin", C.c_int32), ("denoiseRowEnd", C.c_int32)]
+
+
+class StripExchange(C.Structure):
+    """rt_strip_exchange: what a strip-local denoise asks the host to exchange (rt_set_collective_hook)."""
+    _fields_ = [("frameNum", C.c_int32), ("rowBegin", C.c_int32), ("rowEnd", C.c_int32), ("historySet", C.c_int32)]
+
+
+COLLECTIVE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.POINTER(StripExchange))
+HOOK_HISTOGRAM, HOOK_ROWS = 0, 1
 
 
 # every entry point declared in include/rtx_amd.h, with its ctypes signature
@@ -113,6 +123,7 @@ SIGNATURES = {
     "rt_set_post_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "rt_set_gather_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "rt_bind_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
+    "rt_set_collective_hook": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_get_ray_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "rt_build_bvh": (C.c_int, [C.c_void_p]),
     "rt_trace_primary": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
@@ -303,6 +314,28 @@ class RayTracer:
         0 is the null stream (torch's default stream), as in set_stream; None turns it off."""
         ptr = C.c_void_p(-2) if stream is None else C.c_void_p(stream)  # RT_STREAM_OFF
         self._check(self.lib.rt_set_gather_stream(self.h, ptr), "rt_set_gather_stream")
+
+    def set_collective_hook(self, fn):
+        """fn(stage, stream_handle, exchange) -> None, called on the host when a strip-local denoise
+        needs its histogram all-reduce (HOOK_HISTOGRAM) or its rows all-gather (HOOK_ROWS) enqueued
+        on stream_handle; None removes the hook (every rank then denoises the whole frame)."""
+        if fn is None:
+            self._hook = None
+            self._check(self.lib.rt_set_collective_hook(self.h, None, None), "rt_set_collective_hook")
+            return
+
+        def tramp(arg, stage, stream, x):
+            try:
+                fn(stage, stream or 0, x.contents)
+                return 0
+            except Exception:  # reported through rt_last_error's RT_ERR_STATE
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        self._hook = COLLECTIVE_FN(tramp)  # keep the thunk alive as long as the context
+        self._check(self.lib.rt_set_collective_hook(self.h, C.cast(self._hook, C.c_void_p), None),
+                    "rt_set_collective_hook")
 
     def bind_buffer(self, name: str, device_ptr: int, nbytes: int, gbuffer_set: int = 0):
         what = BUF[name] | (int(gbuffer_set) << 8)  # RT_BUF_SET1 / RT_BUF_SET2

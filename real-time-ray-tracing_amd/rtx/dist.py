@@ -116,3 +116,107 @@ class StripGather:
     def bytes_per_frame(self) -> int:
         """Bytes each rank receives per frame."""
         return self.stage_bytes * (self.world - 1)
+
+
+DENOISE_BLOCK = 64  # kDenoiseBlock (bvh_kernels.h): one texel row of the 1/64 DownScale4 level
+
+
+def denoise_rows(height: int, world: int, rank: int) -> tuple[int, int]:
+    """[a, b) rows rank denoises in the strip-local denoise (denoise_rows in the renderer): the
+    frame's 64-row blocks split into `world` contiguous runs as evenly as whole blocks allow."""
+    nb = math.ceil(height / DENOISE_BLOCK)
+    if nb < world:
+        raise ValueError("height %d has fewer 64-row blocks than %d ranks" % (height, world))
+    b0, b1 = rank * nb // world, (rank + 1) * nb // world
+    return b0 * DENOISE_BLOCK, min(b1 * DENOISE_BLOCK, height)
+
+
+class StripDenoise:
+    """The strip-local denoise's exchanges (rt_set_collective_hook).
+
+    Every rank denoises only its contiguous rows (plus the halo its passes read, inside the
+    renderer) instead of the whole frame.  Per frame the renderer asks for two collectives, enqueued
+    on the stream the denoise runs on:
+      * HOOK_HISTOGRAM: all-reduce (sum) of the 64-bin luminance histogram — each rank counted the
+        Histogram2 texels of its own rows — before AutoExposure reads it;
+      * HOOK_ROWS: all-gather of every rank's rows of the accumulation buffer, of the history
+        buffer TemporalFilter2 just wrote (the frame's final HDR) and of the RGBA8 output, which the
+        next frame's temporal passes read at reprojected positions anywhere on screen.
+    The four buffers are caller-owned tensors bound into the renderer, so the collectives move
+    them in place; the rows travel in one staging buffer per rank (padded to the largest strip):
+    20 B per pixel of the strip.  On a separate process group, so these collectives never
+    interleave with the G-buffer gathers of StripGather on one communicator."""
+
+    def __init__(self, width: int, height: int, world: int, rank: int, device, rt=None, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.W, self.H, self.world, self.rank, self.device = width, height, world, rank, device
+        self.rows = [denoise_rows(height, world, r) for r in range(world)]
+        self.a, self.b = self.rows[rank]
+        self.max_rows = max(b - a for a, b in self.rows)
+        P = width * height
+        u8 = dict(dtype=torch.uint8, device=device)
+        self.accum = torch.zeros(P * 8, **u8)
+        self.history = [torch.zeros(P * 8, **u8), torch.zeros(P * 8, **u8)]
+        self.rgba = torch.zeros(P * 4, **u8)
+        self.histogram = torch.zeros(64, dtype=torch.int32, device=device)
+        self.row_bytes = width * (8 + 8 + 4)
+        self.send = torch.zeros(self.max_rows * self.row_bytes, **u8)
+        self.recv = torch.zeros(world * self.max_rows * self.row_bytes, **u8)
+        self.group = group if group is not None else (dist.new_group(list(range(world))) if world > 1 else None)
+        self.rt = rt
+        if rt is not None:
+            rt.bind_buffer("ACCUMULATION", self.accum.data_ptr(), self.accum.numel())
+            rt.bind_buffer("HISTORY_COLOR", self.history[0].data_ptr(), self.history[0].numel(), gbuffer_set=0)
+            rt.bind_buffer("HISTORY_COLOR", self.history[1].data_ptr(), self.history[1].numel(), gbuffer_set=1)
+            rt.bind_buffer("HISTOGRAM", self.histogram.data_ptr(), 256)
+            rt.bind_buffer("RGBA8", self.rgba.data_ptr(), self.rgba.numel())
+            rt.set_collective_hook(self.hook)
+
+    def bytes_per_frame(self) -> int:
+        """Bytes each rank receives per frame for the rows exchange."""
+        return (self.world - 1) * self.max_rows * self.row_bytes
+
+    def _views(self, history_set: int):
+        W, H = self.W, self.H
+        return (self.accum.view(H, W * 8), self.history[history_set].view(H, W * 8), self.rgba.view(H, W * 4))
+
+    def exchange_histogram(self):
+        import torch.distributed as dist
+
+        dist.all_reduce(self.histogram, group=self.group)
+
+    def exchange_rows(self, history_set: int):
+        import torch.distributed as dist
+
+        acc, his, rgb = self._views(history_set)
+        W, n = self.W, self.b - self.a
+        s = self.send.view(self.max_rows, self.row_bytes)
+        s[:n, :W * 8].copy_(acc[self.a:self.b])
+        s[:n, W * 8:W * 16].copy_(his[self.a:self.b])
+        s[:n, W * 16:].copy_(rgb[self.a:self.b])
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+        else:
+            dist.all_gather(list(self.recv.view(self.world, -1).unbind(0)), self.send, group=self.group)
+        every = self.recv.view(self.world, self.max_rows, self.row_bytes)
+        for r, (a, b) in enumerate(self.rows):
+            if r == self.rank:
+                continue
+            m = b - a
+            acc[a:b].copy_(every[r, :m, :W * 8])
+            his[a:b].copy_(every[r, :m, W * 8:W * 16])
+            rgb[a:b].copy_(every[r, :m, W * 16:])
+
+    def hook(self, stage: int, stream: int, x):
+        """rt_set_collective_hook callback: enqueue the exchange on the renderer's stream."""
+        import torch
+
+        s = torch.cuda.ExternalStream(stream, device=self.device) if stream else torch.cuda.default_stream(self.device)
+        with torch.cuda.stream(s):
+            if stage == 0:
+                self.exchange_histogram()
+            else:
+                assert (x.rowBegin, x.rowEnd) == (self.a, self.b), "renderer and host disagree on the strip"
+                self.exchange_rows(int(x.historySet))

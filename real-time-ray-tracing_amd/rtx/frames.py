@@ -8,17 +8,20 @@ bench.py times exactly this object's ``frame`` calls and the parity tests run th
   (rt_set_post_stream) beside the trace kernels of frame f+1;
 * with N ranks (rtx/dist.py) every rank path traces its interleaved row blocks, the G-buffers
   are all-gathered (RCCL on its own stream when the backend is nccl, after a host sync with
-  gloo) and the denoise/post chain runs on the assembled frame.
+  gloo), and each rank denoises its own contiguous rows of the assembled frame (StripDenoise:
+  the histogram all-reduce and the accumulation / history / RGBA8 row all-gathers the renderer
+  asks for through its collective hook; strip_denoise=False denoises the whole frame on every rank).
 """
 from __future__ import annotations
 
 
 class FramePipeline:
-    def __init__(self, rt, device, pipelined: bool = True, world: int = 1, rank: int = 0, backend: str = "nccl"):
+    def __init__(self, rt, device, pipelined: bool = True, world: int = 1, rank: int = 0, backend: str = "nccl",
+                 strip_denoise: bool = True):
         import torch
 
         import rtx
-        from rtx.dist import StripGather
+        from rtx.dist import StripDenoise, StripGather
 
         self.rt, self.device, self.pipelined = rt, device, pipelined
         self.world, self.rank = world, rank
@@ -39,6 +42,9 @@ class FramePipeline:
         self.gs = torch.cuda.Stream(device) if (self.gather is not None and backend == "nccl") else None
         if self.gs is not None:
             rt.set_gather_stream(self.gs.cuda_stream)
+        info = rt.info()
+        self.denoise = (StripDenoise(info.renderWidth, info.renderHeight, world, rank, device, rt)
+                        if (world > 1 and strip_denoise) else None)
 
     def frame(self, f: int, hdr: bool = False):
         """LBVH rebuild, path trace, (gather,) denoise + post of frame f, enqueued asynchronously."""

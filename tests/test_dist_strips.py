@@ -133,3 +133,57 @@ def test_strip_allgather_pipelined_sets(tmp_path):
                     # gathered set: every rank's blocks; the others: this rank's own blocks only
                     want = 10 * k + q if (k == 1 or q == r) else 0
                     assert (a[:, q] == want).all(), (r, name, k, q)
+
+
+def denoise_worker(rank, world, port, result_dir):
+    import torch
+    import torch.distributed as dist
+
+    from rtx.dist import StripDenoise
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        Wd, Hd = 40, 200  # 4 blocks of 64 rows (the last one short)
+        sd = StripDenoise(Wd, Hd, world, rank, torch.device("cpu"))
+        rng = np.random.default_rng(11)
+        full = dict(accum=rng.integers(0, 256, Wd * Hd * 8, dtype=np.uint8),
+                    h1=rng.integers(0, 256, Wd * Hd * 8, dtype=np.uint8),
+                    rgba=rng.integers(0, 256, Wd * Hd * 4, dtype=np.uint8))
+        a, b = sd.a, sd.b
+        # this rank computed its own rows (and stale halo rows elsewhere): only [a, b) are right
+        for t, key, bpp in ((sd.accum, "accum", 8), (sd.history[1], "h1", 8), (sd.rgba, "rgba", 4)):
+            t.fill_(0xEE)
+            t[a * Wd * bpp:b * Wd * bpp] = torch.from_numpy(full[key][a * Wd * bpp:b * Wd * bpp].copy())
+        sd.history[0].fill_(0x55)  # the other history buffer is not exchanged this frame
+        sd.histogram.copy_(torch.arange(64, dtype=torch.int32) * (rank + 1))
+        sd.exchange_histogram()
+        sd.exchange_rows(1)
+        np.savez(os.path.join(result_dir, "d%d.npz" % rank), accum=sd.accum.numpy(), h1=sd.history[1].numpy(),
+                 rgba=sd.rgba.numpy(), h0=sd.history[0].numpy(), hist=sd.histogram.numpy(),
+                 **{"full_" + k: v for k, v in full.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_strip_denoise_exchange(tmp_path, world):
+    """StripDenoise (the strip-local denoise's collectives) with gloo on CPU: after the histogram
+    all-reduce and the rows all-gather every rank holds the whole frame's accumulation, history
+    (only the buffer TemporalFilter2 wrote) and RGBA8, and the summed histogram."""
+    import torch.multiprocessing as mp
+
+    from rtx.dist import denoise_rows
+
+    assert [denoise_rows(1080, 8, r) for r in (0, 7)] == [(0, 128), (896, 1080)]
+    assert sum(b - a for a, b in (denoise_rows(2160, 8, r) for r in range(8))) == 2160
+    with pytest.raises(ValueError):
+        denoise_rows(100, 3, 0)  # 2 blocks of 64 rows for 3 ranks
+    mp.start_processes(denoise_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
+    for r in range(world):
+        d = np.load(tmp_path / ("d%d.npz" % r))
+        for k in ("accum", "h1", "rgba"):
+            assert np.array_equal(d[k], d["full_" + k]), (r, k)
+        assert (d["h0"] == 0x55).all()
+        assert np.array_equal(d["hist"], np.arange(64) * sum(range(1, world + 1)))

@@ -21,12 +21,15 @@ def free_port():
     return p
 
 
-def render(rank, world, port, out_dir, pipelined, gather_stream):
+def render(rank, world, port, out_dir, pipelined, gather_stream, strip_denoise=False, size=(W, H), frames=FRAMES,
+           tag=""):
     import torch
     import torch.distributed as dist
 
     import rtx
-    from rtx.dist import StripGather, strip_config
+    from rtx.dist import StripDenoise, StripGather, strip_config
+
+    W, H = size
 
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -46,8 +49,12 @@ def render(rank, world, port, out_dir, pipelined, gather_stream):
     gs = torch.cuda.Stream(dev) if (gather_stream and sg is not None) else None
     if gs is not None:
         rt.set_gather_stream(gs.cuda_stream)
+    sd = StripDenoise(W, H, world, rank, dev, rt) if (strip_denoise and world > 1) else None
+    if sd is not None:
+        i = rt.info()
+        assert (i.denoiseRowBegin, i.denoiseRowEnd) == (sd.a, sd.b)
     cam0 = rt.camera
-    for f in range(1, FRAMES + 1):
+    for f in range(1, frames + 1):
         c = rt.camera
         c.yaw = cam0.yaw + 0.02 * f
         rt.camera = c
@@ -63,9 +70,11 @@ def render(rank, world, port, out_dir, pipelined, gather_stream):
                 sg.gather()
         rt.denoise_post(f)
     rgba = rt.download("RGBA8", np.uint8).copy()
-    hdr = rt.get_buffer("RENDER_COLOR").copy()
+    hdr = rt.get_buffer("HISTORY_COLOR").copy()  # TemporalFilter2's output: the frame's final HDR
+    acc = rt.get_buffer("ACCUMULATION").copy()
+    expo = rt.download("EXPOSURE", np.uint8).copy()
     rt.cleanup()
-    np.savez(os.path.join(out_dir, "r%d_of%d.npz" % (rank, world)), rgba=rgba, hdr=hdr)
+    np.savez(os.path.join(out_dir, "%sr%d_of%d.npz" % (tag, rank, world)), rgba=rgba, hdr=hdr, acc=acc, expo=expo)
     if world > 1:
         dist.destroy_process_group()
 
@@ -83,5 +92,37 @@ def test_two_ranks_one_gpu_match_single_rank(tmp_path, pipelined, gather_stream)
     ref = np.load(tmp_path / "r0_of1.npz")
     for r in range(2):
         got = np.load(tmp_path / ("r%d_of2.npz" % r))
-        assert np.array_equal(got["rgba"], ref["rgba"]), "rank %d RGBA8" % r
-        assert np.array_equal(got["hdr"], ref["hdr"]), "rank %d HDR" % r
+        for k in ("rgba", "hdr", "acc", "expo"):
+            assert np.array_equal(got[k], ref[k]), "rank %d %s" % (r, k)
+
+
+@pytest.mark.parametrize("pipelined,gather_stream", [(True, True), (False, False)])
+def test_two_ranks_strip_local_denoise(tmp_path, pipelined, gather_stream):
+    """Each rank denoises only its own 64-row-block strip (rt_set_collective_hook + rtx.dist.StripDenoise:
+    histogram all-reduce, accumulation / history / RGBA8 row all-gathers); after 4 frames of a moving
+    camera both ranks hold the single-rank frame bit for bit."""
+    import torch.multiprocessing as mp
+
+    mp.start_processes(render, args=(1, 0, str(tmp_path), pipelined, gather_stream), nprocs=1, start_method="spawn")
+    mp.start_processes(render, args=(2, free_port(), str(tmp_path), pipelined, gather_stream, True), nprocs=2,
+                       start_method="spawn")
+    ref = np.load(tmp_path / "r0_of1.npz")
+    for r in range(2):
+        got = np.load(tmp_path / ("r%d_of2.npz" % r))
+        for k in ("rgba", "hdr", "acc", "expo"):
+            assert np.array_equal(got[k], ref[k]), "rank %d %s" % (r, k)
+
+
+def test_two_ranks_4k_strip_local_denoise(tmp_path):
+    """Config 5's frame (3840x2160) split over two ranks (gloo on one GPU), strip-local denoise,
+    two pipelined frames, against a single-rank render."""
+    import torch.multiprocessing as mp
+
+    args = (True, True, True, (3840, 2160), 2, "k")
+    mp.start_processes(render, args=(1, 0, str(tmp_path)) + args, nprocs=1, start_method="spawn")
+    mp.start_processes(render, args=(2, free_port(), str(tmp_path)) + args, nprocs=2, start_method="spawn")
+    ref = np.load(tmp_path / "kr0_of1.npz")
+    for r in range(2):
+        got = np.load(tmp_path / ("kr%d_of2.npz" % r))
+        for k in ("rgba", "hdr", "acc", "expo"):
+            assert np.array_equal(got[k], ref[k]), "rank %d %s" % (r, k)

@@ -21,8 +21,11 @@ mismatch exits non-zero.
 
 N ranks (torch.distributed.run, one per GPU): each rank rebuilds the BVH, path traces its rows
 of the frame (16-row blocks dealt round-robin), the ranks' G-buffer blocks are all-gathered over
-RCCL (rtx/dist.py) and the denoise/post chain runs on the assembled frame.  Total work per frame
-is fixed as N grows ("strong" scaling).  Timing: barrier + device sync on both sides of exactly
+RCCL (rtx/dist.py), and each rank denoises only its own contiguous 64-row-block strip of the
+assembled frame (plus the halo its passes read), exchanging the histogram (all-reduce) and its
+rows of the accumulation, history (the final HDR) and RGBA8 buffers (all-gather) with the others.
+Rank 0's self-check compares its frame with a single-GPU serial render.  Total work per frame is
+fixed as N grows ("strong" scaling).  Timing: barrier + device sync on both sides of exactly
 K frames, max over ranks; value = rays of all ranks / that time.
 
 Roofline: per path-trace kernel, algorithmic bytes from the GPU's own work
@@ -279,7 +282,9 @@ def main():
         "config": {"workload": "BASELINE config 3: %dx%d, %d spp path trace + SVGF denoise + auto-exposure/"
                                "tone map, per-frame LBVH rebuild" % (W, H, S),
                    "width": W, "height": H, "spp": S,
-                   "parallelism": ("interleaved 16-row strips x%d + RCCL all-gather of G-buffers" % world if world > 1
+                   "parallelism": ("interleaved 16-row strips x%d + RCCL all-gather of G-buffers, strip-local "
+                                   "denoise (64-row blocks) with histogram all-reduce and accumulation/history/RGBA8 "
+                                   "row all-gathers" % world if world > 1
                                    else "single GPU")
                                   + ("; pipelined frames: denoise/post of f-1 and LBVH build + camera rays of "
                                      "f+1 on their own streams beside the trace kernels of f" if pipeline

@@ -842,14 +842,15 @@ extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t s
     hipError_t e = hipSuccess;  // the counters were zeroed before the camera kernel (rtk_launch_pt_camera)
     int k = 1;  // kernel 1 = shade; marks[2k] / marks[2k + 1] bracket kernel k on this stream
     auto begin = [&]() { return marks ? hipEventRecord(marks[2 * k], stream) : hipSuccess; };
-    auto end = [&]() {
+    auto end = [&]() {  // the mark first: a hook that blocks the host must not delay it
+        const hipError_t me = marks ? hipEventRecord(marks[2 * k + 1], stream) : hipSuccess;
+        if (me != hipSuccess) return me;
         if (hook && hook->fn) {
             const hipError_t he = hook->fn(hook->arg, k);
             if (he != hipSuccess) return he;
         }
-        const hipError_t me = marks ? hipEventRecord(marks[2 * k + 1], stream) : hipSuccess;
         ++k;
-        return me;
+        return hipSuccess;
     };
     if ((e = begin()) != hipSuccess) return e;
     if (p->ws.glossy) hipLaunchKernelGGL(k_pt_shade0<true>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);

@@ -533,6 +533,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     {  // material table (init.cu:215-251): only mirror / glass ids make steps 1-2 trace
         const int m = ctx->materialOverride;
         p.ws.glossy = m >= 0 && (m == 1 || m == 5 || m >= 10);
+        p.ws.microfacet = m == 4;  // mat_type: only id 4 is MICROFACET, the reference table uses 3 / 6
     }
     if (with_detail) {  // per-pixel counters: everything in order on the context stream
         if (ctx->postStream && (rc = sync_streams(ctx)) != RT_OK) return rc;

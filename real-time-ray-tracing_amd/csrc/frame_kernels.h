@@ -97,6 +97,7 @@ struct PtWorkspace {
     uint32_t cap;               // entries per queue (= rows * W * spp)
     uint32_t persistBlocks;     // grid of the persistent queue kernels
     int glossy;                 // materials can be glossy: steps 1-2 may trace (materialOverride)
+    int microfacet;             // materials can be the microfacet one (materialOverride 4): GGX compiled in
     uint32_t* itersOut = nullptr;  // optional [cap]: traversal iterations per queue entry (rt_trace_rays)
 };
 

@@ -161,7 +161,10 @@ RT_DEV void tri_plane(const PathTraceParams& P, F2 uv, float lod, F3 normal, F3 
 }
 
 // DiffuseSurfaceInteraction (surfaceInteraction.cuh:36-310); random numbers rn[2*bounce] and
-// rn[2*bounce+1]
+// rn[2*bounce+1].  kMF: the material table can hold the microfacet material (id 4, only through
+// materialOverride); without it the GGX branch, whose live values set the kernels' register peak,
+// is not compiled in.
+template <bool kMF>
 RT_DEV void diffuse(PathCtx& c, int bounce, RayState& rs, F3& beta) {
     if (rs.hitLight || !rs.isDiffuse || rs.isOccluded) return;
     const PathTraceParams& P = c.P;
@@ -207,7 +210,7 @@ RT_DEV void diffuse(PathCtx& c, int bounce, RayState& rs, F3& beta) {
     sample_light(P, c.sunDir, lDir, lPdf, lIdx, r2[0], r2[1], c.skyTree, c.sunTree);
     F3 sDir, sBsdf, lBsdf, tmp;
     float sPdf = 0.0f;
-    if (rs.matType == LAMBERTIAN) {
+    if (!kMF || rs.matType == LAMBERTIAN) {
         lambertian_sample(F2{r[0], r[1]}, sDir, normal);
         sBsdf = albedo / kPi;
         sPdf = fmx(dot(sDir, normal), kSafeCos) / kPi;
@@ -268,7 +271,7 @@ RT_DEV float ray_cone_width(const PathTraceParams& P, int ix, int iy) {
 // set, step k0's intersection result is *hit (a deferred ray that came back from the queue
 // tracer).  An intersection at a step >= kDeferFrom is not traced here: the step is returned
 // and the caller queues the ray.  Returns 5 when the path is complete.
-template <int kDeferFrom>
+template <int kDeferFrom, bool kMF>
 RT_DEV int run_path(PathCtx& c, PathVars& v, int k0, const HitInfo* hit, const SceneView& sc, uint32_t* stkA,
                     float* stkT) {
     RayState& rs = v.rs;
@@ -304,7 +307,7 @@ RT_DEV int run_path(PathCtx& c, PathVars& v, int k0, const HitInfo* hit, const S
         if (k >= 2) {
             const bool first = k == 2;
             F3 beta = f3(1.0f);
-            diffuse(c, first ? 0 : 1, rs, beta);
+            diffuse<kMF>(c, first ? 0 : 1, rs, beta);
             if (first) {
                 v.beta1 = beta;
                 v.outNormal = rs.fakeNormal;
@@ -462,12 +465,16 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
             F2 uv;
             generate_ray_jittered(P.cam, x, y, F2{rnd(c, 0, 0), rnd(c, 0, 1)}, F2{rnd(c, 0, 2), rnd(c, 0, 3)}, org,
                                   dir, uv);
-            TravRay tr;
-            trav_setup(sc, org, dir, tr);
             TravState st;
-            trav_init(st);
-            for (int it = 0; it < 1024; ++it)
-                if (trav_step(sc, tr, st, stkA + tid, stkT + tid, 256)) break;
+            if (root_surely_missed(sc, org, dir)) {  // most sky rays: settled without the ray-box helper
+                trav_root_miss(st);
+            } else {
+                TravRay tr;
+                trav_setup(sc, org, dir, tr);
+                trav_init(st);
+                for (int it = 0; it < 1024; ++it)
+                    if (trav_step(sc, tr, st, stkA + tid, stkT + tid, 256)) break;
+            }
             ++rays;
             if (P.statsOut) {
                 atomicAdd(&P.statsOut[p].y, st.visits);
@@ -559,7 +566,7 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
 // them back to back.  The folding thread (sample wave 0) then combines the round's samples in
 // sample order through LDS — colour and albedo sums, the first deferred sample, the per-sample
 // colours the resolve kernel needs — exactly as the sequential loop of PathTrace's caller does.
-template <bool kGlossy>
+template <bool kGlossy, bool kMF>
 __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
     __shared__ uint32_t stkA[kGlossy ? 16 * 256 : 1];
     __shared__ float stkT[kGlossy ? 16 * 256 : 1];
@@ -618,7 +625,8 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
                 HitInfo h;
                 finalize_hit(sc, v.rs.orig, v.rs.dir, hr.x, (int)__float_as_uint(hr.y), hr.z, hr.w, P.ws.hit0Err[q],
                              h);
-                kd = run_path<kGlossy ? 3 : 1>(c, v, 0, &h, sc, stkA + (kGlossy ? tid : 0), stkT + (kGlossy ? tid : 0));
+                kd = run_path<kGlossy ? 3 : 1, kMF>(c, v, 0, &h, sc, stkA + (kGlossy ? tid : 0),
+                                                     stkT + (kGlossy ? tid : 0));
                 if (kd < 3) {  // cannot happen without mirror/glass materials: flag it, finish the sample
                     atomicAdd(&P.ws.counters[kCntError], 1u);
                     kd = 5;
@@ -717,7 +725,7 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
 }
 
 // Resumes the samples of queue kStep (3 or 4) once k_trace_queue has written their hits.
-template <int kStep>
+template <int kStep, bool kMF>
 __global__ __launch_bounds__(256) void k_pt_resume(PathTraceParams P) {
     __shared__ uint32_t sob[256];
     __shared__ unsigned long long wgRays[4];
@@ -771,7 +779,7 @@ __global__ __launch_bounds__(256) void k_pt_resume(PathTraceParams P) {
             rs.matType = MAT_SKY;
             HitInfo h;
             finalize_hit(sc, rs.orig, rs.dir, hr.x, (int)__float_as_uint(hr.y), hr.z, hr.w, herr, h);
-            kd = run_path<0>(c, v, kStep, &h, sc, nullptr, nullptr);
+            kd = run_path<0, kMF>(c, v, kStep, &h, sc, nullptr, nullptr);
         }
         const uint32_t slot = wave_append(kd == 4, &P.ws.counters[kCntQ4]);
         if (active) {
@@ -853,16 +861,19 @@ extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t s
         return hipSuccess;
     };
     if ((e = begin()) != hipSuccess) return e;
-    if (p->ws.glossy) hipLaunchKernelGGL(k_pt_shade0<true>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
-    else hipLaunchKernelGGL(k_pt_shade0<false>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
+    const dim3 pg(p->ws.persistBlocks), pb(256);
+    if (p->ws.glossy) hipLaunchKernelGGL((k_pt_shade0<true, false>), pg, pb, 0, stream, *p);
+    else if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_shade0<false, true>), pg, pb, 0, stream, *p);
+    else hipLaunchKernelGGL((k_pt_shade0<false, false>), pg, pb, 0, stream, *p);
     if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
     if ((e = rtk_launch_trace_queue(p, 3, stream)) != hipSuccess || (e = end()) != hipSuccess) return e;
     if ((e = begin()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pt_resume<3>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
+    if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_resume<3, true>), pg, pb, 0, stream, *p);
+    else hipLaunchKernelGGL((k_pt_resume<3, false>), pg, pb, 0, stream, *p);
     if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
     if ((e = rtk_launch_trace_queue(p, 4, stream)) != hipSuccess || (e = end()) != hipSuccess) return e;
     if ((e = begin()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_pt_resume<4>, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
+    hipLaunchKernelGGL((k_pt_resume<4, false>), pg, pb, 0, stream, *p);  // step 4 shades nothing
     if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_pt_resolve, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
     if ((e = end()) != hipSuccess) return e;

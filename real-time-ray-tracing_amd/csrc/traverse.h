@@ -207,6 +207,31 @@ RT_DEV void trav_setup(const SceneView& sc, F3 org, F3 dir, TravRay& r) {
     r.tr = make_triray(dir);
 }
 
+// Scene cull.  TraverseBvh's first iteration visits the TLAS root and ends the ray when neither
+// child box is hit (85 % of the default view's camera rays).  A plain float slab test against the
+// root's merged box grown by a margin — 1 % of its largest extent plus 0.01 — settles that case
+// without the conservative ray-box helper: the helper's rounding terms move a box face by
+// ulp-level amounts (origin offsets of ~5 * 2^-24 times the distance to the scene box, reciprocals
+// scaled by (1 +- 2^-23)^2), and the plain test's own rounding is of the same order, both many
+// orders below the margin.  So when even the grown box is missed, both children (inside the
+// merged box) are missed by the exact test, and the ray's result is that first iteration's:
+// a miss after one iteration and one node visit.  Any NaN leaves the ray to the full traversal.
+RT_DEV bool root_surely_missed(const SceneView& sc, F3 org, F3 dir) {
+    const Box b = node_merged(sc.tlas[0]);
+    const float m = 0.01f * fmx(fmx(b.mx.x - b.mn.x, b.mx.y - b.mn.y), b.mx.z - b.mn.z) + 0.01f;
+    const F3 inv = f3(safe_divide(1.0f, dir.x), safe_divide(1.0f, dir.y), safe_divide(1.0f, dir.z));
+    const float ax = (b.mn.x - m - org.x) * inv.x, bx = (b.mx.x + m - org.x) * inv.x;
+    const float ay = (b.mn.y - m - org.y) * inv.y, by = (b.mx.y + m - org.y) * inv.y;
+    const float az = (b.mn.z - m - org.z) * inv.z, bz = (b.mx.z + m - org.z) * inv.z;
+    const float tn = fmx(fmx(fmn(ax, bx), fmn(ay, by)), fmn(az, bz));
+    const float tf = fmn(fmn(fmx(ax, bx), fmx(ay, by)), fmx(az, bz));
+    const bool finite = tn == tn && tf == tf && ax == ax && bx == bx && ay == ay && by == by && az == az && bz == bz;
+    return finite && !(tn <= tf && tf > 0.0f);
+}
+
+// the state TraverseBvh ends in for a ray root_surely_missed settles (one root visit, no hit)
+RT_DEV void trav_root_miss(TravState& s);
+
 RT_DEV void trav_init(TravState& s) {
     s.t = kRayMax;
     s.hitIdx = -1;
@@ -217,6 +242,12 @@ RT_DEV void trav_init(TravState& s) {
     s.cBlas = false; s.cLeaf = false;
     s.cT = -kFltMax;
     s.visits = 0; s.tests = 0; s.dropped = 0; s.iters = 0;
+}
+
+RT_DEV void trav_root_miss(TravState& s) {
+    trav_init(s);
+    s.iters = 1;
+    s.visits = 1;
 }
 
 // One loop iteration; returns true when the stack ran empty (TestForFinish, traverse.h:88-105).
@@ -338,12 +369,16 @@ RT_DEV void finalize_hit(const SceneView& sc, F3 org, F3 dir, float t, int hitId
 }
 
 RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint32_t* stkA, float* stkT, int stride, HitInfo& out) {
-    TravRay r;
-    trav_setup(sc, org, dir, r);
     TravState s;
-    trav_init(s);
-    for (int it = 0; it < 1024; ++it)
-        if (trav_step(sc, r, s, stkA, stkT, stride)) break;
+    if (root_surely_missed(sc, org, dir)) {
+        trav_root_miss(s);
+    } else {
+        TravRay r;
+        trav_setup(sc, org, dir, r);
+        trav_init(s);
+        for (int it = 0; it < 1024; ++it)
+            if (trav_step(sc, r, s, stkA, stkT, stride)) break;
+    }
     finalize_hit(sc, org, dir, s.t, s.hitIdx, s.hitU, s.hitV, s.hitErrT, out);
     out.u = s.u;
     out.v = s.v;

@@ -10,7 +10,7 @@ LIBDIR   := $(PKG)/lib
 OBJDIR   := $(PKG)/lib/obj
 # -ffp-contract=off on host AND device: every expression rounds once per operation, as the
 # CPU oracle does (DESIGN.md §4 numerics policy).
-HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude -I$(CSRC)
+HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude -I$(CSRC) $(ABLFLAGS)
 CXXFLAGS := -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude -I$(CSRC)
 
 HIP_SRCS := $(wildcard $(CSRC)/*.hip)

@@ -369,7 +369,9 @@ int rt_frame_init(rt_context* ctx) {
         int dev = 0, cus = 0;
         HIP_TRY(ctx, hipGetDevice(&dev));
         HIP_TRY(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        const int perCu = rtk_trace_queue_blocks_per_cu();
+        int perCu = rtk_trace_queue_blocks_per_cu();
+        if (const char* a = getenv("RTX_TRACE_PER_CU"))  // tuning aid: fewer resident blocks per CU
+            if (atoi(a) > 0 && atoi(a) < perCu) perCu = atoi(a);
         ws.persistBlocks = (uint32_t)((cus > 0 ? cus : 256) * (perCu > 0 ? perCu : 4));
     }
     ALLOC(fr.colorB, P * 8);

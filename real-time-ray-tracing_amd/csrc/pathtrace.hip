@@ -73,14 +73,12 @@ struct PathVars {
 };
 
 RT_DEV void update_material(const PathTraceParams& P, RayState& rs) {
-    if (!rs.hit) {
-        rs.matType = MAT_SKY;
-        rs.matId = 99999;
-    } else {
-        if (P.materialOverride >= 0) rs.matId = P.materialOverride;
-        else rs.matId = (rs.objectIdx >= 0 && rs.objectIdx < (int)P.triCount) ? 3 : 6;  // SAFE_LOAD(.., 6)
-        rs.matType = (rs.matId >= 0 && rs.matId < 10) ? mat_type(rs.matId) : PERFECT_REFLECTION;
-    }
+    // values first, one store each: stores sunk behind a branch became a private array
+    const int id = P.materialOverride >= 0 ? P.materialOverride
+                   : (rs.objectIdx >= 0 && rs.objectIdx < (int)P.triCount) ? 3 : 6;  // SAFE_LOAD(.., 6)
+    const int type = (id >= 0 && id < 10) ? mat_type(id) : PERFECT_REFLECTION;
+    rs.matId = rs.hit ? id : 99999;
+    rs.matType = rs.hit ? type : MAT_SKY;
     if (rs.isShadowRay) {
         if ((rs.matType == EMISSIVE && rs.lightIdx == rs.objectIdx) || (rs.matType == MAT_SKY && rs.lightIdx == kEnvLightId))
             rs.hitLight = true;

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Bounce-ray (queue 3 / queue 4) traversal profile of a bench frame: the iteration distribution,
+SIMT efficiency per 64-ray wave and the queue tracer's kernel ms for several ray orders, through
+rt_trace_rays on the rays the frame itself queued.  Tuning aid."""
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "real-time-ray-tracing_amd")]
+
+
+def main():
+    import rtx
+
+    out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/q3"
+    os.makedirs(out, exist_ok=True)
+    W, H, S = 1920, 1080, 4
+    cfg = rtx.write_config(os.path.join(tempfile.mkdtemp(), "q.toml"), W, H, spp=S)
+    rt = rtx.RayTracer(W, H, cfg).init()
+    rt.set_delta_time(16.667)
+    for f in range(1, 4):
+        rt.build_bvh()
+        rt.path_trace(f)
+        rt.sync()
+        if f < 3:
+            rt.denoise_post(f)
+    q = rt.download("PT_QUEUE", np.uint32)
+    res = {}
+    for step, (no, nd, cnt) in {3: ("PT_Q3_ORIGINS", "PT_Q3_DIRS", q[0]), 4: ("PT_Q4_ORIGINS", "PT_Q4_DIRS", q[1])}.items():
+        n = int(cnt)
+        o = rt.download(no, np.float32).reshape(-1, 4)[:n, :3].copy()
+        d = rt.download(nd, np.float32).reshape(-1, 4)[:n, :3].copy()
+        t, tri, u, v, it, _ = rt.trace_rays(o, d, want_iters=True)
+        np.save(os.path.join(out, "q%d_iters.npy" % step), it)
+        np.save(os.path.join(out, "q%d_rays.npy" % step), np.concatenate([o, d], 1))
+        rng = np.random.default_rng(1)
+        orders = {"queue": np.arange(n), "shuffled": rng.permutation(n), "by_iters": np.argsort(-it.astype(np.int64), kind="stable")}
+        r = dict(rays=n, iters_sum=int(it.sum()), iters_max=int(it.max()),
+                 iters_q=[int(x) for x in np.quantile(it, [0.5, 0.9, 0.99, 0.999])])
+        for name, ordr in orders.items():
+            ii = it[ordr]
+            pad = (-n) % 64
+            wv = np.concatenate([ii, np.zeros(pad, ii.dtype)]).reshape(-1, 64)
+            ms = min(rt.trace_rays(o[ordr], d[ordr])[-1] for _ in range(5))
+            r[name] = dict(ms=round(ms, 4), simt_eff=round(float(ii.sum() / (wv.max(1).sum() * 64)), 4),
+                           wave_max_sum=int(wv.max(1).sum()))
+        res[step] = r
+        print(step, json.dumps(r), flush=True)
+    json.dump(res, open(os.path.join(out, "q_probe.json"), "w"), indent=1)
+    rt.cleanup()
+
+
+if __name__ == "__main__":
+    main()

@@ -13,11 +13,11 @@ constexpr int kSunW = 32, kSunH = 32, kSunSize = kSunW * kSunH;    // SUN_WIDTH/
 constexpr int kSkyScanBlock = 256, kSunScanBlock = 32;               // SKY/SUN_SCAN_BLOCK_SIZE
 constexpr int kTexLevels = 11, kTexSize = 1024;                      // soil textures, 11 mips
 
-// ushort4-texel offset of mip level l in the concatenated chain
+// ushort4-texel offset of mip level l in the concatenated chain: sum over k < l of (S >> k)^2
+// = 4 (S^2 - (S >> l)^2) / 3 for a power-of-two S (closed form: no loop on the texture path)
+static_assert((kTexSize & (kTexSize - 1)) == 0 && kTexSize <= 16384, "power-of-two texture size");
 __host__ __device__ constexpr uint32_t tex_level_offset(int l) {
-    uint32_t off = 0;
-    for (int k = 0; k < l; ++k) off += (uint32_t)(kTexSize >> k) * (uint32_t)(kTexSize >> k);
-    return off;
+    return 4u * ((uint32_t)(kTexSize * kTexSize) - (uint32_t)(kTexSize >> l) * (uint32_t)(kTexSize >> l)) / 3u;
 }
 constexpr uint32_t kTexTexels = tex_level_offset(kTexLevels);
 

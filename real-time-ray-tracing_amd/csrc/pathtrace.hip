@@ -150,7 +150,11 @@ RT_DEV void tri_plane(const PathTraceParams& P, F2 uv, float lod, F3 normal, F3 
     uv.x *= 0.5f;
     uv.y *= 0.5f;
     const F4 t0 = sample_lod(P.texAlbedo, uv, lod);
+    // scheduling fences: the gamma chain and the normal-map fetches would otherwise interleave,
+    // and the live texels of both maps set the register peak of the shading kernels
+    __builtin_amdgcn_sched_barrier(0);
     alb = f3(rt_powf(t0.x, 2.2f), rt_powf(t0.y, 2.2f), rt_powf(t0.z, 2.2f));
+    __builtin_amdgcn_sched_barrier(0);
     const F4 t1 = sample_lod(P.texNormal, uv, lod);
     const F3 n = f3(t1.x - 0.5f, t1.y - 0.5f, t1.z - 0.5f);
     const F3 u = cross(normal, w);
@@ -724,7 +728,7 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
 
 // Resumes the samples of queue kStep (3 or 4) once k_trace_queue has written their hits.
 template <int kStep, bool kMF>
-__global__ __launch_bounds__(256) void k_pt_resume(PathTraceParams P) {
+__global__ __launch_bounds__(256, kMF ? 2 : 3) void k_pt_resume(PathTraceParams P) {
     __shared__ uint32_t sob[256];
     __shared__ unsigned long long wgRays[4];
     // step 4 ends the path before any diffuse interaction: no light sampling there

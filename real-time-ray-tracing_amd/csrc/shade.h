@@ -42,15 +42,18 @@ RT_DEV bool isnan3(F3 v) { return v.x != v.x || v.y != v.y || v.z != v.z; }
 struct F4 { float x, y, z, w; };
 
 RT_DEV F4 load_u16x4(const uint2* tex, uint32_t texel) {
-    const uint2 q = tex[texel];
+    // a 32-bit byte offset from the (uniform) chain base: one VGPR per address, not two
+    const uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(tex) + texel * 8u);
     return F4{(float)(q.x & 0xFFFFu) / 65535.0f, (float)(q.x >> 16) / 65535.0f, (float)(q.y & 0xFFFFu) / 65535.0f,
               (float)(q.y >> 16) / 65535.0f};
 }
 
-RT_DEV int wrap_repeat(int v, int size) {  // BoundaryFuncRepeat, then the surface read's clamp
-    if (v >= size) v %= size;
-    if (v < 0) v = size - (-v) % size;  // `size` for multiples of -size
-    return v < size ? v : size - 1;
+// BoundaryFuncRepeat, then the surface read's clamp: v % size for v >= size, size - (-v) % size
+// for v < 0 — which is `size` for multiples of -size, clamped to size - 1.  Mip sizes are powers
+// of two, so both remainders are a mask.
+RT_DEV int wrap_repeat(int v, int size) {
+    const int r = v & (size - 1);
+    return (v < 0 && r == 0) ? size - 1 : r;
 }
 
 // SampleBicubicSmoothStep<Load2DFuncUshort4<Float4>, Float4, BoundaryFuncRepeat> on one mip level

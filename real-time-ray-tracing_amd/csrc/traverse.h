@@ -219,7 +219,9 @@ RT_DEV void trav_setup(const SceneView& sc, F3 org, F3 dir, TravRay& r) {
 RT_DEV bool root_surely_missed(const SceneView& sc, F3 org, F3 dir) {
     const Box b = node_merged(sc.tlas[0]);
     const float m = 0.01f * fmx(fmx(b.mx.x - b.mn.x, b.mx.y - b.mn.y), b.mx.z - b.mn.z) + 0.01f;
-    const F3 inv = f3(safe_divide(1.0f, dir.x), safe_divide(1.0f, dir.y), safe_divide(1.0f, dir.z));
+    // the hardware reciprocal (1 ulp): its error is as far below the margin as the helper's
+    // rounding; a zero component gives an infinity, and a 0 * inf NaN goes to the full traversal
+    const F3 inv = f3(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y), __builtin_amdgcn_rcpf(dir.z));
     const float ax = (b.mn.x - m - org.x) * inv.x, bx = (b.mx.x + m - org.x) * inv.x;
     const float ay = (b.mn.y - m - org.y) * inv.y, by = (b.mx.y + m - org.y) * inv.y;
     const float az = (b.mn.z - m - org.z) * inv.z, bz = (b.mx.z + m - org.z) * inv.z;

@@ -4,16 +4,15 @@
 // MSVC's libm on the host (e.g. bsdf.cuh:33, sky.cuh:167-191, kernel.cuh:105-109).
 // Neither is available here, and ROCm's ocml and glibc disagree in the last ulp, which
 // would flip Monte-Carlo decisions between the GPU kernels and the CPU oracle.  Every
-// transcendental on the hot path therefore goes through this header: each function is
-// evaluated in IEEE double with plain +,-,*,/ (no contraction: every translation unit that
-// includes this header is built with -ffp-contract=off) and rounded once to float.  The results are faithfully rounded
-// (correctly rounded in all but rare ties) and identical on the GPU and on the host, so
-// kernel-vs-oracle parity can be tested bit-exact.
+// transcendental on the hot path therefore goes through this header, written with plain
+// +,-,*,/, explicit fma and sqrt only (no contraction: every translation unit that includes this
+// header is built with -ffp-contract=off), so each function returns the same bits on gfx950 and
+// on x86-64 and kernel-vs-oracle parity can be tested bit-exact.
 //
-// Cost: the polynomial cores are Horner chains in double with the shortest series whose
-// truncation error stays below 1e-13 relative on the reduced range, far inside the 2^-24 a
-// faithful float result needs.  The denoiser evaluates powf/expf per filter tap, so these
-// chains sit on its critical path.
+// Two families: float cores (sin/cos for |x| <= 64, atan, atan2, exp, log, pow — the per-sample
+// and per-tap hot trig) in float arithmetic with error-free float-pair steps, faithful (within
+// 1 ulp; tests/test_rtmath.py); and double-precision cores rounded once to float (correctly
+// rounded in all but rare ties) for the rest (asin/acos, tan, large sin/cos arguments).
 //
 // sqrtf and float division stay native: both are correctly rounded on both sides
 // (hipcc's default -fhip-fp32-correctly-rounded-divide-sqrt, SSE2 on the host).
@@ -362,6 +361,103 @@ RT_HD void log2_pair(float x, float& hi, float& lo) {
     lo = lo - (t - hi);
     hi = t;
 }
+
+// ---- float cores of sin / cos / atan / atan2 (the path tracer's per-sample trig: the aperture
+// disk, cosine-weighted and light directions, the sky lookup's longitude).  Float arithmetic with
+// explicit fmaf and error-free float-pair steps where the last bits are decided, so the result is
+// the same on the GPU and the host and faithful (within 1 ulp of the exact value; the double path
+// above is kept for arguments outside the reduced range).  Constants: pi/2 = C1 + C2 + C3 + C4
+// with C1..C3 of 18 significant bits; musl's __sindf / __cosdf kernels (relative error < 2^-37 on
+// |r| <= pi/4) rounded to float; atan(i/8) and pi/2 - atan(i/8) as float pairs.
+constexpr float kPio2C1 = 0x1.921f8p+0f, kPio2C2 = 0x1.aa22p-19f, kPio2C3 = 0x1.68c2p-39f, kPio2C4 = 0x1.a62634p-58f;
+constexpr float kSinS1 = -0x1.555556p-3f, kSinS2 = 0x1.111108p-7f, kSinS3 = -0x1.a00f9ep-13f, kSinS4 = 0x1.6cd878p-19f;
+constexpr float kCosC0d = 0x1.79d0cp-29f, kCosC1 = 0x1.55553ep-5f, kCosC2 = -0x1.6c087ep-10f, kCosC3 = 0x1.99342ep-16f;  // kCosC0d = C0 + 1/2
+constexpr float kPiHi = 0x1.921fb6p+1f, kPiLo = -0x1.777a5cp-24f, kPio2Hi = 0x1.921fb6p+0f, kPio2Lo = -0x1.777a5cp-25f;
+
+RT_HD void two_sum(float a, float b, float& s, float& e) {
+    s = a + b;
+    const float bb = s - a;
+    e = (a - (s - bb)) + (b - bb);
+}
+
+// sin x, cos x for |x| <= 64 (|k| <= 41: k C1, k C2, k C3 are exact, C1..C3 having 18 significant
+// bits), the reduced argument x - k pi/2 carried as the float pair rh + rl
+RT_HD void sincosf_fcore(float x, float& sn, float& cs) {
+    const float k = __builtin_rintf(x * 0.636619772f);
+    const float r1 = f_fma(-k, kPio2C1, x);  // exact
+    float rh, rl, e;
+    two_sum(r1, -(k * kPio2C2), rh, rl);
+    two_sum(rh, -(k * kPio2C3), rh, e);
+    rl = f_fma(-k, kPio2C4, rl + e);
+    two_sum(rh, rl, rh, rl);  // renormalise: |rl| <= ulp(rh) / 2
+    const float z = rh * rh;
+    const float zl = f_fma(rh, rh, -z);                // z + zl = rh^2 exactly
+    const float hz = 0.5f * z;
+    // sin(rh + rl) = rh + rh z S(z) + rl (1 - z/2)
+    const float sp = z * f_fma(z, f_fma(z, f_fma(z, kSinS4, kSinS3), kSinS2), kSinS1);
+    const float s = rh + f_fma(rh, sp, rl * (1.0f - hz));
+    // cos(rh + rl) = (1 - z/2) + [z (C0 + 1/2) + z^2 C(z) - zl/2 - rh rl], 1 - z/2 split exactly
+    const float w = 1.0f - hz;
+    const float we = (1.0f - w) - hz;
+    const float cp = f_fma(z * z, f_fma(z, f_fma(z, kCosC3, kCosC2), kCosC1), z * kCosC0d);
+    const float c = w + (((we - 0.5f * zl) + cp) - rh * rl);
+    const int q = (int)k & 3;
+    sn = q == 0 ? s : q == 1 ? c : q == 2 ? -s : -c;
+    cs = q == 0 ? c : q == 1 ? -s : q == 2 ? -c : s;
+}
+
+// entry i in {0, 2..8} of a 9-entry table, by a select chain (no indexed private array)
+RT_HD float tab9(int i, float v0, float v2, float v3, float v4, float v5, float v6, float v7, float v8) {
+    return i == 8 ? v8 : i == 7 ? v7 : i == 6 ? v6 : i == 5 ? v5 : i == 4 ? v4 : i == 3 ? v3 : i == 2 ? v2 : v0;
+}
+
+// atan(num / den) as hi + lo (hi a table value, lo the rest) for 0 <= num, den finite, not both 0:
+// with a <= b the smaller and larger of the two, atan(a / b) = atan(c) + atan(t),
+// t = (a - c b) / (b + c a), c = i / 8 nearest to a / b (i = 1 taken as 0, so that |atan t| stays
+// below a third of the result when i > 0), and the odd series of atan t to t^13 (|t| < 3/16).
+RT_HD void atan_ratio_f(float num, float den, float& hi, float& lo) {
+    const bool swap = num > den;
+    const float a = swap ? den : num, b = swap ? num : den;
+    int i = (int)((a / b) * 8.0f + 0.5f);
+    if (i == 1) i = 0;
+    const float c = (float)i * 0.125f;
+    const float t = f_fma(-c, b, a) / f_fma(c, a, b);
+    const float t2 = t * t;
+    float p = 1.0f / 13.0f;
+    p = f_fma(p, t2, -1.0f / 11.0f);
+    p = f_fma(p, t2, 1.0f / 9.0f);
+    p = f_fma(p, t2, -1.0f / 7.0f);
+    p = f_fma(p, t2, 1.0f / 5.0f);
+    p = f_fma(p, t2, -1.0f / 3.0f);
+    const float at = f_fma(t * t2, p, t);
+    // atan(i/8) and pi/2 - atan(i/8) as float pairs
+    const float th = swap ? tab9(i, 0x1.921fb6p+0f,
+                            0x1.5368cap+0f, 0x1.36475p+0f, 0x1.1b6e1ap+0f, 0x1.031f58p+0f, 0x1.dac67p-1f, 0x1.b434eep-1f, 0x1.921fb6p-1f)
+                          : tab9(i, 0.0f,
+                            0x1.f5b76p-3f, 0x1.6f6194p-2f, 0x1.dac67p-2f, 0x1.1e00bap-1f, 0x1.4978fap-1f, 0x1.700a7cp-1f, 0x1.921fb6p-1f);
+    const float tl = swap ? tab9(i, -0x1.777a5cp-25f,
+                            -0x1.5c2c6p-25f, 0x1.e57aaep-27f, -0x1.a28838p-25f, -0x1.ab5242p-28f, 0x1.586ed4p-27f, 0x1.8809fep-28f, -0x1.777a5cp-26f)
+                          : tab9(i, 0.0f,
+                            -0x1.b4dfc8p-29f, 0x1.e4defp-30f, 0x1.586ed4p-28f, 0x1.7bdfd6p-26f, 0x1.934f7p-28f, 0x1.5e118cp-27f, -0x1.777a5cp-26f);
+    hi = th;
+    lo = swap ? tl - at : tl + at;
+}
+
+RT_HD float atan2f_fcore(float y, float x) {
+    const uint32_t yb = float_to_bits(y), xb = float_to_bits(x);
+    const float ay = bits_to_float(yb & 0x7FFFFFFFu), ax = bits_to_float(xb & 0x7FFFFFFFu);
+    float hi, lo;
+    atan_ratio_f(ay, ax, hi, lo);
+    float r;
+    if (xb >> 31) {  // pi - atan(|y| / |x|)
+        float s, e;
+        two_sum(kPiHi, -hi, s, e);
+        r = s + ((e + kPiLo) - lo);
+    } else {
+        r = hi + lo;
+    }
+    return (yb >> 31) ? -r : r;
+}
 }  // namespace rtm
 
 RT_HD float rt_exp2f(float x) {
@@ -417,20 +513,37 @@ RT_HD void rt_sincos_d(float x, double& s, double& c) {
     if (rtm::d_abs((double)x) <= 1e5) rtm::sincosf_core((double)x, s, c);  // NaN and inf fail the test
     else rtm::sincosd((double)x, s, c);
 }
-RT_HD float rt_sinf(float x) { double s, c; rt_sincos_d(x, s, c); return (float)s; }
-RT_HD float rt_cosf(float x) { double s, c; rt_sincos_d(x, s, c); return (float)c; }
 RT_HD void rt_sincosf(float x, float* s, float* c) {
-    double sd, cd; rt_sincos_d(x, sd, cd); *s = (float)sd; *c = (float)cd;
+    if (__builtin_fabsf(x) <= 64.0f) {  // NaN and inf fail the test
+        rtm::sincosf_fcore(x, *s, *c);
+        return;
+    }
+    double sd, cd;
+    rt_sincos_d(x, sd, cd);
+    *s = (float)sd;
+    *c = (float)cd;
 }
+RT_HD float rt_sinf(float x) { float s, c; rt_sincosf(x, &s, &c); return s; }
+RT_HD float rt_cosf(float x) { float s, c; rt_sincosf(x, &s, &c); return c; }
 RT_HD float rt_tanf(float x) { double s, c; rt_sincos_d(x, s, c); return (float)(s / c); }
 RT_HD float rt_atanf(float x) {
     if (x != x) return x;
-    const double a = (double)x;
-    if (rtm::d_abs(a) == rtm::d_inf()) return a > 0 ? 1.57079632679489661923f : -1.57079632679489661923f;
-    const double r = a == 0.0 ? 0.0 : rtm::atan_ratio(rtm::d_abs(a), 1.0);
-    return (float)(a < 0.0 ? -r : (a == 0.0 ? a : r));
+    if (x == 0.0f) return x;
+    const float ax = __builtin_fabsf(x);
+    if (ax == rtm::bits_to_float(0x7F800000u)) return x > 0.0f ? 1.57079632679489661923f : -1.57079632679489661923f;
+    float hi, lo;
+    rtm::atan_ratio_f(ax, 1.0f, hi, lo);
+    const float r = hi + lo;
+    return x < 0.0f ? -r : r;
 }
-RT_HD float rt_atan2f(float y, float x) { return (float)rtm::atan2f_core((double)y, (double)x); }
+RT_HD float rt_atan2f(float y, float x) {
+    const float ay = __builtin_fabsf(y), ax = __builtin_fabsf(x);
+    // finite, not both zero and neither zero: the float core; the rest (zeros, infinities, NaN)
+    // take the double path's C99 special cases
+    if (ay > 0.0f && ax > 0.0f && ay < rtm::bits_to_float(0x7F800000u) && ax < rtm::bits_to_float(0x7F800000u))
+        return rtm::atan2f_fcore(y, x);
+    return (float)rtm::atan2f_core((double)y, (double)x);
+}
 RT_HD float rt_asinf(float x) {
     double d = (double)x;
     if (!(d >= -1.0 && d <= 1.0)) return (float)rtm::d_nan();

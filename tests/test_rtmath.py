@@ -74,3 +74,29 @@ def test_rtmath_subnormal_range(oracle):
     for x in (np.float32(2.0) ** rng.uniform(-149, -126, 2000)).astype(np.float32):
         worst = max(worst, ulp_err(oracle.rtmath("log2", float(x)), np.log2(np.float64(x))))
     assert worst <= 1, worst
+
+
+def test_rtmath_float_trig_cores_near_quadrant_boundaries(oracle):
+    """sin/cos through the float core (|x| <= 64) stay faithful where the reduced argument is
+    tiny: floats within a few hundred ulps of k pi/2, k = -40..40 (the float-pair reduction)."""
+    worst = 0
+    for k in range(-40, 41, 3):
+        c = np.float32(k * np.pi / 2)
+        for d in range(-60, 61, 7):
+            x = (c.view(np.int32) + np.int32(d)).view(np.float32)
+            if abs(float(x)) > 64:
+                continue
+            worst = max(worst, ulp_err(oracle.rtmath("sin", float(x)), np.sin(np.float64(x))))
+            worst = max(worst, ulp_err(oracle.rtmath("cos", float(x)), np.cos(np.float64(x))))
+    assert worst <= 1, worst
+
+
+def test_rtmath_atan2_quadrants_and_ratios(oracle):
+    """atan2 through the float core over all four quadrants and |y/x| from 1e-6 to 1e6."""
+    rng = np.random.default_rng(13)
+    worst = 0
+    for _ in range(3000):
+        x = np.float32(rng.choice([-1, 1]) * 10.0 ** rng.uniform(-3, 3))
+        y = np.float32(rng.choice([-1, 1]) * 10.0 ** rng.uniform(-3, 3))
+        worst = max(worst, ulp_err(oracle.rtmath("atan2", float(y), float(x)), np.arctan2(np.float64(y), np.float64(x))))
+    assert worst <= 1, worst

@@ -369,10 +369,20 @@ int rt_frame_init(rt_context* ctx) {
         int dev = 0, cus = 0;
         HIP_TRY(ctx, hipGetDevice(&dev));
         HIP_TRY(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        int perCu = rtk_trace_queue_blocks_per_cu();
-        if (const char* a = getenv("RTX_TRACE_PER_CU"))  // tuning aid: fewer resident blocks per CU
-            if (atoi(a) > 0 && atoi(a) < perCu) perCu = atoi(a);
-        ws.persistBlocks = (uint32_t)((cus > 0 ? cus : 256) * (perCu > 0 ? perCu : 4));
+        const int perCu = rtk_trace_queue_blocks_per_cu();
+        if (cus <= 0) cus = 256;
+        ws.persistBlocks = (uint32_t)(cus * (perCu > 0 ? perCu : 4));
+        // the queue tracers run one block per CU below their residency (5 at 32 KiB of LDS stack
+        // each): a bounce queue then holds more rays than lanes, so lanes refill as rays finish,
+        // and the CUs keep room for the denoise and next-frame waves beside the traversal tail
+        // (measured: DESIGN.md §7)
+        int tracePerCu = perCu > 2 ? perCu - 2 : 1, trace4PerCu = 1;
+        if (const char* a = getenv("RTX_TRACE_PER_CU"))  // tuning aids
+            if (atoi(a) > 0 && atoi(a) <= perCu) tracePerCu = atoi(a);
+        if (const char* a = getenv("RTX_TRACE4_PER_CU"))
+            if (atoi(a) > 0 && atoi(a) <= perCu) trace4PerCu = atoi(a);
+        ws.traceBlocks = (uint32_t)(cus * tracePerCu);
+        ws.trace4Blocks = (uint32_t)(cus * trace4PerCu);
     }
     ALLOC(fr.colorB, P * 8);
     ALLOC(fr.accum, P * 8);

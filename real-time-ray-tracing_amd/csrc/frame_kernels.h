@@ -96,6 +96,8 @@ struct PtWorkspace {
     uint32_t* fetch;            // [2][8 parts x 16]: k_trace_queue fetch counters, 64 B apart
     uint32_t cap;               // entries per queue (= rows * W * spp)
     uint32_t persistBlocks;     // grid of the persistent queue kernels
+    uint32_t traceBlocks;       // grid of the queue tracer of queue 3 (k_trace_queue)
+    uint32_t trace4Blocks;      // ... of queue 4 (a short queue: a few percent of queue 3)
     int glossy;                 // materials can be glossy: steps 1-2 may trace (materialOverride)
     int microfacet;             // materials can be the microfacet one (materialOverride 4): GGX compiled in
     uint32_t* itersOut = nullptr;  // optional [cap]: traversal iterations per queue entry (rt_trace_rays)

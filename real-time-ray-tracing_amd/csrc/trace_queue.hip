@@ -160,7 +160,9 @@ extern "C" int rtk_trace_queue_blocks_per_cu() {
 }
 
 extern "C" hipError_t rtk_launch_trace_queue(const PathTraceParams* p, int step, hipStream_t stream) {
-    const dim3 grid(p->ws.persistBlocks);
+    const uint32_t blocks = step == 3 ? p->ws.traceBlocks : p->ws.trace4Blocks;
+    if (blocks < 1) return hipErrorInvalidValue;
+    const dim3 grid(blocks);
     if (step == 3) hipLaunchKernelGGL(k_trace_queue<3>, grid, dim3(kTraceBlock), 0, stream, *p);
     else hipLaunchKernelGGL(k_trace_queue<4>, grid, dim3(kTraceBlock), 0, stream, *p);
     return hipGetLastError();

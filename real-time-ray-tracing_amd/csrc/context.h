@@ -188,8 +188,9 @@ struct rt_context {
     // at the next host read / denoise call, whichever comes first
     bool postPending = false;
     int postPendingSet = 0;
-    int overlapAfter = 1;  // after k_pt_shade0: measured best with cameraAfter = 3 at 1-8 ranks
-    int cameraAfter = 3;   // the next frame's camera rays start after this frame's resume<3>
+    int overlapAfter = 1;  // after k_pt_shade0: measured best at 1-8 ranks
+    int cameraAfter = 3;   // the next frame's camera rays start after this frame's kernel 2 (queue-3
+                           // trace) on 1-2 GPUs, kernel 3 (resume<3>) on more (rt_set_post_stream)
     hipEvent_t cameraGate = nullptr;
     bool cameraGated = false;
     DenoisePostParams postParams{};

@@ -907,6 +907,9 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
     if (!ctx->overlapEv) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->overlapEv, hipEventDisableTiming));
     if (!ctx->cameraGate) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->cameraGate, hipEventDisableTiming));
     ctx->cameraGated = false;
+    // the next frame's camera rays: beside this frame's queue-3 traversal tail on one or two
+    // GPUs, after its resume<3> on more, where the per-rank tail is shorter
+    ctx->cameraAfter = ctx->stripCount <= 2 ? 2 : 3;
     if (const char* a = getenv("RTX_OVERLAP_AFTER")) ctx->overlapAfter = atoi(a);  // tuning aids
     if (const char* a = getenv("RTX_CAMERA_AFTER")) ctx->cameraAfter = atoi(a);
     ctx->postStream = (hipStream_t)stream;

@@ -12,6 +12,7 @@ Each pass directory holds one `rocprofv3 --pmc ... --kernel-trace --output-forma
   wait_inst_any_frac = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES  (share of wave time waiting to issue)
   valu_busy_frac     = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES"""
 import collections
+import re
 import csv
 import glob
 import json
@@ -23,8 +24,12 @@ STAGE = ("k_pt_camera", "k_pt_shade0", "k_trace_queue<3>", "k_pt_resume<3>", "k_
 
 
 def short(name):
+    """Stage name of a kernel symbol: the boolean template arguments (material-table variants)
+    dropped, the queue step kept: k_pt_shade0<false, false> -> k_pt_shade0, k_pt_resume<3, false>
+    -> k_pt_resume<3>."""
     n = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
-    return n.replace("<true>", "").replace("<false>", "")
+    n = re.sub(r"<(\d+)(, (true|false))+>", r"<\1>", n)
+    return re.sub(r"<(true|false)(, (true|false))*>", "", n)
 
 
 def main():

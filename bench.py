@@ -20,10 +20,11 @@ fresh single-GPU context and compares the last frame bit for bit (--no-self-chec
 mismatch exits non-zero.
 
 N ranks (torch.distributed.run, one per GPU): each rank rebuilds the BVH, path traces its rows
-of the frame (16-row blocks dealt round-robin), the ranks' G-buffer blocks are all-gathered over
-RCCL (rtx/dist.py), and each rank denoises only its own contiguous 64-row-block strip of the
-assembled frame (plus the halo its passes read), exchanging the histogram (all-reduce) and its
-rows of the accumulation, history (the final HDR) and RGBA8 buffers (all-gather) with the others.
+of the frame (16-row blocks dealt round-robin), the G-buffer blocks each rank's denoise reads are
+sent to it in one RCCL all-to-all (its strip plus the halo its passes read: rtx/dist.py
+StripGather.exchange), and each rank denoises only its own contiguous 64-row-block strip,
+exchanging the histogram (all-reduce) and its rows of the accumulation, history (the final HDR)
+and RGBA8 buffers (all-gather) with the others.
 Rank 0's self-check compares its frame with a single-GPU serial render.  Total work per frame is
 fixed as N grows ("strong" scaling).  Timing: barrier + device sync on both sides of exactly
 K frames, max over ranks; value = rays of all ranks / that time.
@@ -282,9 +283,9 @@ def main():
         "config": {"workload": "BASELINE config 3: %dx%d, %d spp path trace + SVGF denoise + auto-exposure/"
                                "tone map, per-frame LBVH rebuild" % (W, H, S),
                    "width": W, "height": H, "spp": S,
-                   "parallelism": ("interleaved 16-row strips x%d + RCCL all-gather of G-buffers, strip-local "
-                                   "denoise (64-row blocks) with histogram all-reduce and accumulation/history/RGBA8 "
-                                   "row all-gathers" % world if world > 1
+                   "parallelism": ("interleaved 16-row strips x%d + RCCL all-to-all of the G-buffer rows each "
+                                   "rank's strip-local denoise reads (64-row blocks + halo), histogram all-reduce "
+                                   "and accumulation/history/RGBA8 row all-gathers" % world if world > 1
                                    else "single GPU")
                                   + ("; pipelined frames: denoise/post of f-1 and LBVH build + camera rays of "
                                      "f+1 on their own streams beside the trace kernels of f" if pipeline
@@ -301,6 +302,12 @@ def main():
     counters = rt.download("PT_QUEUE", np.uint32).copy()  # per-kernel work of this detail launch
     pmc = pmc_kernels()
     matches = pmc is not None and pmc.get("workload_key") == "%dx%dx%d" % (W, H, S) and world == 1
+    if world > 1:  # what each rank receives per frame over the collectives (the G-buffer rows its
+        # strip-local denoise reads, its peers' accumulation / history / RGBA8 rows, 256 B histogram)
+        g = fp.gather.exchange_bytes_per_frame(fp.need) if fp.need else fp.gather.bytes_per_frame()
+        r_ = fp.denoise.bytes_per_frame() if fp.denoise else 0
+        result["comm_bytes_per_rank_per_frame"] = {"gbuffer_rows": int(g), "denoise_rows": int(r_),
+                                                   "gbuffer_allgather_would_be": int(fp.gather.bytes_per_frame())}
     fk_iters = 20
     kernels_ms = rt.time_frame_kernels(last + 2, fk_iters)
     per = kernel_roofline(counters, W, rows, S, kernels_ms, pmc, matches)

@@ -181,6 +181,8 @@ typedef struct rt_info {
     uint32_t spp;               /* samples (reference PathTrace evaluations) per frame */
     int32_t gbufferSet;         /* G-buffer set the last rt_path_trace wrote (0..2, see rt_set_post_stream) */
     int32_t denoiseRowBegin, denoiseRowEnd; /* rows of a strip-local denoise (rt_set_collective_hook) */
+    int32_t gbufferRowBegin, gbufferRowEnd; /* G-buffer rows the next denoise reads: its strip plus
+                                               halo when it is strip-local, else the whole frame */
 } rt_info;
 
 int rt_get_info(const rt_context* ctx, rt_info* out);

@@ -68,6 +68,17 @@ inline bool denoise_rows(uint32_t height, uint32_t nStrips, uint32_t strip, uint
     return true;
 }
 
+// G-buffer rows a strip-local denoise of [a, b) reads: its passes run on the strip's 16-row tiles
+// widened by at most 4 tiles (TemporalFilter, denoise.hip tile_range) and read the G-buffers at
+// most one row beyond those (3x3 taps; the wider stencils run on narrower tile ranges), so one
+// more tile on each side covers every read.  Multi-GPU hosts move only these rows between ranks.
+constexpr uint32_t kGbufHaloTiles = 5;
+inline void gbuffer_rows(uint32_t height, uint32_t a, uint32_t b, uint32_t& lo, uint32_t& hi) {
+    const uint32_t t0 = a / 16, t1 = (b + 15) / 16;
+    lo = t0 > kGbufHaloTiles ? (t0 - kGbufHaloTiles) * 16 : 0;
+    hi = (t1 + kGbufHaloTiles) * 16 < height ? (t1 + kGbufHaloTiles) * 16 : height;
+}
+
 struct TracePrimaryParams {
     TraceCamera cam;
     uint32_t width, height;

@@ -442,6 +442,10 @@ int rt_get_info(const rt_context* ctx, rt_info* out) {
     if (ctx->stripCount > 1) denoise_rows((uint32_t)ctx->renderH, (uint32_t)ctx->stripCount, (uint32_t)ctx->stripIndex, a, b);
     out->denoiseRowBegin = (int32_t)a;
     out->denoiseRowEnd = (int32_t)b;
+    uint32_t sa = 0, sb = 0, lo = 0, hi = (uint32_t)ctx->renderH;
+    if (ctx->inited && strip_local_denoise(ctx, sa, sb)) gbuffer_rows((uint32_t)ctx->renderH, sa, sb, lo, hi);
+    out->gbufferRowBegin = (int32_t)lo;
+    out->gbufferRowEnd = (int32_t)hi;
     return RT_OK;
 }
 

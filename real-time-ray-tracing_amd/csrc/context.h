@@ -243,6 +243,7 @@ int dalloc(rt_context* ctx, T** p, size_t bytes) {
 }
 int rt_frame_init(rt_context* ctx);  // frame.cpp: sky tables, textures, G-buffers
 int sync_streams(rt_context* ctx);   // frame.cpp: context, post and side streams
+bool strip_local_denoise(const rt_context* ctx, uint32_t& a, uint32_t& b);  // frame.cpp: next denoise's rows
 extern "C" int copy_rgba_out(rt_context* ctx, void* dst);  // frame.cpp: the last frame's RGBA8 to host memory
 extern "C" size_t rt_alloc_bytes(const rt_context* ctx, int name);  // frame.cpp: allocated size of a render buffer
 extern "C" void bvh_select(rt_context* ctx, int k);  // context.cpp: point the dTriPos.. views at bvh[k]

@@ -202,6 +202,23 @@ void select_gbuffers(FrameResources& fr) {
 
 // the denoise/post chain of one frame on stream s: phase 0, the histogram exchange, phase 1, the
 // rows exchange (the exchanges only for a strip-local denoise, through the caller's hook)
+// Whether this context's next denoise is strip-local (multi-GPU: a collective hook, and none of
+// the passes that read the whole frame), and its rows [a, b) (the whole frame otherwise).
+bool strip_local_denoise(const rt_context* ctx, uint32_t& a, uint32_t& b) {
+    const rt_render_pass_settings& ps = ctx->params.pass;
+    const uint32_t H = (uint32_t)ctx->renderH;
+    a = 0;
+    b = H;
+    const bool strip = ctx->stripCount > 1 && ctx->hook != nullptr && !ps.enableNoiseLevelVisualize &&
+                       !(ps.enablePostProcess && (ps.enableBloomEffect || ps.enableLensFlare)) &&
+                       ctx->screenW == ctx->renderW && ctx->screenH == ctx->renderH;
+    uint32_t sa = 0, sb = H;
+    if (!strip || !denoise_rows(H, (uint32_t)ctx->stripCount, (uint32_t)ctx->stripIndex, sa, sb)) return false;
+    a = sa;
+    b = sb;
+    return true;
+}
+
 int run_denoise(rt_context* ctx, DenoisePostParams& p, hipStream_t s) {
     rt_strip_exchange x{p.frameNum, (int32_t)p.rowA, (int32_t)p.rowB, p.histOutSet};
     HIP_TRY(ctx, rtk_denoise_phase(&p, s, 0));
@@ -648,13 +665,10 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.ty0 = 0;
     p.ty1 = (int)((p.H + 15) / 16);
     {  // multi-GPU strip-local denoise: only with a collective hook, and for the passes it covers
-        const bool strip = ctx->stripCount > 1 && ctx->hook != nullptr && !ps.enableNoiseLevelVisualize &&
-                           !(ps.enablePostProcess && (ps.enableBloomEffect || ps.enableLensFlare)) &&
-                           ctx->screenW == ctx->renderW && ctx->screenH == ctx->renderH;
         uint32_t a = 0, b = p.H;
-        p.stripLocal = strip && denoise_rows(p.H, (uint32_t)ctx->stripCount, (uint32_t)ctx->stripIndex, a, b) ? 1 : 0;
-        p.rowA = p.stripLocal ? a : 0;
-        p.rowB = p.stripLocal ? b : p.H;
+        p.stripLocal = strip_local_denoise(ctx, a, b) ? 1 : 0;
+        p.rowA = a;
+        p.rowB = b;
     }
     p.histDepth = fr.histDepth;
     p.noise8 = fr.noise8;

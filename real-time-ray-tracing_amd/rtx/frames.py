@@ -6,9 +6,10 @@ bench.py times exactly this object's ``frame`` calls and the parity tests run th
 * the renderer's stages go to a high-priority torch stream (the trace chain is the critical
   path) and, pipelined, the denoise/post chain of frame f to a low-priority second stream
   (rt_set_post_stream) beside the trace kernels of frame f+1;
-* with N ranks (rtx/dist.py) every rank path traces its interleaved row blocks, the G-buffers
-  are all-gathered (RCCL on its own stream when the backend is nccl, after a host sync with
-  gloo), and each rank denoises its own contiguous rows of the assembled frame (StripDenoise:
+* with N ranks (rtx/dist.py) every rank path traces its interleaved row blocks, the G-buffer
+  rows each rank's denoise reads are exchanged (RCCL on its own stream when the backend is nccl,
+  after a host sync with gloo: an all-to-all of the strip-plus-halo rows, or the all-gather when
+  every rank denoises the whole frame), and each rank denoises its own contiguous rows (StripDenoise:
   the histogram all-reduce and the accumulation / history / RGBA8 row all-gathers the renderer
   asks for through its collective hook; strip_denoise=False denoises the whole frame on every rank).
 """
@@ -21,7 +22,7 @@ class FramePipeline:
         import torch
 
         import rtx
-        from rtx.dist import StripDenoise, StripGather
+        from rtx.dist import StripDenoise, StripGather, gbuffer_rows
 
         self.rt, self.device, self.pipelined = rt, device, pipelined
         self.world, self.rank = world, rank
@@ -45,6 +46,9 @@ class FramePipeline:
         info = rt.info()
         self.denoise = (StripDenoise(info.renderWidth, info.renderHeight, world, rank, device, rt)
                         if (world > 1 and strip_denoise) else None)
+        # with the strip-local denoise each rank receives only the G-buffer rows it reads
+        self.need = ([gbuffer_rows(info.renderHeight, world, r) for r in range(world)]
+                     if self.denoise is not None else None)
 
     def frame(self, f: int, hdr: bool = False):
         """LBVH rebuild, path trace, (gather,) denoise + post of frame f, enqueued asynchronously."""
@@ -54,13 +58,20 @@ class FramePipeline:
         rt.build_bvh()
         rt.path_trace(f)
         if self.gather is not None:
+            move = self.gather.gather
+            if self.need is not None:  # strip-local denoise this frame: only the rows it reads
+                i = rt.info()
+                if (i.gbufferRowBegin, i.gbufferRowEnd) != (0, i.renderHeight):
+                    if (i.gbufferRowBegin, i.gbufferRowEnd) != self.need[self.rank]:
+                        raise RuntimeError("renderer and host disagree on the strip's G-buffer rows")
+                    move = lambda: self.gather.exchange(self.need)  # noqa: E731
             if self.gs is not None:
                 self.gs.wait_stream(torch.cuda.current_stream(self.device))  # this frame's path trace
                 with torch.cuda.stream(self.gs):
-                    self.gather.gather()
+                    move()
             else:
                 rt.sync()  # gloo copies through the host: the strip must be complete
-                self.gather.gather()
+                move()
         rt.denoise_post(f, hdr)
 
     def finish(self):

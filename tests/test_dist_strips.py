@@ -187,3 +187,70 @@ def test_strip_denoise_exchange(tmp_path, world):
             assert np.array_equal(d[k], d["full_" + k]), (r, k)
         assert (d["h0"] == 0x55).all()
         assert np.array_equal(d["hist"], np.arange(64) * sum(range(1, world + 1)))
+
+
+def exchange_worker(rank, world, port, result_dir):
+    import torch
+    import torch.distributed as dist
+
+    from rtx.dist import gbuffer_rows
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        We, He = 8, 1080
+        sg = StripGather(We, He, world, rank, torch.device("cpu"), sets=2)
+        need = [gbuffer_rows(He, world, r) for r in range(world)]
+        full = {}
+        for name, bpp in GBUFFERS:
+            rows = len(sg.sets[1][name]) // (We * bpp)
+            v = (np.arange(rows * We * bpp, dtype=np.int64) * 7 + len(name)) % 251
+            full[name] = v.astype(np.uint8)
+            t = sg.sets[1][name]
+            t.fill_(0xEE)
+            for y0, n in strip_blocks(He, world, rank):  # this rank path traced its own blocks
+                lo, hi = y0 * We * bpp, (y0 + n) * We * bpp
+                t[lo:hi] = torch.from_numpy(full[name][lo:hi].copy())
+            sg.sets[0][name].fill_(0x11)
+        sg.exchange(need, gbuffer_set=1)
+        np.savez(os.path.join(result_dir, "x%d.npz" % rank), recv=np.array(sg.exchange_bytes_per_frame(need)),
+                 **{name: sg.sets[1][name].numpy() for name, _ in GBUFFERS},
+                 **{"set0_" + name: sg.sets[0][name].numpy() for name, _ in GBUFFERS},
+                 **{"full_" + name: full[name] for name, _ in GBUFFERS})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_strip_exchange_delivers_the_rows_each_rank_reads(tmp_path, world):
+    """StripGather.exchange (gloo, CPU): after the all-to-all every rank holds the whole frame's
+    G-buffers in the rows gbuffer_rows says its strip-local denoise reads, its own blocks
+    everywhere, and nothing else was written; the other G-buffer set is untouched; each rank
+    receives well under the all-gather's (N - 1) / N of the frame."""
+    import torch.multiprocessing as mp
+
+    from rtx.dist import gbuffer_rows
+
+    assert gbuffer_rows(1080, 8, 0) == (0, 208) and gbuffer_rows(1080, 8, 7) == (816, 1080)
+    mp.start_processes(exchange_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
+    We, He = 8, 1080
+    for r in range(world):
+        d = np.load(tmp_path / ("x%d.npz" % r))
+        lo, hi = gbuffer_rows(He, world, r)
+        mine = np.zeros(He, bool)
+        for y0, n in strip_blocks(He, world, r):
+            mine[y0:y0 + n] = True
+        frame_bytes = 0
+        for name, bpp in GBUFFERS:
+            got = d[name][:He * We * bpp].reshape(He, We * bpp)
+            want = d["full_" + name][:He * We * bpp].reshape(He, We * bpp)
+            frame_bytes += He * We * bpp
+            rows = np.arange(He)
+            exact = ((rows >= lo) & (rows < hi)) | mine
+            assert np.array_equal(got[exact], want[exact]), (r, name)
+            # outside its rows a rank may receive whole 16-row blocks that straddle lo / hi only
+            far = (rows < (lo // ROW_BLOCK) * ROW_BLOCK) | (rows >= -(-hi // ROW_BLOCK) * ROW_BLOCK)
+            assert (got[far & ~mine] == 0xEE).all(), (r, name)
+            assert (d["set0_" + name] == 0x11).all()
+        assert int(d["recv"]) < 0.75 * frame_bytes * (world - 1) / world, (r, int(d["recv"]))

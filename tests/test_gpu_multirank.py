@@ -22,12 +22,12 @@ def free_port():
 
 
 def render(rank, world, port, out_dir, pipelined, gather_stream, strip_denoise=False, size=(W, H), frames=FRAMES,
-           tag=""):
+           tag="", exchange=False):
     import torch
     import torch.distributed as dist
 
     import rtx
-    from rtx.dist import StripDenoise, StripGather, strip_config
+    from rtx.dist import StripDenoise, StripGather, gbuffer_rows, strip_config
 
     W, H = size
 
@@ -50,9 +50,13 @@ def render(rank, world, port, out_dir, pipelined, gather_stream, strip_denoise=F
     if gs is not None:
         rt.set_gather_stream(gs.cuda_stream)
     sd = StripDenoise(W, H, world, rank, dev, rt) if (strip_denoise and world > 1) else None
+    need = None
     if sd is not None:
         i = rt.info()
         assert (i.denoiseRowBegin, i.denoiseRowEnd) == (sd.a, sd.b)
+        assert (i.gbufferRowBegin, i.gbufferRowEnd) == gbuffer_rows(H, world, rank)
+        if exchange:  # only the G-buffer rows each rank's strip-local denoise reads
+            need = [gbuffer_rows(H, world, r) for r in range(world)]
     cam0 = rt.camera
     for f in range(1, frames + 1):
         c = rt.camera
@@ -62,12 +66,13 @@ def render(rank, world, port, out_dir, pipelined, gather_stream, strip_denoise=F
         rt.path_trace(f)
         if sg is not None:
             rt.sync()  # gloo reads the tensors on the host side: the strip must be complete
+            move = sg.gather if need is None else (lambda: sg.exchange(need))
             if gs is not None:  # gathers on their own stream; the denoise waits for it
                 gs.wait_stream(torch.cuda.current_stream(dev))
                 with torch.cuda.stream(gs):
-                    sg.gather()
+                    move()
             else:
-                sg.gather()
+                move()
         rt.denoise_post(f)
     rgba = rt.download("RGBA8", np.uint8).copy()
     hdr = rt.get_buffer("HISTORY_COLOR").copy()  # TemporalFilter2's output: the frame's final HDR
@@ -114,15 +119,32 @@ def test_two_ranks_strip_local_denoise(tmp_path, pipelined, gather_stream):
 
 
 def test_two_ranks_4k_strip_local_denoise(tmp_path):
-    """Config 5's frame (3840x2160) split over two ranks (gloo on one GPU), strip-local denoise,
-    two pipelined frames, against a single-rank render."""
+    """Config 5's frame (3840x2160) split over two ranks (gloo on one GPU), strip-local denoise and
+    the strip exchange of the G-buffers, two pipelined frames, against a single-rank render."""
     import torch.multiprocessing as mp
 
-    args = (True, True, True, (3840, 2160), 2, "k")
+    args = (True, True, True, (3840, 2160), 2, "k", True)  # with the strip exchange
     mp.start_processes(render, args=(1, 0, str(tmp_path)) + args, nprocs=1, start_method="spawn")
     mp.start_processes(render, args=(2, free_port(), str(tmp_path)) + args, nprocs=2, start_method="spawn")
     ref = np.load(tmp_path / "kr0_of1.npz")
     for r in range(2):
         got = np.load(tmp_path / ("kr%d_of2.npz" % r))
+        for k in ("rgba", "hdr", "acc", "expo"):
+            assert np.array_equal(got[k], ref[k]), "rank %d %s" % (r, k)
+
+
+@pytest.mark.parametrize("pipelined", [True, False])
+def test_two_ranks_strip_exchange(tmp_path, pipelined):
+    """The strip exchange instead of the all-gather (StripGather.exchange: each rank receives only
+    the G-buffer rows its strip-local denoise reads, gbuffer_rows): at 256x512 the two ranks need
+    rows [0, 336) and [176, 512); after 4 frames of a moving camera both hold the single-rank frame."""
+    import torch.multiprocessing as mp
+
+    args = (pipelined, True, True, (256, 512), FRAMES, "x", True)
+    mp.start_processes(render, args=(1, 0, str(tmp_path)) + args, nprocs=1, start_method="spawn")
+    mp.start_processes(render, args=(2, free_port(), str(tmp_path)) + args, nprocs=2, start_method="spawn")
+    ref = np.load(tmp_path / "xr0_of1.npz")
+    for r in range(2):
+        got = np.load(tmp_path / ("xr%d_of2.npz" % r))
         for k in ("rgba", "hdr", "acc", "expo"):
             assert np.array_equal(got[k], ref[k]), "rank %d %s" % (r, k)

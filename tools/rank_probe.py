@@ -3,7 +3,8 @@
 (stripCount = N), pipelined exactly as bench.py runs it, without the G-buffer all-gather itself.
 The rows other ranks would deliver are filled once with a full-frame render (the denoiser's cost
 depends on them: sky pixels skip the filters), so the denoise sees the frame it would see after
-the gather.  Prints ms per frame for each N.  Usage: tools/rank_probe.py [N ...] (default 1 2 4 8)."""
+the gather.  STRIP_DN=1: each rank denoises only its strip (+ halo), with the collective hook a
+no-op (compute only: the exchanges are left out).  Prints ms per frame for each N.  Usage: tools/rank_probe.py [N ...] (default 1 2 4 8)."""
 import os
 import sys
 import tempfile
@@ -35,7 +36,7 @@ def full_frame(W, H, spp):
     return _FULL[key]
 
 
-def run(n, frames=30, warm=3, W=1920, H=1080, spp=4, pipeline=True, denoise=True):
+def run(n, frames=int(os.environ.get("FRAMES", "30")), warm=3, W=1920, H=1080, spp=4, pipeline=True, denoise=True):
     d = tempfile.mkdtemp()
     rt = rtx.RayTracer(W, H, rtx.write_config(os.path.join(d, "c.toml"), W, H, spp=spp,
                                               extra=strip_config(n, 0))).init()
@@ -46,6 +47,8 @@ def run(n, frames=30, warm=3, W=1920, H=1080, spp=4, pipeline=True, denoise=True
     rt.set_stream(main.cuda_stream)
     if pipeline:
         rt.set_post_stream(post.cuda_stream)
+    if n > 1 and os.environ.get("STRIP_DN"):  # strip-local denoise, exchanges left out (no-op hook)
+        rt.set_collective_hook(lambda stage, stream, x: None)
     if n > 1:  # bound full-frame G-buffers holding the other ranks' rows, as after the gather
         sg = StripGather(W, H, n, 0, torch.device("cuda", 0), rt, sets=rtx.GBUFFER_SETS if pipeline else 1)
         full = full_frame(W, H, spp)
@@ -68,6 +71,9 @@ def run(n, frames=30, warm=3, W=1920, H=1080, spp=4, pipeline=True, denoise=True
     rt.sync()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / frames
+    if os.environ.get("STAGES"):  # serial stage times of this rank's share (LBVH, path trace, denoise)
+        st = [rt.time_stage(k, 20) / 20 for k in (1, 2, 4)]
+        print("  N=%d stages serial: lbvh %.3f  path trace %.3f  denoise %.3f ms" % (n, *st), flush=True)
     rt.cleanup()
     return ms
 

@@ -60,6 +60,11 @@ struct HistCamera { float pos[3], left[3], up[3], dir[3]; };  // HistoryCamera (
 //   rayO  = orig.xyz, pixel index (bits)            rayD = dir.xyz, flags (bits, kQFlag*)
 //   st0   = albedo.xyz, rayConeWidth                 st1  = beta1.xyz, rayConeSpread
 //   st2   = beta0.xyz, 0
+// rayD.w bit 0: the entry is a shadow ray (isShadowRay).  Only whether a shadow ray, or any
+// step-4 ray, hits something decides its sample's colour (the path ends there, and a hit never
+// has matType MAT_SKY), so the queue tracer ends those traversals at their first hit.
+constexpr uint32_t kQShadowFlag = 1u;
+
 struct PtQueue {
     float4* rayO;
     float4* rayD;

@@ -31,7 +31,7 @@ using namespace rtd;
 namespace {
 
 // queue-entry flags (PtQueue rayD.w)
-constexpr uint32_t kQShadow = 1u;          // isShadowRay
+constexpr uint32_t kQShadow = kQShadowFlag;  // isShadowRay
 constexpr int kQSampleShift = 1;           // sample index s (6 bits, spp <= 64)
 constexpr int kQLightShift = 16;           // lightIdx (16 bits: 7777 or 9999)
 

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
     Fetch f;
     fetch_init(f, n, gridDim.x * wavesPerBlock, blockIdx.x * wavesPerBlock + (uint32_t)(tid >> 6));
 
-    bool active = false, exhausted = false;
+    bool active = false, exhausted = false, occlusion = false;
     uint32_t idx = 0, accV = 0, accT = 0;
     TravRay r;
     TravState s;
@@ -112,6 +112,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
                     trav_setup(sc, f3(o.x, o.y, o.z), f3(d.x, d.y, d.z), r);
                     trav_init(s);
                     active = true;
+                    occlusion = kStep == 4 || (__float_as_uint(d.w) & kQShadowFlag) != 0u;
                 } else if (none) {
                     exhausted = true;
                 }
@@ -120,7 +121,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
         }
         if (__ballot(active) == 0ull) break;
         if (trav_lane_steps(active, s)) {
-            const bool done = trav_step(sc, r, s, stkA + tid, stkT + tid, kTraceBlock) || s.iters >= 1024u;
+            const bool done = trav_step(sc, r, s, stkA + tid, stkT + tid, kTraceBlock) || s.iters >= 1024u ||
+                              (occlusion && s.hitIdx >= 0);
             if (done) {
                 P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);
                 P.ws.hitErr[idx] = s.hitErrT;

@@ -373,6 +373,14 @@ def main():
                                      "denoise_post": round(rt.time_stage(4, 20) / 20, 5),
                                      "primary_rays_1spp": round(rt.time_stage(1, 20) / 20, 5)}
         result["primary_mray_s"] = round(W * rows / (result["stage_ms_serial"]["primary_rays_1spp"] * 1e-3) / 1e6, 2)
+        # serial frames (no post stream: rt_draw's mode) run trace<3> .. resume<4> as one fused
+        # launch, k_pt_chain, in kernel slot 2 (slots 3-5 stay empty)
+        sk = rt.time_path_trace_kernels(20)
+        names = list(sk)
+        if all(sk[k] < 0.02 for k in names[3:6]):
+            sk = {("k_pt_chain" if i == 2 else k): v for i, (k, v) in enumerate(sk.items()) if not 3 <= i <= 5}
+        result["serial_kernels_ms"] = {k: round(v, 5) for k, v in sk.items()}
+        result["serial_kernels_ms"]["sum"] = round(sum(sk.values()), 5)
     rt.cleanup()
 
     if final is not None:

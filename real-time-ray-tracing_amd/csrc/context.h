@@ -189,8 +189,9 @@ struct rt_context {
     bool postPending = false;
     int postPendingSet = 0;
     int overlapAfter = 1;  // after k_pt_shade0: measured best at 1-8 ranks
-    int cameraAfter = 3;   // the next frame's camera rays start after this frame's kernel 2 (queue-3
-                           // trace) on 1-2 GPUs, kernel 3 (resume<3>) on more (rt_set_post_stream)
+    int cameraAfter = 3;   // the next frame's camera rays start after this frame's kernel cameraAfter
+                           // ends (0: no gate; 1 GPU), kernel 2 = trace<3> on 2 GPUs, kernel 3 =
+                           // resume<3> on more (set by rt_set_post_stream)
     hipEvent_t cameraGate = nullptr;
     bool cameraGated = false;
     DenoisePostParams postParams{};

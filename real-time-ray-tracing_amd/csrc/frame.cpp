@@ -399,6 +399,7 @@ int rt_frame_init(rt_context* ctx) {
         if (const char* a = getenv("RTX_TRACE4_PER_CU"))
             if (atoi(a) > 0 && atoi(a) <= perCu) trace4PerCu = atoi(a);
         ws.traceBlocks = (uint32_t)(cus * tracePerCu);
+        ws.chain = getenv("RTX_NO_CHAIN") ? 0 : 1;  // A/B aid: the four separate bounce-chain kernels
         ws.trace4Blocks = (uint32_t)(cus * trace4PerCu);
     }
     ALLOC(fr.colorB, P * 8);
@@ -564,6 +565,10 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
         p.ws.glossy = m >= 0 && (m == 1 || m == 5 || m >= 10);
         p.ws.microfacet = m == 4;  // mat_type: only id 4 is MICROFACET, the reference table uses 3 / 6
     }
+    // the fused bounce chain shortens a serial frame; pipelined frames keep the four lean kernels,
+    // beside which the next frame's camera waves fit (k_pt_chain's 168 VGPRs at 3 waves/SIMD leave
+    // them no room): DESIGN.md §4.1
+    p.ws.chain = fr.ws.chain && !ctx->postStream;
     if (with_detail) {  // per-pixel counters: everything in order on the context stream
         if (ctx->postStream && (rc = sync_streams(ctx)) != RT_OK) return rc;
         HIP_TRY(ctx, hipMemsetAsync(fr.rays, 0, (size_t)ctx->renderW * ctx->renderH * 4, ctx->stream));
@@ -921,9 +926,10 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
     if (!ctx->overlapEv) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->overlapEv, hipEventDisableTiming));
     if (!ctx->cameraGate) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->cameraGate, hipEventDisableTiming));
     ctx->cameraGated = false;
-    // the next frame's camera rays: beside this frame's queue-3 traversal tail on one or two
-    // GPUs, after its resume<3> on more, where the per-rank tail is shorter
-    ctx->cameraAfter = ctx->stripCount <= 2 ? 2 : 3;
+    // the next frame's camera rays: ungated on one GPU (they run beside this frame's shade and
+    // queue-3 traversal at low priority), after this frame's trace<3> on two GPUs and after its
+    // resume<3> on more, where a rank's tails are shorter (measured per N: DESIGN.md §7)
+    ctx->cameraAfter = ctx->stripCount == 1 ? 0 : ctx->stripCount == 2 ? 2 : 3;
     if (const char* a = getenv("RTX_OVERLAP_AFTER")) ctx->overlapAfter = atoi(a);  // tuning aids
     if (const char* a = getenv("RTX_CAMERA_AFTER")) ctx->cameraAfter = atoi(a);
     ctx->postStream = (hipStream_t)stream;

@@ -105,6 +105,7 @@ struct PtWorkspace {
     uint32_t trace4Blocks;      // ... of queue 4 (a short queue: a few percent of queue 3)
     int glossy;                 // materials can be glossy: steps 1-2 may trace (materialOverride)
     int microfacet;             // materials can be the microfacet one (materialOverride 4): GGX compiled in
+    int chain = 1;              // default materials: trace<3> .. resume<4> as one launch (k_pt_chain)
     uint32_t* itersOut = nullptr;  // optional [cap]: traversal iterations per queue entry (rt_trace_rays)
 };
 

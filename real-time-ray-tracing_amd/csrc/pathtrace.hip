@@ -23,6 +23,7 @@
 // the other G-buffers come from sample 0.
 #include "frame_kernels.h"
 #include "pt_common.h"
+#include "queue_fetch.h"
 #include "shade.h"
 #include "traverse.h"
 
@@ -726,6 +727,50 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
     add_rays(P, wgRays, raysWg);
 }
 
+// Entry i of queue kStep (3 or 4): reloads the sample's state, applies the hit the tracer found
+// (t, triangle index bits, u, v; errorT) and runs the rest of its sequence.  Returns 4 when the
+// I4 ray must be traced (kStep == 3 only), else 5 (the sample is complete).
+template <int kStep, bool kMF>
+RT_DEV int resume_entry(PathCtx& c, const PtQueue& q, const SceneView& sc, uint32_t i, float4 hr, float herr,
+                        PathVars& v, uint32_t& p, uint32_t& s) {
+    const PathTraceParams& P = c.P;
+    const float4 o = q.rayO[i], d = q.rayD[i], s0 = q.st0[i], s1 = q.st1[i], s2 = q.st2[i];
+    p = __float_as_uint(o.w);
+    const uint32_t flags = __float_as_uint(d.w);
+    s = (flags >> kQSampleShift) & 63u;
+    const int x = (int)(p % P.width), y = (int)(p / P.width);
+    c.bp = bn_pixel(P.bluenoise, x, y);
+    c.frameIdx = (int)P.spp * (P.frameNum - 1) + 1 + (int)s;
+    RayState& rs = v.rs;
+    rs.orig = f3(o.x, o.y, o.z);
+    rs.dir = f3(d.x, d.y, d.z);
+    rs.isShadowRay = (flags & kQShadow) != 0u;
+    rs.lightIdx = (int)(flags >> kQLightShift);
+    rs.albedo = f3(s0.x, s0.y, s0.z);
+    rs.rayConeWidth = s0.w;
+    v.beta1 = f3(s1.x, s1.y, s1.z);
+    rs.rayConeSpread = s1.w;
+    v.beta0 = f3(s2.x, s2.y, s2.z);
+    rs.hitLight = false;  // a traced ray had neither flag set
+    rs.isOccluded = false;
+    rs.isHitProcessed = true;
+    rs.isDiffuse = false;
+    rs.centerRaydir = f3(0.0f);  // read by D0 only
+    rs.matId = 0;
+    rs.matType = MAT_SKY;
+    HitInfo h;
+    finalize_hit(sc, rs.orig, rs.dir, hr.x, (int)__float_as_uint(hr.y), hr.z, hr.w, herr, h);
+    return run_path<0, kMF>(c, v, kStep, &h, sc, nullptr, nullptr);
+}
+
+// a completed sample of a queue entry: its radiance goes to the late-resolve slot
+RT_DEV void store_path_L(const PathCtx& c, const PathVars& v, uint32_t p, uint32_t s) {
+    const PathTraceParams& P = c.P;
+    const F3 Ls = finish(c, v);
+    const uint32_t pl = local_row(P.y0, P.nStrips, p / P.width) * P.width + p % P.width;
+    P.ws.pathL[(size_t)pl * P.spp + s] = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
+}
+
 // Resumes the samples of queue kStep (3 or 4) once k_trace_queue has written their hits.
 template <int kStep, bool kMF>
 __global__ __launch_bounds__(256, kMF ? 2 : 3) void k_pt_resume(PathTraceParams P) {
@@ -752,46 +797,14 @@ __global__ __launch_bounds__(256, kMF ? 2 : 3) void k_pt_resume(PathTraceParams 
         PathVars v;
         int kd = 5;
         uint32_t p = 0, s = 0;
-        if (active) {
-            const float4 o = q.rayO[i], d = q.rayD[i], s0 = q.st0[i], s1 = q.st1[i], s2 = q.st2[i];
-            const float4 hr = P.ws.hitRec[i];
-            const float herr = P.ws.hitErr[i];
-            p = __float_as_uint(o.w);
-            const uint32_t flags = __float_as_uint(d.w);
-            s = (flags >> kQSampleShift) & 63u;
-            const int x = (int)(p % P.width), y = (int)(p / P.width);
-            c.bp = bn_pixel(P.bluenoise, x, y);
-            c.frameIdx = (int)P.spp * (P.frameNum - 1) + 1 + (int)s;
-            RayState& rs = v.rs;
-            rs.orig = f3(o.x, o.y, o.z);
-            rs.dir = f3(d.x, d.y, d.z);
-            rs.isShadowRay = (flags & kQShadow) != 0u;
-            rs.lightIdx = (int)(flags >> kQLightShift);
-            rs.albedo = f3(s0.x, s0.y, s0.z);
-            rs.rayConeWidth = s0.w;
-            v.beta1 = f3(s1.x, s1.y, s1.z);
-            rs.rayConeSpread = s1.w;
-            v.beta0 = f3(s2.x, s2.y, s2.z);
-            rs.hitLight = false;  // a traced ray had neither flag set
-            rs.isOccluded = false;
-            rs.isHitProcessed = true;
-            rs.isDiffuse = false;
-            rs.centerRaydir = f3(0.0f);  // read by D0 only
-            rs.matId = 0;
-            rs.matType = MAT_SKY;
-            HitInfo h;
-            finalize_hit(sc, rs.orig, rs.dir, hr.x, (int)__float_as_uint(hr.y), hr.z, hr.w, herr, h);
-            kd = run_path<0, kMF>(c, v, kStep, &h, sc, nullptr, nullptr);
-        }
+        if (active) kd = resume_entry<kStep, kMF>(c, q, sc, i, P.ws.hitRec[i], P.ws.hitErr[i], v, p, s);
         const uint32_t slot = wave_append(kd == 4, &P.ws.counters[kCntQ4]);
         if (active) {
             if (kd < 5) {  // kStep == 3 only: the I4 ray
                 ++c.rays;
                 enqueue(P.ws.q4, slot, v, p, s);
             } else {
-                const F3 Ls = finish(c, v);
-                const uint32_t pl = local_row(P.y0, P.nStrips, p / P.width) * P.width + p % P.width;
-                P.ws.pathL[(size_t)pl * P.spp + s] = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
+                store_path_L(c, v, p, s);
             }
             if (P.raysOut && c.rays) atomicAdd(&P.raysOut[p], c.rays);
             if (P.statsOut) {
@@ -803,6 +816,202 @@ __global__ __launch_bounds__(256, kMF ? 2 : 3) void k_pt_resume(PathTraceParams 
         }
     }
     if (kStep == 3 && P.statsOut) wave_add(rsD, &P.ws.counters[kCntDiffRes3]);
+    add_rays(P, wgRays, rays);
+}
+
+constexpr int kChainRanges = 32;  // queue-3 reserves a wave records before it resumes them
+#ifndef RTX_CHAIN_STATIC
+#define RTX_CHAIN_STATIC 0
+#endif
+constexpr bool kChainStaticFirst = RTX_CHAIN_STATIC != 0;  // ablation: static first batch per wave
+
+// The bounce chain of the default materials in one launch: trace<3> -> resume<3> -> trace<4> ->
+// resume<4>.  As separate kernels every stage ends on its slowest wave, so a frame
+// paid the longest queue-3 traversal plus the longest queue-4 traversal one after the other.
+// Here each wave resumes the queue-3 entries it traced itself, then traces and finishes the I4
+// rays those produced, while other waves are still in their queue-3 tails; the launch ends on
+// the wave whose chain is longest, not on the sum of two tails.
+//
+//   phase 1  k_trace_queue<3>'s refilling traversal loop (same Fetch), plus a per-wave list of
+//            the reserves [lo, hi) the wave took; every entry of a reserve is traced by its lanes.
+//   phase 2  (every lane idle) the wave resumes its reserves 64 entries at a time — resume<3> —
+//            appends the I4 rays to queue 4 and to a per-wave slot list, and once 64 slots could
+//            overflow, or at the end, traces them one per lane and finishes them (resume<4>).
+//   repeat   when the reserve list was full before the queue drained.
+// Per sample the code is the one the separate kernels run (resume_entry, trav_step), so the
+// G-buffers are identical.  The hit records a wave reads in phase 2 are ones its own lanes wrote
+// (a workgroup-scope fence orders them), so no record crosses workgroups inside the launch.
+__global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
+    __shared__ uint32_t stkA[16 * 256];
+    __shared__ float stkT[16 * 256];
+    __shared__ uint32_t sob[256];
+    __shared__ uint2 ranges[4][kChainRanges];
+    __shared__ uint32_t q4list[4][64];
+    __shared__ unsigned long long wgRays[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const unsigned long long ltMask = (1ull << lane) - 1ull;
+    bn_stage_sobol(P.bluenoise, sob, tid, 256);
+    __syncthreads();
+    const uint32_t n = P.ws.counters[kCntQ3];
+    const SceneView sc = scene_of(P);
+    const PtQueue& q = P.ws.q3;
+    const uint32_t allParts = (1u << kParts) - 1u;
+    Fetch f;
+    fetch_init(f, n, gridDim.x * 4u, blockIdx.x * 4u + (uint32_t)w, kChainStaticFirst);
+    uint32_t rays = 0;
+#pragma unroll 1
+    while (true) {  // wave-uniform
+        // ---- phase 1: trace queue-3 entries, recording the reserves taken
+        uint32_t nRanges = 0;
+        if (f.resLo < f.resHi) {  // the rest of a reserve (the static first batch, or one cut short)
+            if (lane == 0) ranges[w][0] = make_uint2(f.resLo, f.resHi);
+            nRanges = 1;
+        }
+        bool active = false, exhausted = false, occlusion = false;
+        uint32_t idx = 0;
+        TravRay r;
+        TravState s;
+        r.org = f3(0.0f);
+        trav_init(s);
+#pragma unroll 1
+        while (true) {
+            const unsigned long long need = __ballot(!active && !exhausted);
+            const unsigned long long busy = __ballot(active);
+            if (need != 0ull && (__popcll(need) >= kRefillMin || busy == 0ull)) {
+                const uint32_t k = (uint32_t)__popcll(need);
+                if (f.resLo == f.resHi && nRanges < (uint32_t)kChainRanges) {
+                    fetch_topup(f, n, P.ws.fetch, lane);
+                    if (f.resLo < f.resHi) {
+                        if (lane == 0) ranges[w][nRanges] = make_uint2(f.resLo, f.resHi);
+                        ++nRanges;
+                    }
+                }
+                const uint32_t avail = f.resHi - f.resLo;
+                const bool none = avail == 0u;  // drained, or the reserve list is full
+                if (!active && !exhausted) {
+                    const uint32_t rank = (uint32_t)__popcll(need & ltMask);
+                    if (rank < avail) {
+                        idx = f.resLo + rank;
+                        const float4 o = q.rayO[idx], d = q.rayD[idx];
+                        trav_setup(sc, f3(o.x, o.y, o.z), f3(d.x, d.y, d.z), r);
+                        trav_init(s);
+                        active = true;
+                        occlusion = (__float_as_uint(d.w) & kQShadowFlag) != 0u;
+                    } else if (none) {
+                        exhausted = true;
+                    }
+                }
+                f.resLo += k < avail ? k : avail;
+            }
+            if (__ballot(active) == 0ull) break;
+            if (trav_lane_steps(active, s)) {
+                const bool done = trav_step(sc, r, s, stkA + tid, stkT + tid, 256) || s.iters >= 1024u ||
+                                  (occlusion && s.hitIdx >= 0);
+                if (done) {
+                    P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);
+                    P.ws.hitErr[idx] = s.hitErrT;
+                    if (P.statsOut) {
+                        const uint32_t p = __float_as_uint(q.rayO[idx].w);
+                        atomicAdd(&P.statsOut[p].y, s.visits);
+                        atomicAdd(&P.statsOut[p].z, s.tests);
+                        atomicMax(&P.ws.counters[kCntMaxIter3], s.iters);
+                        atomicAdd(&P.ws.counters[kCntVisQ3], s.visits);  // detail launches only
+                        atomicAdd(&P.ws.counters[kCntTstQ3], s.tests);
+                    }
+                    active = false;
+                }
+            }
+        }
+        // ---- phase 2: resume this wave's entries, trace and finish their I4 rays
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the hit records this wave wrote
+#if defined(RTX_CHAIN_ABL) && RTX_CHAIN_ABL == 1
+        nRanges = 0;  // timing ablation: no phase 2
+#endif
+        PathCtx c{P, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), sob, BnPixel{0u, 0u}, 0, 0u, 0u, 0u, 0u};
+        c.skyTree = P.skyTree;  // the light-CDF heaps from L2: LDS holds the traversal stacks
+        c.sunTree = P.sunTree;
+        uint32_t ri = 0, nq4 = 0;
+#pragma unroll 1
+        while (true) {
+            const bool more = ri < nRanges;
+            const uint2 rg = more ? ranges[w][ri] : make_uint2(0u, 0u);
+            if (nq4 > 0u && (!more || nq4 + (rg.y - rg.x) > 64u)) {
+                // trace the listed I4 rays (one per lane) to their first hit, then finish them
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // queue-4 records, slot list
+                bool act = (uint32_t)lane < nq4;
+                const uint32_t slot = act ? q4list[w][lane] : 0u;
+                TravRay r4;
+                TravState s4;
+                {
+                    const float4 o = P.ws.q4.rayO[slot], d = P.ws.q4.rayD[slot];  // slot 0 for idle lanes
+                    trav_setup(sc, f3(o.x, o.y, o.z), f3(d.x, d.y, d.z), r4);
+                }
+                trav_init(s4);
+                const bool mine = act;
+#if defined(RTX_CHAIN_ABL) && RTX_CHAIN_ABL == 2
+                act = false;  // timing ablation: I4 rays not traced
+#endif
+#pragma unroll 1
+                while (__ballot(act) != 0ull) {
+                    if (trav_lane_steps(act, s4)) {
+                        if (trav_step(sc, r4, s4, stkA + tid, stkT + tid, 256) || s4.iters >= 1024u || s4.hitIdx >= 0)
+                            act = false;
+                    }
+                }
+                if (mine) {
+                    PathVars v;
+                    uint32_t p = 0, smp = 0;
+                    c.rays = 0;
+                    (void)resume_entry<4, false>(c, P.ws.q4, sc, slot,
+                                                 make_float4(s4.t, __uint_as_float((uint32_t)s4.hitIdx), s4.hitU, s4.hitV),
+                                                 s4.hitErrT, v, p, smp);
+                    store_path_L(c, v, p, smp);
+                    if (P.statsOut) {
+                        atomicAdd(&P.statsOut[p].y, s4.visits);
+                        atomicAdd(&P.statsOut[p].z, s4.tests);
+                        atomicMax(&P.ws.counters[kCntMaxIter4], s4.iters);
+                        atomicAdd(&P.ws.counters[kCntVisQ4], s4.visits);
+                        atomicAdd(&P.ws.counters[kCntTstQ4], s4.tests);
+                    }
+                }
+                nq4 = 0u;
+                continue;
+            }
+            if (!more) break;
+            const uint32_t i = rg.x + (uint32_t)lane;
+            const bool act = i < rg.y;
+            PathVars v;
+            int kd = 5;
+            uint32_t p = 0, smp = 0;
+            c.rays = 0;
+            c.diffuse = 0;
+            if (act) kd = resume_entry<3, false>(c, q, sc, i, P.ws.hitRec[i], P.ws.hitErr[i], v, p, smp);
+            const bool i4 = kd == 4;
+            const uint32_t slot = wave_append(i4, &P.ws.counters[kCntQ4]);
+            const unsigned long long m4 = __ballot(i4);
+            if (act) {
+                if (i4) {
+                    ++c.rays;
+                    enqueue(P.ws.q4, slot, v, p, smp);
+                    q4list[w][nq4 + (uint32_t)__popcll(m4 & ltMask)] = slot;
+                } else {
+                    store_path_L(c, v, p, smp);
+                }
+                if (P.raysOut && c.rays) atomicAdd(&P.raysOut[p], c.rays);
+                if (P.statsOut) {
+                    if (c.rays) atomicAdd(&P.statsOut[p].x, c.rays);
+                    if (c.diffuse) {
+                        atomicAdd(&P.statsOut[p].w, c.diffuse);
+                        atomicAdd(&P.ws.counters[kCntDiffRes3], c.diffuse);
+                    }
+                }
+                rays += c.rays;
+            }
+            nq4 += (uint32_t)__popcll(m4);
+            ++ri;
+        }
+        if (f.resLo == f.resHi && f.drained == allParts) break;  // queue 3 drained
+    }
     add_rays(P, wgRays, rays);
 }
 
@@ -868,15 +1077,23 @@ extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t s
     else if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_shade0<false, true>), pg, pb, 0, stream, *p);
     else hipLaunchKernelGGL((k_pt_shade0<false, false>), pg, pb, 0, stream, *p);
     if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
-    if ((e = rtk_launch_trace_queue(p, 3, stream)) != hipSuccess || (e = end()) != hipSuccess) return e;
-    if ((e = begin()) != hipSuccess) return e;
-    if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_resume<3, true>), pg, pb, 0, stream, *p);
-    else hipLaunchKernelGGL((k_pt_resume<3, false>), pg, pb, 0, stream, *p);
-    if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
-    if ((e = rtk_launch_trace_queue(p, 4, stream)) != hipSuccess || (e = end()) != hipSuccess) return e;
-    if ((e = begin()) != hipSuccess) return e;
-    hipLaunchKernelGGL((k_pt_resume<4, false>), pg, pb, 0, stream, *p);  // step 4 shades nothing
-    if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
+    if (p->ws.chain && !p->ws.glossy && !p->ws.microfacet) {
+        // kernel 2 = the fused bounce chain (trace<3> .. resume<4>); slots 3-5 stay empty, so the
+        // hook's kernel numbers and the per-kernel timing slots keep their meaning
+        hipLaunchKernelGGL(k_pt_chain, dim3(p->ws.traceBlocks), pb, 0, stream, *p);
+        for (int j = 0; j < 4; ++j)
+            if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
+    } else {
+        if ((e = rtk_launch_trace_queue(p, 3, stream)) != hipSuccess || (e = end()) != hipSuccess) return e;
+        if ((e = begin()) != hipSuccess) return e;
+        if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_resume<3, true>), pg, pb, 0, stream, *p);
+        else hipLaunchKernelGGL((k_pt_resume<3, false>), pg, pb, 0, stream, *p);
+        if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
+        if ((e = rtk_launch_trace_queue(p, 4, stream)) != hipSuccess || (e = end()) != hipSuccess) return e;
+        if ((e = begin()) != hipSuccess) return e;
+        hipLaunchKernelGGL((k_pt_resume<4, false>), pg, pb, 0, stream, *p);  // step 4 shades nothing
+        if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_pt_resolve, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);
     if ((e = end()) != hipSuccess) return e;
     return hipGetLastError();

@@ -16,6 +16,7 @@
 // wave leaves the loop when no lane holds a ray, which every wave reaches because the fetch
 // counters only grow and every ray ends within 1024 iterations.
 #include "frame_kernels.h"
+#include "queue_fetch.h"
 #include "traverse.h"
 
 using namespace rtd;
@@ -23,52 +24,6 @@ using namespace rtd;
 namespace {
 
 constexpr int kTraceBlock = 256;
-constexpr int kRefillMin = 16;  // idle lanes that trigger a refill
-constexpr int kParts = 8;       // fetch counters (one per XCD by blockIdx % 8): spreads the atomics
-
-// Work distribution.  Wave g first takes items [64 g, 64 g + 64) with no atomic: a short queue
-// (a sky-dominated frame) costs no atomics at all.  The rest, [64 * waves, n), is cut into
-// kParts contiguous parts; a wave tops up a 64-item reserve from its home part (one atomic per
-// 64 items), moving on to the next part when its home part is drained.  A same-address
-// device-scope atomic serialises at the memory side, so both the static first batch and the
-// per-part counters keep the queue of atomics on any one address short.
-struct Fetch {
-    uint32_t resLo, resHi;  // wave-uniform reserve [resLo, resHi)
-    uint32_t dynBase, partLen;
-    uint32_t drained;       // bit x: part x has no items left
-    int home;
-};
-
-RT_DEV void fetch_init(Fetch& f, uint32_t n, uint32_t wavesTotal, uint32_t gw) {
-    const uint32_t s0 = gw * 64u;
-    f.resLo = s0 < n ? s0 : n;
-    f.resHi = s0 + 64u < n ? s0 + 64u : n;
-    f.dynBase = wavesTotal * 64u;
-    const uint32_t dyn = n > f.dynBase ? n - f.dynBase : 0u;
-    f.partLen = (dyn + kParts - 1) / kParts;
-    f.drained = dyn == 0u ? (1u << kParts) - 1u : 0u;
-    f.home = (int)(blockIdx.x % kParts);
-}
-
-// refill an empty reserve from the first part that still has items (wave-uniform call)
-RT_DEV void fetch_topup(Fetch& f, uint32_t n, uint32_t* counters, int lane) {
-    while (f.resLo == f.resHi && f.drained != (1u << kParts) - 1u) {
-        int part = f.home;
-        while (f.drained & (1u << part)) part = (part + 1) % kParts;
-        uint32_t got = 0u;
-        if (lane == 0) got = atomicAdd(&counters[part * 16], 64u);  // counters 64 B apart
-        got = __shfl(got, 0);
-        const uint32_t lo = f.dynBase + part * f.partLen + got;
-        uint32_t hi = f.dynBase + part * f.partLen + (got + 64u < f.partLen ? got + 64u : f.partLen);
-        if (hi > n) hi = n;
-        if (got >= f.partLen || lo >= hi) {
-            f.drained |= 1u << part;
-            continue;
-        }
-        f.resLo = lo;
-        f.resHi = hi;
-    }
-}
 
 template <int kStep>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) {

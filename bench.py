@@ -201,6 +201,30 @@ def kernel_roofline(q, W, rows, S, kernels_ms, pmc, workload_matches):
     return out
 
 
+def time_draw(rtx, torch, dev, W, H, S, tmp, frames=20):
+    """ms/frame of rt_draw_device, sync and async, BASELINE config 3 (fixed deltaTime)."""
+    out = {}
+    target = torch.empty((H, W, 4), dtype=torch.uint8, device=dev)
+    for mode in ("sync", "async"):
+        d = rtx.RayTracer(W, H, rtx.write_config(os.path.join(tmp, "draw_%s.toml" % mode), W, H, dynamic=False,
+                                                 spp=S)).init()
+        d.set_delta_time(DELTA_MS)
+        asy = mode == "async"
+        for _ in range(3):
+            d.draw_device(target.data_ptr(), 0, asynchronous=asy)
+        d.sync()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            d.draw_device(target.data_ptr(), 0, asynchronous=asy)
+        d.sync()
+        torch.cuda.synchronize()
+        out[mode + "_ms_per_frame"] = round((time.perf_counter() - t0) * 1e3 / frames, 4)
+        d.cleanup()
+    out["frames"] = frames
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -399,6 +423,12 @@ def main():
         ref.cleanup()
         result["self_check"] = dict(same, frames=last, against="serial single-GPU re-render of frames 1..%d" % last,
                                     ok=all(same.values()))
+
+    if not args.no_extras and rank == 0 and world == 1:
+        # the reference host's entry point, RayTracer::draw(SurfObj*) (kernel.cu:259): rt_draw_device
+        # into a caller-owned device RGBA8 target, synchronous (serial frames, fused bounce chain)
+        # and asynchronous (RT_DRAW_ASYNC: the frame pipeline), in a fresh context
+        result["draw_device"] = time_draw(rtx, torch, dev, W, H, S, tmp)
 
     if not args.no_extras and rank == 0:
         # BASELINE config 4: per-frame rebuild of the ~1M-triangle variant (chunkDim 4)

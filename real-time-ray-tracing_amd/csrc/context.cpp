@@ -100,15 +100,68 @@ bool load_triangle_bin(const std::string& path, rtscene::SceneMesh& m, std::stri
 
 }  // namespace
 
-int rt_dalloc_bytes(rt_context* ctx, void** p, size_t bytes) {
+namespace {
+constexpr size_t kArenaChunk = 256ull << 20, kArenaMaxBuffer = 64ull << 20, kArenaAlign = 2ull << 20;
+bool arena_enabled() {
+    static const bool on = getenv("RTX_NO_ARENA") == nullptr;  // A/B aid
+    return on;
+}
+int raw_alloc(rt_context* ctx, void** p, size_t bytes) {
     void* q = nullptr;
-    hipError_t e = hipMalloc(&q, bytes < 16 ? 16 : bytes);
+    hipError_t e = hipMalloc(&q, bytes);
     if (e != hipSuccess) {
         ctx->err = std::string("hipMalloc(") + std::to_string(bytes) + "): " + hipGetErrorString(e);
         return RT_ERR_HIP;
     }
     ctx->allocations.push_back(q);
     *p = q;
+    return RT_OK;
+}
+}  // namespace
+
+// A renderer stream.  The frame pipeline needs its streams to run concurrently, but HIP maps
+// ordinary streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4) shared round-robin with every
+// stream created before in the process — a framework's stream pool, say.  Measured: after torch
+// had created its pools, rt_draw_device(RT_DRAW_ASYNC) ran 1.42 ms/frame instead of 1.10, two of
+// its streams having landed on one queue.  A stream created with a CU mask gets a hardware queue
+// of its own, so the renderer's streams use a full mask; they then carry no priority, which
+// measured no difference.  RTX_STREAMS=prio: plain streams with priorities.
+int rt_create_stream(rt_context* ctx, hipStream_t* s, bool high) {
+    static const bool prio = [] {
+        const char* v = getenv("RTX_STREAMS");
+        return v && strcmp(v, "prio") == 0;
+    }();
+    if (!prio) {
+        uint32_t mask[32];  // 1024 CUs' worth of bits; bits past the device's CU count are ignored
+        for (uint32_t& m : mask) m = 0xFFFFFFFFu;
+        HIP_TRY(ctx, hipExtStreamCreateWithCUMask(s, 32, mask));
+        return RT_OK;
+    }
+    int least = 0, greatest = 0;
+    HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(ctx, hipStreamCreateWithPriority(s, hipStreamNonBlocking, high ? greatest : least));
+    return RT_OK;
+}
+
+// Device buffers of a context.  Buffers up to 64 MiB (the BVH, triangles, textures, sky tables,
+// G-buffers, counters) are carved from 256-MiB chunks, each buffer starting on a 2-MiB boundary,
+// so the data a frame reads lies in a few large, contiguous allocations rather than in dozens of
+// separate ones wherever a fragmented device heap puts them; the large, sparsely
+// used queue planes get allocations of their own.
+int rt_dalloc_bytes(rt_context* ctx, void** p, size_t bytes) {
+    if (bytes < 16) bytes = 16;
+    if (!arena_enabled() || bytes > kArenaMaxBuffer) return raw_alloc(ctx, p, bytes);
+    size_t at = (ctx->arenaUsed + kArenaAlign - 1) / kArenaAlign * kArenaAlign;
+    if (!ctx->arenaPtr || at + bytes > ctx->arenaCap) {
+        void* chunk = nullptr;
+        const int rc = raw_alloc(ctx, &chunk, kArenaChunk);
+        if (rc != RT_OK) return rc;
+        ctx->arenaPtr = (char*)chunk;
+        ctx->arenaCap = kArenaChunk;
+        at = 0;
+    }
+    *p = ctx->arenaPtr + at;
+    ctx->arenaUsed = at + bytes;
     return RT_OK;
 }
 
@@ -297,7 +350,9 @@ int rt_init(rt_context* ctx) {
     if (ctx->B >= 1024) { ctx->err = "batch count must stay below 1024 (init.cu:126)"; return RT_ERR_ARG; }
     ctx->nv = (uint32_t)(ctx->mesh.vertices.size() / 3);
 
-    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->ownStream, hipStreamNonBlocking));
+    // the trace chain is a frame's critical path: it outranks the pipelined denoise and the next
+    // frame's camera rays, whose streams are created at the lowest priority
+    if (int rc = rt_create_stream(ctx, &ctx->ownStream, true)) return rc;
     ctx->stream = ctx->ownStream;
     HIP_TRY(ctx, hipEventCreate(&ctx->ev0));
     HIP_TRY(ctx, hipEventCreate(&ctx->ev1));

@@ -222,6 +222,9 @@ struct rt_context {
     FrameResources fr{};  // path-trace / denoise / post buffers (frame_kernels.h)
 
     std::vector<void*> allocations;
+    // device arena (rt_dalloc_bytes): buffers up to kArenaMaxBuffer are carved from 256-MiB chunks
+    char* arenaPtr = nullptr;
+    size_t arenaUsed = 0, arenaCap = 0;
 };
 
 // helpers shared by the C-ABI translation units
@@ -242,6 +245,7 @@ int dalloc(rt_context* ctx, T** p, size_t bytes) {
     *p = (T*)q;
     return rc;
 }
+int rt_create_stream(rt_context* ctx, hipStream_t* s, bool high);  // context.cpp: renderer streams
 int rt_frame_init(rt_context* ctx);  // frame.cpp: sky tables, textures, G-buffers
 int sync_streams(rt_context* ctx);   // frame.cpp: context, post and side streams
 bool strip_local_denoise(const rt_context* ctx, uint32_t& a, uint32_t& b);  // frame.cpp: next denoise's rows

@@ -814,11 +814,7 @@ int rt_draw_device(rt_context* ctx, void* rgba8_device, size_t pitch_bytes, int 
     if ((flags & ~RT_DRAW_ASYNC) != 0) { ctx->err = "rt_draw_device: unknown flags"; return RT_ERR_ARG; }
     int rc;
     if ((flags & RT_DRAW_ASYNC) && !ctx->postStream) {  // pipelined frames on an internal low-priority stream
-        if (!ctx->ownPostStream) {
-            int least = 0, greatest = 0;
-            HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
-            HIP_TRY(ctx, hipStreamCreateWithPriority(&ctx->ownPostStream, hipStreamNonBlocking, least));
-        }
+        if (!ctx->ownPostStream && (rc = rt_create_stream(ctx, &ctx->ownPostStream, false)) != RT_OK) return rc;
         if ((rc = rt_set_post_stream(ctx, ctx->ownPostStream)) != RT_OK) return rc;
     }
     if ((rc = enqueue_frame(ctx, (uint32_t*)rgba8_device, (uint32_t)(pitch_bytes / 4), false)) != RT_OK) return rc;
@@ -905,11 +901,8 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
         }
     }
 #undef ALLOC
-    if (!ctx->sideStream) {  // lowest priority: it should fill what the trace chain leaves idle
-        int least = 0, greatest = 0;
-        HIP_TRY(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_TRY(ctx, hipStreamCreateWithPriority(&ctx->sideStream, hipStreamNonBlocking, least));
-    }
+    // lowest priority: it should fill what the trace chain leaves idle
+    if (!ctx->sideStream && (rc = rt_create_stream(ctx, &ctx->sideStream, false)) != RT_OK) return rc;
     for (hipEvent_t* e : {&ctx->buildDone[0], &ctx->buildDone[1], &ctx->bvhFree[0], &ctx->bvhFree[1]})
         if (!*e) HIP_TRY(ctx, hipEventCreateWithFlags(e, hipEventDisableTiming));
     for (int k = 0; k < kGbSets; ++k) {

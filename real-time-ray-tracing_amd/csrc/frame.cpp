@@ -399,7 +399,9 @@ int rt_frame_init(rt_context* ctx) {
         if (const char* a = getenv("RTX_TRACE4_PER_CU"))
             if (atoi(a) > 0 && atoi(a) <= perCu) trace4PerCu = atoi(a);
         ws.traceBlocks = (uint32_t)(cus * tracePerCu);
-        ws.chain = getenv("RTX_NO_CHAIN") ? 0 : 1;  // A/B aid: the four separate bounce-chain kernels
+        ws.chain = 1;  // RTX_CHAIN=off|serial|always: A/B aid (default serial)
+        if (const char* a = getenv("RTX_CHAIN")) ws.chain = strcmp(a, "off") == 0 ? 0 : strcmp(a, "always") == 0 ? 2 : 1;
+        if (getenv("RTX_NO_CHAIN")) ws.chain = 0;
         ws.trace4Blocks = (uint32_t)(cus * trace4PerCu);
     }
     ALLOC(fr.colorB, P * 8);
@@ -567,8 +569,9 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     }
     // the fused bounce chain shortens a serial frame; pipelined frames keep the four lean kernels,
     // beside which the next frame's camera waves fit (k_pt_chain's 168 VGPRs at 3 waves/SIMD leave
-    // them no room): DESIGN.md §4.1
-    p.ws.chain = fr.ws.chain && !ctx->postStream;
+    // them no room), except on a rank of 8 or more, whose strip's camera rays are few and whose
+    // frame the traversal tails dominate
+    p.ws.chain = fr.ws.chain == 2 || (fr.ws.chain == 1 && (!ctx->postStream || ctx->stripCount >= 8));
     if (with_detail) {  // per-pixel counters: everything in order on the context stream
         if (ctx->postStream && (rc = sync_streams(ctx)) != RT_OK) return rc;
         HIP_TRY(ctx, hipMemsetAsync(fr.rays, 0, (size_t)ctx->renderW * ctx->renderH * 4, ctx->stream));
@@ -920,9 +923,10 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
     if (!ctx->cameraGate) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->cameraGate, hipEventDisableTiming));
     ctx->cameraGated = false;
     // the next frame's camera rays: ungated on one GPU (they run beside this frame's shade and
-    // queue-3 traversal at low priority), after this frame's trace<3> on two GPUs and after its
-    // resume<3> on more, where a rank's tails are shorter (measured per N: DESIGN.md §7)
-    ctx->cameraAfter = ctx->stripCount == 1 ? 0 : ctx->stripCount == 2 ? 2 : 3;
+    // queue-3 traversal), after this frame's trace<3> on two GPUs and its resume<3> on four, where
+    // a rank's tails are shorter, and after its shade on eight (beside the fused chain) (measured
+    // per N: DESIGN.md §7)
+    ctx->cameraAfter = ctx->stripCount == 1 ? 0 : ctx->stripCount == 2 ? 2 : ctx->stripCount < 8 ? 3 : 1;
     if (const char* a = getenv("RTX_OVERLAP_AFTER")) ctx->overlapAfter = atoi(a);  // tuning aids
     if (const char* a = getenv("RTX_CAMERA_AFTER")) ctx->cameraAfter = atoi(a);
     ctx->postStream = (hipStream_t)stream;

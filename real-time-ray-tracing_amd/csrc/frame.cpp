@@ -401,7 +401,6 @@ int rt_frame_init(rt_context* ctx) {
         ws.traceBlocks = (uint32_t)(cus * tracePerCu);
         ws.chain = 1;  // RTX_CHAIN=off|serial|always: A/B aid (default serial)
         if (const char* a = getenv("RTX_CHAIN")) ws.chain = strcmp(a, "off") == 0 ? 0 : strcmp(a, "always") == 0 ? 2 : 1;
-        if (getenv("RTX_NO_CHAIN")) ws.chain = 0;
         ws.trace4Blocks = (uint32_t)(cus * trace4PerCu);
     }
     ALLOC(fr.colorB, P * 8);

@@ -56,6 +56,18 @@ def test_pipelined_frames_match_serial(rtx, tmp_path):
         assert np.array_equal(a, b), "frame %d" % (f + 1)
 
 
+@pytest.mark.parametrize("chain", ["always", "off"])
+def test_pipelined_chain_modes_match_serial(rtx, tmp_path, monkeypatch, chain):
+    """The bounce chain as one launch (k_pt_chain: what serial frames, and pipelined frames on
+    8-strip ranks, run) and as four kernels (pipelined frames on 1-4 ranks), each pipelined,
+    against serial frames (k_pt_chain): identical outputs."""
+    ref, _, _ = run(rtx, tmp_path, False, False)
+    monkeypatch.setenv("RTX_CHAIN", chain)
+    got, _, _ = run(rtx, tmp_path, True, False)
+    for k in ref:
+        assert np.array_equal(ref[k], got[k]), k
+
+
 def test_sync_on_null_stream_then_other_stream(rtx, oracle, tmp_path, default_scene):
     """rt_sync with the renderer on the null stream (set_stream(0), torch's default stream) must
     still issue the deferred denoise and wait for every renderer stream: G-buffers bound as torch

@@ -388,12 +388,13 @@ int rt_frame_init(rt_context* ctx) {
         HIP_TRY(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         const int perCu = rtk_trace_queue_blocks_per_cu();
         if (cus <= 0) cus = 256;
-        ws.persistBlocks = (uint32_t)(cus * (perCu > 0 ? perCu : 4));
-        // the queue tracers run one block per CU below their residency (5 at 32 KiB of LDS stack
-        // each): a bounce queue then holds more rays than lanes, so lanes refill as rays finish,
-        // and the CUs keep room for the denoise and next-frame waves beside the traversal tail
-        // (measured: DESIGN.md §7)
-        int tracePerCu = perCu > 2 ? perCu - 2 : 1, trace4PerCu = 1;
+        // grid of the persistent shade / resume kernels: 5 workgroups per CU (measured)
+        ws.persistBlocks = (uint32_t)(cus * 5);
+        // the queue tracers run below their residency (5 workgroups per CU at 32 KiB of LDS
+        // stack each): queue 3 at 3 per CU, queue 4 at 1, so a bounce queue holds
+        // more rays than lanes, lanes refill as rays finish, and the CUs keep room for the
+        // denoise and next-frame waves beside the traversal tail (measured: DESIGN.md §7)
+        int tracePerCu = perCu >= 3 ? 3 : (perCu > 0 ? perCu : 1), trace4PerCu = 1;
         if (const char* a = getenv("RTX_TRACE_PER_CU"))  // tuning aids
             if (atoi(a) > 0 && atoi(a) <= perCu) tracePerCu = atoi(a);
         if (const char* a = getenv("RTX_TRACE4_PER_CU"))

@@ -275,8 +275,7 @@ RT_DEV float ray_cone_width(const PathTraceParams& P, int ix, int iy) {
 // tracer).  An intersection at a step >= kDeferFrom is not traced here: the step is returned
 // and the caller queues the ray.  Returns 5 when the path is complete.
 template <int kDeferFrom, bool kMF>
-RT_DEV int run_path(PathCtx& c, PathVars& v, int k0, const HitInfo* hit, const SceneView& sc, uint32_t* stkA,
-                    float* stkT) {
+RT_DEV int run_path(PathCtx& c, PathVars& v, int k0, const HitInfo* hit, const SceneView& sc, uint2* stk) {
     RayState& rs = v.rs;
 #pragma unroll 1
     for (int k = k0; k < 5; ++k) {
@@ -286,7 +285,7 @@ RT_DEV int run_path(PathCtx& c, PathVars& v, int k0, const HitInfo* hit, const S
             if (k >= kDeferFrom) return k;
             ++c.rays;
             HitInfo h;
-            intersect(sc, rs.orig, rs.dir, stkA, stkT, 256, h);
+            intersect(sc, rs.orig, rs.dir, stk, 256, h);
             c.visits += h.visits;
             c.tests += h.tests;
             apply_hit(c.P, rs, h);
@@ -430,8 +429,7 @@ __host__ __device__ inline int cam_sample_waves(uint32_t spp) { return spp >= 4 
 // gets its G-buffer texels from this kernel and never reaches the shading kernels.  The other
 // pixels keep their samples' hit records and are appended to the surface list for k_pt_shade0.
 __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
-    __shared__ uint32_t stkA[16 * 256];
-    __shared__ float stkT[16 * 256];
+    __shared__ uint2 stk[16 * 256];
     __shared__ uint32_t sob[256];
     __shared__ float4 fold[4][64];   // this round's samples: sky colour xyz, w = 1 when it hit
     __shared__ uint32_t surf[4][64]; // pixel has a sample that hit (set by its folding thread)
@@ -476,7 +474,7 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
                 trav_setup(sc, org, dir, tr);
                 trav_init(st);
                 for (int it = 0; it < 1024; ++it)
-                    if (trav_step(sc, tr, st, stkA + tid, stkT + tid, 256)) break;
+                    if (trav_step(sc, tr, st, stk + tid, 256)) break;
             }
             ++rays;
             if (P.statsOut) {
@@ -571,8 +569,7 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
 // colours the resolve kernel needs — exactly as the sequential loop of PathTrace's caller does.
 template <bool kGlossy, bool kMF>
 __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
-    __shared__ uint32_t stkA[kGlossy ? 16 * 256 : 1];
-    __shared__ float stkT[kGlossy ? 16 * 256 : 1];
+    __shared__ uint2 stk[kGlossy ? 16 * 256 : 1];
     __shared__ uint32_t sob[256];
     __shared__ float4 foldL[4][64];  // this round's samples: finished colour xyz, w = 1 when deferred
     __shared__ float4 foldA[4][64];  // their albedo
@@ -628,8 +625,7 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
                 HitInfo h;
                 finalize_hit(sc, v.rs.orig, v.rs.dir, hr.x, (int)__float_as_uint(hr.y), hr.z, hr.w, P.ws.hit0Err[q],
                              h);
-                kd = run_path<kGlossy ? 3 : 1, kMF>(c, v, 0, &h, sc, stkA + (kGlossy ? tid : 0),
-                                                     stkT + (kGlossy ? tid : 0));
+                kd = run_path<kGlossy ? 3 : 1, kMF>(c, v, 0, &h, sc, stk + (kGlossy ? tid : 0));
                 if (kd < 3) {  // cannot happen without mirror/glass materials: flag it, finish the sample
                     atomicAdd(&P.ws.counters[kCntError], 1u);
                     kd = 5;
@@ -760,7 +756,7 @@ RT_DEV int resume_entry(PathCtx& c, const PtQueue& q, const SceneView& sc, uint3
     rs.matType = MAT_SKY;
     HitInfo h;
     finalize_hit(sc, rs.orig, rs.dir, hr.x, (int)__float_as_uint(hr.y), hr.z, hr.w, herr, h);
-    return run_path<0, kMF>(c, v, kStep, &h, sc, nullptr, nullptr);
+    return run_path<0, kMF>(c, v, kStep, &h, sc, nullptr);
 }
 
 // a completed sample of a queue entry: its radiance goes to the late-resolve slot
@@ -842,8 +838,7 @@ constexpr bool kChainStaticFirst = RTX_CHAIN_STATIC != 0;  // ablation: static f
 // G-buffers are identical.  The hit records a wave reads in phase 2 are ones its own lanes wrote
 // (a workgroup-scope fence orders them), so no record crosses workgroups inside the launch.
 __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
-    __shared__ uint32_t stkA[16 * 256];
-    __shared__ float stkT[16 * 256];
+    __shared__ uint2 stk[16 * 256];
     __shared__ uint32_t sob[256];
     __shared__ uint2 ranges[4][kChainRanges];
     __shared__ uint32_t q4list[4][64];
@@ -905,7 +900,7 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
             }
             if (__ballot(active) == 0ull) break;
             if (trav_lane_steps(active, s)) {
-                const bool done = trav_step(sc, r, s, stkA + tid, stkT + tid, 256) || s.iters >= 1024u ||
+                const bool done = trav_step(sc, r, s, stk + tid, 256) || s.iters >= 1024u ||
                                   (occlusion && s.hitIdx >= 0);
                 if (done) {
                     P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);
@@ -954,7 +949,7 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
 #pragma unroll 1
                 while (__ballot(act) != 0ull) {
                     if (trav_lane_steps(act, s4)) {
-                        if (trav_step(sc, r4, s4, stkA + tid, stkT + tid, 256) || s4.iters >= 1024u || s4.hitIdx >= 0)
+                        if (trav_step(sc, r4, s4, stk + tid, 256) || s4.iters >= 1024u || s4.hitIdx >= 0)
                             act = false;
                     }
                 }

@@ -16,8 +16,7 @@
 using namespace rtd;
 
 __global__ __launch_bounds__(256) void k_trace_primary(TracePrimaryParams P) {
-    __shared__ uint32_t stkA[16 * 256];
-    __shared__ float stkT[16 * 256];
+    __shared__ uint2 stk[16 * 256];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
     const int yl = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
@@ -37,7 +36,7 @@ __global__ __launch_bounds__(256) void k_trace_primary(TracePrimaryParams P) {
     sc.nodes = (const Node*)P.nodes;
     sc.tlas = (const Node*)P.tlasNodes;
     HitInfo hi;
-    intersect(sc, org, dir, stkA + tid, stkT + tid, 256, hi);
+    intersect(sc, org, dir, stk + tid, 256, hi);
 
     const size_t p = (size_t)y * P.width + x;
     P.hitOut[p] = make_float4(hi.t, __int_as_float(hi.objectIdx), hi.u, hi.v);

@@ -27,8 +27,7 @@ constexpr int kTraceBlock = 256;
 
 template <int kStep>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) {
-    __shared__ uint32_t stkA[16 * kTraceBlock];
-    __shared__ float stkT[16 * kTraceBlock];
+    __shared__ uint2 stk[16 * kTraceBlock];
     const int tid = threadIdx.x;
     const int lane = (int)__lane_id();
     const PtQueue& q = kStep == 3 ? P.ws.q3 : P.ws.q4;
@@ -76,7 +75,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
         }
         if (__ballot(active) == 0ull) break;
         if (trav_lane_steps(active, s)) {
-            const bool done = trav_step(sc, r, s, stkA + tid, stkT + tid, kTraceBlock) || s.iters >= 1024u ||
+            const bool done = trav_step(sc, r, s, stk + tid, kTraceBlock) || s.iters >= 1024u ||
                               (occlusion && s.hitIdx >= 0);
             if (done) {
                 P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);

@@ -17,10 +17,20 @@
 
 namespace rtd {
 
+// explicit LDS (address space 3) view: reads through it are ds_read_*, whatever the compiler can
+// infer about the generic pointer it is made from (which must point into LDS)
+typedef __attribute__((address_space(3))) const unsigned long long LdsU64;
+
+typedef float F2v __attribute__((ext_vector_type(2)));
+
+// The conservative ray-box helper per world axis a = x, y, z as (near, far) pairs: o_a = (origin
+// of the near plane test, of the far plane test), s_a = (near reciprocal rounded down twice, far
+// one rounded up twice), n_a = direction component < 0.  Scalar members, no arrays: the box test
+// runs on packed pairs, and arrays of these ended up in scratch.
 struct RayBox {
-    // per world axis a = x, y, z
-    float on[3], of[3], rn[3], rf[3];
-    bool neg[3];
+    F2v o0, o1, o2;
+    F2v s0, s1, s2;
+    int n0, n1, n2;
 };
 
 RT_DEV int max_dim(F3 d) {
@@ -55,40 +65,52 @@ RT_DEV RayBox make_raybox(F3 org, F3 dir, const Box& scene, F3 inv) {
     const float ofz = comp(org, kz);
     if (comp(dir, kx) < 0.0f) { const float t = onx; onx = ofx; ofx = t; }
     if (comp(dir, ky) < 0.0f) { const float t = ony; ony = ofy; ofy = t; }
-    RayBox h;
     const float on_k[3] = {onx, ony, onz}, of_k[3] = {ofx, ofy, ofz};
     const int ks[3] = {kx, ky, kz};
+    float on[3], of[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             if (ks[q] == a) {
-                h.on[a] = on_k[q];
-                h.of[a] = of_k[q];
-                const float ia = comp(inv, a);
-                h.rn[a] = Dn(Dn(ia));
-                h.rf[a] = Up(Up(ia));
-                h.neg[a] = comp(dir, a) < 0.0f;
+                on[a] = on_k[q];
+                of[a] = of_k[q];
             }
         }
     }
+    RayBox h;
+    h.o0 = F2v{on[0], of[0]};
+    h.o1 = F2v{on[1], of[1]};
+    h.o2 = F2v{on[2], of[2]};
+    h.s0 = F2v{Dn(Dn(inv.x)), Up(Up(inv.x))};
+    h.s1 = F2v{Dn(Dn(inv.y)), Up(Up(inv.y))};
+    h.s2 = F2v{Dn(Dn(inv.z)), Up(Up(inv.z))};
+    h.n0 = dir.x < 0.0f;
+    h.n1 = dir.y < 0.0f;
+    h.n2 = dir.z < 0.0f;
     return h;
 }
 
-// box test; min/max order is irrelevant here (no NaN can arise, and the sign of a zero
-// tNear is erased by max(tNear, 0)), so the hardware 3-operand min/max are used.
-RT_DEV bool box_test(const RayBox& h, float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float& tNear) {
-    const float tnx = ((h.neg[0] ? mxx : mnx) - h.on[0]) * h.rn[0];
-    const float tny = ((h.neg[1] ? mxy : mny) - h.on[1]) * h.rn[1];
-    const float tnz = ((h.neg[2] ? mxz : mnz) - h.on[2]) * h.rn[2];
-    const float tfx = ((h.neg[0] ? mnx : mxx) - h.of[0]) * h.rf[0];
-    const float tfy = ((h.neg[1] ? mny : mxy) - h.of[1]) * h.rf[1];
-    const float tfz = ((h.neg[2] ? mnz : mxz) - h.of[2]) * h.rf[2];
-    const float tn = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), tnz);
-    const float tf = __builtin_fminf(__builtin_fminf(tfx, tfy), tfz);
-    const bool hit = tn <= tf && tf > 0.0f;
+// Box test of both children of a node (CreateRayBoxIntersectionHelper / RayAABBIntersect,
+// geometry.cuh:519-629).  Per child and axis the near and far plane distances form one packed
+// pair: ((near coord, far coord) - o_a) * s_a is one v_pk_add_f32 + one v_pk_mul_f32 (gfx950
+// packed FP32), each component rounded exactly as the scalar expression.  min/max order is
+// irrelevant here (no NaN can arise, and the sign of a zero tNear is erased by max(tNear, 0)),
+// so the hardware 3-operand min/max are used.
+RT_DEV void box_pair(const RayBox& h, float mnx, float mny, float mnz, float mxx, float mxy, float mxz, bool& hit,
+                     float& tNear) {
+    const F2v tx = (F2v{h.n0 ? mxx : mnx, h.n0 ? mnx : mxx} - h.o0) * h.s0;
+    const F2v ty = (F2v{h.n1 ? mxy : mny, h.n1 ? mny : mxy} - h.o1) * h.s1;
+    const F2v tz = (F2v{h.n2 ? mxz : mnz, h.n2 ? mnz : mxz} - h.o2) * h.s2;
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(tx.x, ty.x), tz.x);
+    const float tf = __builtin_fminf(__builtin_fminf(tx.y, ty.y), tz.y);
+    hit = tn <= tf && tf > 0.0f;
     tNear = fmx(tn, 0.0f);
-    return hit;
+}
+
+RT_DEV void box_test2(const RayBox& h, const Node& nd, bool& i1, bool& i2, float& t1, float& t2) {
+    box_pair(h, nd.q0.x, nd.q0.y, nd.q0.z, nd.q0.w, nd.q1.x, nd.q1.y, i1, t1);
+    box_pair(h, nd.q1.z, nd.q1.w, nd.q2.x, nd.q2.y, nd.q2.z, nd.q2.w, i2, t2);
 }
 
 struct TriRay {
@@ -174,8 +196,9 @@ RT_DEV Box node_merged(const Node& n) {
 
 RT_DEV F3 f3_of(float4 a) { return f3(a.x, a.y, a.z); }
 
-// stack entry: idx (15) | blasOffset (15) << 15 | isBlas << 30 | isLeaf << 31  + float t
-// stkA / stkT point at this thread's column: element k lives at [k * stride].
+// stack entry: uint2 {idx (15) | blasOffset (15) << 15 | isBlas << 30 | isLeaf << 31, bits of float t};
+// stk points at this thread's column: entry k lives at [k * stride], so a push is one
+// ds_write_b64 and a pop one ds_read_b64 (the pop loop's dependent LDS round trip).
 //
 // The traversal is split into setup / one loop iteration / hit finalisation so that the
 // inline callers (primary rays, intersect()) and the persistent queue tracer (trace_queue.hip)
@@ -258,15 +281,15 @@ RT_DEV void trav_root_miss(TravState& s) {
 // Written for a short dependent chain per iteration (a lone wave's traversal latency sets the
 // tail of the queue tracer): the node visit picks the next node and the pushed sibling with
 // selects instead of the reference's four-way branch, and there is a single branch for the push.
-RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint32_t* stkA, float* stkT, int stride) {
+RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint2* stk, int stride) {
     ++s.iters;
     bool pop;
     if (!s.cLeaf) {
         const Node nd = s.cBlas ? sc.nodes[s.cOff * 1024u + s.cIdx] : sc.tlas[s.cIdx];
         ++s.visits;
         float t1, t2;
-        const bool i1 = box_test(r.h, nd.q0.x, nd.q0.y, nd.q0.z, nd.q0.w, nd.q1.x, nd.q1.y, t1);
-        const bool i2 = box_test(r.h, nd.q1.z, nd.q1.w, nd.q2.x, nd.q2.y, nd.q2.z, nd.q2.w, t2);
+        bool i1, i2;
+        box_test2(r.h, nd, i1, i2, t1, t2);
         // one child hit: go there; both: nearer first (tie -> right), push the other
         const bool both = i1 && i2;
         const bool goLeft = both ? (t1 < t2) : i1;
@@ -277,9 +300,9 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint3
                 ++s.top;
                 const uint32_t pIdx = goLeft ? nd.q3.y : nd.q3.x;
                 const uint32_t pLeaf = goLeft ? nd.q3.w : nd.q3.z;
-                stkA[s.top * stride] = (pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) | ((s.cBlas ? 1u : 0u) << 30) |
-                                       ((pLeaf ? 1u : 0u) << 31);
-                stkT[s.top * stride] = goLeft ? t2 : t1;
+                stk[s.top * stride] = make_uint2((pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) |
+                                                     ((s.cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31),
+                                                 __float_as_uint(goLeft ? t2 : t1));
             }
         }
         pop = !i1 && !i2;
@@ -309,8 +332,11 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint3
     if (pop) {  // TestForFinish (traverse.h:88-105)
         do {
             if (s.top < 0) return true;
-            const uint32_t a = stkA[s.top * stride];
-            s.cT = stkT[s.top * stride];
+            // one 8-byte read per pop: volatile keeps the compiler from splitting it into a
+            // t read inside the loop and an index read sunk after it (two dependent round trips)
+            const unsigned long long e = *(volatile LdsU64*)(&stk[s.top * stride]);
+            const uint32_t a = (uint32_t)e;
+            s.cT = __uint_as_float((uint32_t)(e >> 32));
             --s.top;
             s.cIdx = a & 0x7FFFu;
             s.cOff = (a >> 15) & 0x7FFFu;
@@ -370,7 +396,7 @@ RT_DEV void finalize_hit(const SceneView& sc, F3 org, F3 dir, float t, int hitId
     out.hit = hit;
 }
 
-RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint32_t* stkA, float* stkT, int stride, HitInfo& out) {
+RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint2* stk, int stride, HitInfo& out) {
     TravState s;
     if (root_surely_missed(sc, org, dir)) {
         trav_root_miss(s);
@@ -379,7 +405,7 @@ RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint32_t* stkA, float
         trav_setup(sc, org, dir, r);
         trav_init(s);
         for (int it = 0; it < 1024; ++it)
-            if (trav_step(sc, r, s, stkA, stkT, stride)) break;
+            if (trav_step(sc, r, s, stk, stride)) break;
     }
     finalize_hit(sc, org, dir, s.t, s.hitIdx, s.hitU, s.hitV, s.hitErrT, out);
     out.u = s.u;

@@ -899,9 +899,14 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
                 f.resLo += k < avail ? k : avail;
             }
             if (__ballot(active) == 0ull) break;
-            if (trav_lane_steps(active, s)) {
-                const bool done = trav_step(sc, r, s, stk + tid, 256) || s.iters >= 1024u ||
-                                  (occlusion && s.hitIdx >= 0);
+            // tail (no lane can be refilled: queue drained or reserve list full): plain per-lane
+            // loop, as in k_trace_queue
+            const bool tail = f.resLo == f.resHi && (f.drained == allParts || nRanges >= (uint32_t)kChainRanges);
+            if (tail ? active : trav_lane_steps(active, s)) {
+                bool done = false;
+                do {
+                    done = trav_step(sc, r, s, stk + tid, 256) || s.iters >= 1024u || (occlusion && s.hitIdx >= 0);
+                } while (tail && !done);
                 if (done) {
                     P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);
                     P.ws.hitErr[idx] = s.hitErrT;
@@ -946,11 +951,17 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
 #if defined(RTX_CHAIN_ABL) && RTX_CHAIN_ABL == 2
                 act = false;  // timing ablation: I4 rays not traced
 #endif
+                if (nq4 < 16u) {  // few rays: plain per-lane loop (no ballots, no leaf batching)
 #pragma unroll 1
-                while (__ballot(act) != 0ull) {
-                    if (trav_lane_steps(act, s4)) {
-                        if (trav_step(sc, r4, s4, stk + tid, 256) || s4.iters >= 1024u || s4.hitIdx >= 0)
-                            act = false;
+                    while (act)
+                        if (trav_step(sc, r4, s4, stk + tid, 256) || s4.iters >= 1024u || s4.hitIdx >= 0) act = false;
+                } else {
+#pragma unroll 1
+                    while (__ballot(act) != 0ull) {
+                        if (trav_lane_steps(act, s4)) {
+                            if (trav_step(sc, r4, s4, stk + tid, 256) || s4.iters >= 1024u || s4.hitIdx >= 0)
+                                act = false;
+                        }
                     }
                 }
                 if (mine) {

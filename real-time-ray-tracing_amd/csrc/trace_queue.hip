@@ -74,9 +74,17 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
             f.resLo += k < avail ? k : avail;
         }
         if (__ballot(active) == 0ull) break;
-        if (trav_lane_steps(active, s)) {
-            const bool done = trav_step(sc, r, s, stk + tid, kTraceBlock) || s.iters >= 1024u ||
-                              (occlusion && s.hitIdx >= 0);
+        // Tail: this wave's reserve is empty and every part drained, so no lane can be refilled.
+        // The remaining rays then run in a plain per-lane loop, without the refill ballots and the
+        // leaf batching (a wave in the tail has few lanes left, and its iteration latency is the
+        // kernel's tail).  Each ray's steps are unchanged.
+        const bool tail = f.resLo == f.resHi && f.drained == (1u << kParts) - 1u;
+        if (tail ? active : trav_lane_steps(active, s)) {
+            bool done = false;
+            do {
+                done = trav_step(sc, r, s, stk + tid, kTraceBlock) || s.iters >= 1024u ||
+                       (occlusion && s.hitIdx >= 0);
+            } while (tail && !done);
             if (done) {
                 P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);
                 P.ws.hitErr[idx] = s.hitErrT;

@@ -293,18 +293,16 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint2
         // one child hit: go there; both: nearer first (tie -> right), push the other
         const bool both = i1 && i2;
         const bool goLeft = both ? (t1 < t2) : i1;
-        if (both) {
-            if (s.top >= 15) {
-                ++s.dropped;
-            } else {
-                ++s.top;
-                const uint32_t pIdx = goLeft ? nd.q3.y : nd.q3.x;
-                const uint32_t pLeaf = goLeft ? nd.q3.w : nd.q3.z;
-                stk[s.top * stride] = make_uint2((pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) |
-                                                     ((s.cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31),
-                                                 __float_as_uint(goLeft ? t2 : t1));
-            }
+        const bool push = both && s.top < 15;  // a push onto a full stack is dropped
+        s.dropped += (both && !push) ? 1u : 0u;
+        if (push) {
+            const uint32_t pIdx = goLeft ? nd.q3.y : nd.q3.x;
+            const uint32_t pLeaf = goLeft ? nd.q3.w : nd.q3.z;
+            stk[(s.top + 1) * stride] = make_uint2((pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) |
+                                                       ((s.cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31),
+                                                   __float_as_uint(goLeft ? t2 : t1));
         }
+        s.top += push ? 1 : 0;
         pop = !i1 && !i2;
         if (!pop) {
             s.cIdx = goLeft ? nd.q3.x : nd.q3.y;

@@ -569,9 +569,9 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     }
     // the fused bounce chain shortens a serial frame; pipelined frames keep the four lean kernels,
     // beside which the next frame's camera waves fit (k_pt_chain's 168 VGPRs at 3 waves/SIMD leave
-    // them no room), except on a rank of 8 or more, whose strip's camera rays are few and whose
-    // frame the traversal tails dominate
-    p.ws.chain = fr.ws.chain == 2 || (fr.ws.chain == 1 && (!ctx->postStream || ctx->stripCount >= 8));
+    // them no room); on ranks of 8 strips too, since the queue tracers' refill-free tail loops
+    // (0.436 vs 0.450 ms per rank frame)
+    p.ws.chain = fr.ws.chain == 2 || (fr.ws.chain == 1 && !ctx->postStream);
     if (with_detail) {  // per-pixel counters: everything in order on the context stream
         if (ctx->postStream && (rc = sync_streams(ctx)) != RT_OK) return rc;
         HIP_TRY(ctx, hipMemsetAsync(fr.rays, 0, (size_t)ctx->renderW * ctx->renderH * 4, ctx->stream));
@@ -924,8 +924,7 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
     ctx->cameraGated = false;
     // the next frame's camera rays: ungated on one GPU (they run beside this frame's shade and
     // queue-3 traversal), after this frame's trace<3> on two GPUs and its resume<3> on four, where
-    // a rank's tails are shorter, and after its shade on eight (beside the fused chain) (measured
-    // per N: DESIGN.md §7)
+    // a rank's tails are shorter, and after its shade on eight (measured per N: DESIGN.md §7)
     ctx->cameraAfter = ctx->stripCount == 1 ? 0 : ctx->stripCount == 2 ? 2 : ctx->stripCount < 8 ? 3 : 1;
     if (const char* a = getenv("RTX_OVERLAP_AFTER")) ctx->overlapAfter = atoi(a);  // tuning aids
     if (const char* a = getenv("RTX_CAMERA_AFTER")) ctx->cameraAfter = atoi(a);

@@ -58,9 +58,9 @@ def test_pipelined_frames_match_serial(rtx, tmp_path):
 
 @pytest.mark.parametrize("chain", ["always", "off"])
 def test_pipelined_chain_modes_match_serial(rtx, tmp_path, monkeypatch, chain):
-    """The bounce chain as one launch (k_pt_chain: what serial frames, and pipelined frames on
-    8-strip ranks, run) and as four kernels (pipelined frames on 1-4 ranks), each pipelined,
-    against serial frames (k_pt_chain): identical outputs."""
+    """The bounce chain as one launch (k_pt_chain: what serial frames run) and as four kernels
+    (what pipelined frames run), each pipelined, against serial frames (k_pt_chain): identical
+    outputs."""
     ref, _, _ = run(rtx, tmp_path, False, False)
     monkeypatch.setenv("RTX_CHAIN", chain)
     got, _, _ = run(rtx, tmp_path, True, False)

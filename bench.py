@@ -153,8 +153,40 @@ def cpu_baseline(width, height, spp):
                      "(oracle/pathtrace.cpp, full PathTrace incl. traversal, textures, sky) on %d host threads; "
                      "legs: LBVH build of both scenes (oracle/bvh.cpp, batches over threads), full-frame primary "
                      "traversal" % (width, rows, width, height, spp, reps, threads))
+    legs["c1_frame_256"] = c1_frame(O, threads)
     out["legs"] = legs
     return out
+
+
+def c1_frame(O, threads, size=256):
+    """BASELINE config 1 on the host: the default scene at 256x256, 1 spp, one whole frame on the
+    CPU (LBVH build, PathTrace, the 13-pass denoise + post), ending in an HDR dump (PFM of the
+    pre-tone-map colour) - the oracle's restatement of the reference path, no GPU involved."""
+    t0 = time.perf_counter()
+    v, i, n = O.scene(1)  # init (init.cu): scene input, sky tables, textures, denoiser state
+    nrm = O.smooth_normals(v, i)
+    sky, tex = O.sky(), O.textures()
+    dn = O.Denoiser(size, size)
+    t1 = time.perf_counter()
+    bvh = O.build_bvh(v, i, n, nrm, threads=threads)
+    t2 = time.perf_counter()
+    g = O.pathtrace(bvh, size, size, frame_num=1, spp=1, sky_out=sky, tex=tex, threads=threads)
+    t3 = time.perf_counter()
+    out = dn.draw(g, 1)
+    t4 = time.perf_counter()
+    hdr = out["scaled"].view(np.float16).astype(np.float32).reshape(size, size, 4)[::-1, :, :3]
+    path = os.path.join(tempfile.gettempdir(), "rtx_c1_%d.pfm" % os.getpid())
+    with open(path, "wb") as f:  # PFM: bottom row first, little-endian scale
+        f.write(b"PF\n%d %d\n-1.0\n" % (size, size))
+        f.write(np.ascontiguousarray(hdr, dtype="<f4").tobytes())
+    t5 = time.perf_counter()
+    os.remove(path)
+    rays = int(g["rays"].sum(dtype=np.uint64))
+    ms = lambda a, b: round((b - a) * 1e3, 3)
+    return {"size": [size, size], "spp": 1, "threads": threads, "init_ms": ms(t0, t1),
+            "lbvh_build_ms": ms(t1, t2), "path_trace_ms": ms(t2, t3), "denoise_post_ms": ms(t3, t4),
+            "hdr_dump_ms": ms(t4, t5), "frame_ms": ms(t1, t5), "rays": rays,
+            "path_trace_mray_s": round(rays / max(t3 - t2, 1e-9) / 1e6, 3)}
 
 
 def pmc_kernels():

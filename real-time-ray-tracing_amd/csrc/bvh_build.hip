@@ -237,7 +237,9 @@ RT_DEV void sort_and_build(Lds& s, int n, uint32_t* mortonOut, uint32_t* reorder
     reorderOut[t] = s.idx[1][t];
     karras(s, n);
     __syncthreads();
-    refit(s, n, nodes);
+#if !(defined(RTX_BVH_ABL) && RTX_BVH_ABL == 3)
+    refit(s, n, nodes);  // (ablation 3: no refit; timing only)
+#endif
 }
 
 }  // namespace
@@ -303,6 +305,10 @@ __global__ __launch_bounds__(kT) void k_build_bvh(BvhBuildParams P) {
     }
     __syncthreads();
     if (!s.isLast) return;
+#if defined(RTX_BVH_ABL) && RTX_BVH_ABL == 1
+    if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;  // timing ablation: no TLAS
+#endif
 
     // ---- TLAS (UpdateTLAS, updateGeometry.cuh:264-364; then sort + Karras over B keys)
     s.arrive[t] = 0u;

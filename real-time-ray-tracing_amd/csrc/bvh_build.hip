@@ -242,9 +242,56 @@ RT_DEV void sort_and_build(Lds& s, int n, uint32_t* mortonOut, uint32_t* reorder
 #endif
 }
 
+// The TLAS of a scene of at most 64 batches, built by wave 0 of the last workgroup alone: the
+// same results as the 1024-thread path (UpdateTLAS + RadixSort + BuildLBVH over B keys) without
+// its ~20 workgroup barriers.  The stable sort is a rank count (keys below, plus equal keys of
+// lower index: a stable sort's position); the 1024 - B padding keys (0xFFFFFFFF) keep their
+// order after the real ones, as the radix sort leaves them.  LDS written by one lane and read by
+// another is ordered by wavefront-scope fences.
+RT_DEV void tlas_wave(Lds& s, const BvhBuildParams& P, uint32_t B) {
+    const int lane = threadIdx.x;  // 0..63
+    const Node* nodes = (const Node*)P.nodes;
+    s.arrive[lane] = 0u;
+    Box rb = box_empty();
+    F3 rc = f3(0.0f);
+    if ((uint32_t)lane < B) {
+        const Node nd = nodes[(size_t)lane * kT];
+        Box l, r;
+        l.mn = f3(nd.q0.x, nd.q0.y, nd.q0.z); l.mx = f3(nd.q0.w, nd.q1.x, nd.q1.y);
+        r.mn = f3(nd.q1.z, nd.q1.w, nd.q2.x); r.mx = f3(nd.q2.y, nd.q2.z, nd.q2.w);
+        rb = box_merge(l, r);
+        rc = (rb.mx + rb.mn) / 2.0f;
+        store_box(P.tlasAabbs + 6 * (size_t)lane, rb);
+    }
+    store_box(s.leaf[lane], rb);
+    // the quirk reduction keeps slots with (s & 255) < 128: every slot below 64
+    const Box quirk = wave_reduce(rb);
+    const uint32_t key = (uint32_t)lane < B ? morton_of(rc, quirk) : 0xFFFFFFFFu;
+    if (lane == 0) store_box(P.tlasSceneAabb, quirk);
+    uint32_t rank = 0;
+#pragma unroll 8
+    for (int j = 0; j < 64; ++j) {
+        const uint32_t kj = __shfl(key, j);
+        rank += (kj < key || (kj == key && j < lane)) ? 1u : 0u;
+    }
+    s.key[1][rank] = key;
+    s.idx[1][rank] = (uint16_t)lane;
+    for (int t = lane; t < kT; t += 64) {
+        P.tlasMorton[t] = t < 64 ? 0u : 0xFFFFFFFFu;  // rows < 64 rewritten below
+        P.tlasReorder[t] = (uint32_t)t;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    P.tlasMorton[lane] = s.key[1][lane];
+    P.tlasReorder[lane] = s.idx[1][lane];
+    karras(s, (int)B);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    refit(s, (int)B, (Node*)P.tlasNodes);
+    if (lane == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
-__global__ __launch_bounds__(kT) void k_build_bvh(BvhBuildParams P) {
+__global__ __launch_bounds__(kT, 8) void k_build_bvh(BvhBuildParams P) {  // 8 waves/SIMD = 2 workgroups per CU: <= 64 VGPRs
     __shared__ Lds s;
     const int t = threadIdx.x;
     const uint32_t b = blockIdx.x;
@@ -305,6 +352,10 @@ __global__ __launch_bounds__(kT) void k_build_bvh(BvhBuildParams P) {
     }
     __syncthreads();
     if (!s.isLast) return;
+    if (B <= 64u) {  // small TLAS: wave 0 alone
+        if (t < 64) tlas_wave(s, P, B);
+        return;
+    }
 #if defined(RTX_BVH_ABL) && RTX_BVH_ABL == 1
     if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;  // timing ablation: no TLAS

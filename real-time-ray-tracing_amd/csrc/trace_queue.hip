@@ -81,10 +81,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
         const bool tail = f.resLo == f.resHi && f.drained == (1u << kParts) - 1u;
         if (tail ? active : trav_lane_steps(active, s)) {
             bool done = false;
-            do {  // two steps per trip in the tail: the loop's exec-mask bookkeeping once per two
+            do {  // two steps per trip: the loop's refill / exec-mask bookkeeping once per two
                 done = trav_step(sc, r, s, stk + tid, kTraceBlock) || s.iters >= 1024u ||
                        (occlusion && s.hitIdx >= 0);
-                if (tail && !done)
+                if (!done && (tail || trav_lane_steps(true, s)))
                     done = trav_step(sc, r, s, stk + tid, kTraceBlock) || s.iters >= 1024u ||
                            (occlusion && s.hitIdx >= 0);
             } while (tail && !done);

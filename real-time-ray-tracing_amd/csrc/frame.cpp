@@ -394,7 +394,10 @@ int rt_frame_init(rt_context* ctx) {
         // stack each): queue 3 at 3 per CU, queue 4 at 1, so a bounce queue holds
         // more rays than lanes, lanes refill as rays finish, and the CUs keep room for the
         // denoise and next-frame waves beside the traversal tail (measured: DESIGN.md §7)
-        int tracePerCu = perCu >= 3 ? 3 : (perCu > 0 ? perCu : 1), trace4PerCu = 1;
+        // (one GPU: queue 3 at 2 per CU, which leaves the next frame's camera waves more room:
+        // 1.091 -> 1.081 ms/frame, tools/env_grid.sh, four repeats)
+        const int want3 = ctx->stripCount == 1 ? 2 : 3;
+        int tracePerCu = perCu >= want3 ? want3 : (perCu > 0 ? perCu : 1), trace4PerCu = 1;
         if (const char* a = getenv("RTX_TRACE_PER_CU"))  // tuning aids
             if (atoi(a) > 0 && atoi(a) <= perCu) tracePerCu = atoi(a);
         if (const char* a = getenv("RTX_TRACE4_PER_CU"))

@@ -394,15 +394,17 @@ int rt_frame_init(rt_context* ctx) {
         // stack each): queue 3 at 3 per CU, queue 4 at 1, so a bounce queue holds
         // more rays than lanes, lanes refill as rays finish, and the CUs keep room for the
         // denoise and next-frame waves beside the traversal tail (measured: DESIGN.md §7)
-        // (one GPU: queue 3 at 2 per CU, which leaves the next frame's camera waves more room:
-        // 1.091 -> 1.081 ms/frame, tools/env_grid.sh, four repeats)
-        const int want3 = ctx->stripCount == 1 ? 2 : 3;
-        int tracePerCu = perCu >= want3 ? want3 : (perCu > 0 ? perCu : 1), trace4PerCu = 1;
+        int tracePerCu = perCu >= 3 ? 3 : (perCu > 0 ? perCu : 1), trace4PerCu = 1;
         if (const char* a = getenv("RTX_TRACE_PER_CU"))  // tuning aids
             if (atoi(a) > 0 && atoi(a) <= perCu) tracePerCu = atoi(a);
         if (const char* a = getenv("RTX_TRACE4_PER_CU"))
             if (atoi(a) > 0 && atoi(a) <= perCu) trace4PerCu = atoi(a);
         ws.traceBlocks = (uint32_t)(cus * tracePerCu);
+        // one GPU: a short queue 3 (below kTrace3Short rays, the default view's 323 k) is traced by
+        // 2 workgroups per CU, which leaves the next frame's camera waves more room (1.091 -> 1.081
+        // ms/frame, four repeats); a long one (the terrain view) keeps all of them (2 per CU there:
+        // 4.14 -> 4.44 ms); strip ranks keep 3 (at 2 ranks 0.710 vs 0.727 ms, equal at 4 and 8)
+        ws.trace3ShortBlocks = ctx->stripCount == 1 ? (uint32_t)(cus * 2) : 0u;
         ws.chain = 1;  // RTX_CHAIN=off|serial|always: A/B aid (default serial)
         if (const char* a = getenv("RTX_CHAIN")) ws.chain = strcmp(a, "off") == 0 ? 0 : strcmp(a, "always") == 0 ? 2 : 1;
         ws.trace4Blocks = (uint32_t)(cus * trace4PerCu);

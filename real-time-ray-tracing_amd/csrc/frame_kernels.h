@@ -102,6 +102,7 @@ struct PtWorkspace {
     uint32_t cap;               // entries per queue (= rows * W * spp)
     uint32_t persistBlocks;     // grid of the persistent queue kernels
     uint32_t traceBlocks;       // grid of the queue tracer of queue 3 (k_trace_queue)
+    uint32_t trace3ShortBlocks = 0;  // its workgroups that run when queue 3 is short (0: all)
     uint32_t trace4Blocks;      // ... of queue 4 (a short queue: a few percent of queue 3)
     int glossy;                 // materials can be glossy: steps 1-2 may trace (materialOverride)
     int microfacet;             // materials can be the microfacet one (materialOverride 4): GGX compiled in

@@ -24,6 +24,7 @@ using namespace rtd;
 namespace {
 
 constexpr int kTraceBlock = 256;
+constexpr uint32_t kTrace3Short = 1u << 20;  // queue-3 length below which trace3ShortBlocks apply
 
 template <int kStep>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) {
@@ -39,9 +40,15 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
     sc.nodes = (const Node*)P.nodes;
     sc.tlas = (const Node*)P.tlasNodes;
 
+    // a short queue 3 runs on the first trace3ShortBlocks workgroups only (frame.cpp); the others
+    // leave before taking any work, and the static first batches are cut over the ones that stay
+    uint32_t blocks = gridDim.x;
+    if (kStep == 3 && P.ws.trace3ShortBlocks != 0u && n < kTrace3Short && P.ws.trace3ShortBlocks < blocks)
+        blocks = P.ws.trace3ShortBlocks;
+    if (blockIdx.x >= blocks) return;
     const uint32_t wavesPerBlock = kTraceBlock / 64;
     Fetch f;
-    fetch_init(f, n, gridDim.x * wavesPerBlock, blockIdx.x * wavesPerBlock + (uint32_t)(tid >> 6));
+    fetch_init(f, n, blocks * wavesPerBlock, blockIdx.x * wavesPerBlock + (uint32_t)(tid >> 6));
 
     bool active = false, exhausted = false, occlusion = false;
     uint32_t idx = 0, accV = 0, accT = 0;

@@ -183,6 +183,7 @@ typedef struct rt_info {
     int32_t denoiseRowBegin, denoiseRowEnd; /* rows of a strip-local denoise (rt_set_collective_hook) */
     int32_t gbufferRowBegin, gbufferRowEnd; /* G-buffer rows the next denoise reads: its strip plus
                                                halo when it is strip-local, else the whole frame */
+    int32_t stripLocalDenoise;  /* 1: the next denoise is strip-local (the same on every rank) */
 } rt_info;
 
 int rt_get_info(const rt_context* ctx, rt_info* out);
@@ -371,7 +372,8 @@ enum rt_array_name {
                                     (rt_path_trace with_detail) */
     RT_ARR_TEX_ALBEDO_AO = 37,   /* ushort4, 11-level mip chain of 1024^2 (levels concatenated, 1024 -> 1) */
     RT_ARR_TEX_NORMAL_ROUGHNESS = 38, /* ushort4, same layout */
-    RT_ARR_TEX_HEIGHT = 39       /* ushort, same layout (zero unless uploaded) */
+    RT_ARR_TEX_HEIGHT = 39,      /* ushort, same layout (zero unless uploaded) */
+    RT_ARR_HDR = 40              /* float4[W*H] pre-tone-map HDR of the last rt_draw / rt_denoise_post with_hdr */
 };
 int rt_download(const rt_context* ctx, int what, void* dst, size_t bytes);
 

@@ -498,7 +498,11 @@ int rt_get_info(const rt_context* ctx, rt_info* out) {
     out->denoiseRowBegin = (int32_t)a;
     out->denoiseRowEnd = (int32_t)b;
     uint32_t sa = 0, sb = 0, lo = 0, hi = (uint32_t)ctx->renderH;
-    if (ctx->inited && strip_local_denoise(ctx, sa, sb)) gbuffer_rows((uint32_t)ctx->renderH, sa, sb, lo, hi);
+    out->stripLocalDenoise = 0;
+    if (ctx->inited && strip_local_denoise(ctx, sa, sb)) {
+        gbuffer_rows((uint32_t)ctx->renderH, sa, sb, lo, hi);
+        out->stripLocalDenoise = 1;
+    }
     out->gbufferRowBegin = (int32_t)lo;
     out->gbufferRowEnd = (int32_t)hi;
     return RT_OK;
@@ -718,6 +722,7 @@ size_t rt_array_bytes(const rt_context* ctx, int what) {
             return ((w16 + 3) / 4) * ((h16 + 3) / 4) * 8;
         }
         case RT_ARR_RGBA8: return (size_t)ctx->screenW * ctx->screenH * 4;
+        case RT_ARR_HDR: return P * 16;
         case RT_ARR_PT_STATS: return P * 16;
         case RT_ARR_TEX_ALBEDO_AO: case RT_ARR_TEX_NORMAL_ROUGHNESS: return (size_t)kTexTexels * 8;
         case RT_ARR_TEX_HEIGHT: return (size_t)kTexTexels * 2;
@@ -768,6 +773,7 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
         case RT_ARR_RGBA8:  // the last frame's output, wherever it was drawn (rt_draw_device)
             if (bytes < rt_array_bytes(ctx, what)) { ctx->err = "destination too small"; return RT_ERR_ARG; }
             return copy_rgba_out(ctx, dst);
+        case RT_ARR_HDR: src = ctx->fr.hdr; break;
         case RT_ARR_PT_STATS: src = ctx->fr.ptStats; break;
         case RT_ARR_TEX_ALBEDO_AO: src = ctx->fr.texAlbedo; break;
         case RT_ARR_TEX_NORMAL_ROUGHNESS: src = ctx->fr.texNormal; break;

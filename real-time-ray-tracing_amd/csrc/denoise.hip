@@ -1142,7 +1142,7 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         if ((e = hipMemcpyAsync(P->histDepth, P->depth, Pn * 2, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
     }
     P->finalColor = cur;
-    if (P->hdrOut) {
+    if (P->hdrOut && !P->stripLocal) {  // strip-local: after the rows exchange (rtk_hdr_out, frame.cpp)
         hipLaunchKernelGGL(k_hdr_out, dim3((unsigned)((Pn + 255) / 256)), b256, 0, s, (const uint2*)cur, P->hdrOut, Pn);
         LAUNCH_CHECK();
     }
@@ -1180,6 +1180,12 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         }
     }
     return hipSuccess;
+}
+
+extern "C" hipError_t rtk_hdr_out(const uint2* color, float4* hdr, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hdr_out, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, color, hdr, n);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t rtk_denoise_post(DenoisePostParams* P, hipStream_t s) {

@@ -209,9 +209,10 @@ bool strip_local_denoise(const rt_context* ctx, uint32_t& a, uint32_t& b) {
     const uint32_t H = (uint32_t)ctx->renderH;
     a = 0;
     b = H;
+    // TemporalFilter2 on: its output (the exchanged history buffer) is then the frame's final HDR
     const bool strip = ctx->stripCount > 1 && ctx->hook != nullptr && !ps.enableNoiseLevelVisualize &&
                        !(ps.enablePostProcess && (ps.enableBloomEffect || ps.enableLensFlare)) &&
-                       ctx->screenW == ctx->renderW && ctx->screenH == ctx->renderH;
+                       ps.enableTemporalDenoising2 && ctx->screenW == ctx->renderW && ctx->screenH == ctx->renderH;
     uint32_t sa = 0, sb = H;
     if (!strip || !denoise_rows(H, (uint32_t)ctx->stripCount, (uint32_t)ctx->stripIndex, sa, sb)) return false;
     a = sa;
@@ -222,15 +223,26 @@ bool strip_local_denoise(const rt_context* ctx, uint32_t& a, uint32_t& b) {
 int run_denoise(rt_context* ctx, DenoisePostParams& p, hipStream_t s) {
     rt_strip_exchange x{p.frameNum, (int32_t)p.rowA, (int32_t)p.rowB, p.histOutSet};
     HIP_TRY(ctx, rtk_denoise_phase(&p, s, 0));
-    if (p.stripLocal && ctx->hook(ctx->hookArg, RT_HOOK_HISTOGRAM, (void*)s, &x) != 0) {
+    // the histogram is recomputed only with the post chain on; summing a stale one again would
+    // multiply it by the rank count every frame
+    if (p.stripLocal && p.postProcess && ctx->hook(ctx->hookArg, RT_HOOK_HISTOGRAM, (void*)s, &x) != 0) {
         ctx->err = "collective hook failed (histogram)";
         return RT_ERR_STATE;
     }
     HIP_TRY(ctx, rtk_denoise_phase(&p, s, 1));
-    if (p.stripLocal && ctx->hook(ctx->hookArg, RT_HOOK_ROWS, (void*)s, &x) != 0) {
+    if (!p.stripLocal) return RT_OK;
+    if (ctx->hook(ctx->hookArg, RT_HOOK_ROWS, (void*)s, &x) != 0) {
         ctx->err = "collective hook failed (rows)";
         return RT_ERR_STATE;
     }
+    // whole-frame outputs exist only after the exchange: the HDR copy of the final colour (the
+    // exchanged history buffer) and the caller's draw target (k_scale_post wrote this rank's rows
+    // into the exchanged RGBA8 buffer)
+    const size_t W = p.W, H = p.H;
+    if (p.hdrOut) HIP_TRY(ctx, rtk_hdr_out(p.finalColor, p.hdrOut, W * H, s));
+    if (p.rgbaTarget)
+        HIP_TRY(ctx, hipMemcpy2DAsync(p.rgbaTarget, (size_t)p.rgbaTargetPitch * 4, p.rgba, (size_t)p.Ws * 4,
+                                      (size_t)p.Ws * 4, (size_t)p.Hs, hipMemcpyDeviceToDevice, s));
     return RT_OK;
 }
 
@@ -693,10 +705,14 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.exposure = fr.exposure;
     p.scaledA = fr.scaledA;
     p.scaledB = fr.scaledB;
-    p.rgba = fr.drawTarget ? fr.drawTarget : fr.rgba;  // rt_draw_device: the caller's device target
-    p.rgbaPitch = fr.drawTarget ? fr.drawPitch : (uint32_t)ctx->screenW;
-    fr.outRgba = p.rgba;
-    fr.outPitch = p.rgbaPitch;
+    // rt_draw_device: the caller's device target; a strip-local denoise writes its rows into the
+    // exchanged buffer instead and copies the whole frame to the target after the rows exchange
+    p.rgbaTarget = (p.stripLocal && fr.drawTarget) ? fr.drawTarget : nullptr;
+    p.rgbaTargetPitch = fr.drawTarget ? fr.drawPitch : 0u;
+    p.rgba = (fr.drawTarget && !p.stripLocal) ? fr.drawTarget : fr.rgba;
+    p.rgbaPitch = (fr.drawTarget && !p.stripLocal) ? fr.drawPitch : (uint32_t)ctx->screenW;
+    fr.outRgba = fr.drawTarget ? fr.drawTarget : fr.rgba;
+    fr.outPitch = fr.drawTarget ? fr.drawPitch : (uint32_t)ctx->screenW;
     p.bluenoise = ctx->dBlueNoise;
     p.hdrOut = with_hdr ? fr.hdr : nullptr;
     p.bloom = ps.enablePostProcess && ps.enableBloomEffect;

@@ -201,12 +201,16 @@ struct DenoisePostParams {
     int stripLocal;             // multi-GPU: compute only what rows [rowA, rowB) need (rtk_denoise_phase)
     uint32_t rowA, rowB;        // this context's output rows (64-row aligned; [0, H) when not strip-local)
     int histOutSet;             // which buffer of the history pair histColorOut is (the hook reports it)
+    uint32_t* rgbaTarget;       // strip-local: the caller's draw target, filled from `rgba` after the rows
+    uint32_t rgbaTargetPitch;   // exchange (rgba is then the exchanged buffer); pitch in pixels
     int ty0, ty1;               // per launch (set by the launcher): tile rows of the 16x16-tile kernels
 };
 
 extern "C" hipError_t rtk_denoise_post(DenoisePostParams* p, hipStream_t stream);
 // phase 0: denoise .. DownScale4 + Histogram2; phase 1: AutoExposure .. RGBA8 (finalColor of phase 0 in)
 extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* p, hipStream_t stream, int phase);
+// the render-size float4 HDR copy (rt_draw's hdr_out) of a denoised colour buffer
+extern "C" hipError_t rtk_hdr_out(const uint2* color, float4* hdr, size_t n, hipStream_t stream);
 
 extern "C" hipError_t rtk_launch_sky(const SkyGenParams* p, hipStream_t stream);
 // MipmapGen (texture.hip): levels 1.. of a square 16-bit chain whose level 0 is in place

@@ -61,7 +61,9 @@ class FramePipeline:
             move = self.gather.gather
             if self.need is not None:  # strip-local denoise this frame: only the rows it reads
                 i = rt.info()
-                if (i.gbufferRowBegin, i.gbufferRowEnd) != (0, i.renderHeight):
+                # decided by the renderer's flag, the same on every rank (a rank's G-buffer rows can
+                # span the whole frame while its peers' do not: all ranks must enter one collective)
+                if i.stripLocalDenoise:
                     if (i.gbufferRowBegin, i.gbufferRowEnd) != self.need[self.rank]:
                         raise RuntimeError("renderer and host disagree on the strip's G-buffer rows")
                     move = lambda: self.gather.exchange(self.need)  # noqa: E731

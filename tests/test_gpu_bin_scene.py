@@ -80,3 +80,49 @@ def test_bin_terrain_frame(rtx, oracle, tmp_path, ntri):
         assert np.array_equal(rgba.reshape(-1, 4), o["rgba"]), f
         assert np.array_equal(rt.get_buffer("RENDER_COLOR", (w * h, 4), np.uint16), o["color"]), f
     rt.cleanup()
+
+
+def test_one_triangle_last_batch(rtx, oracle, tmp_path):
+    """N = 1,025: the last BLAS batch holds 1 real triangle and 3 padding ones (triCountArray = 1,
+    init.cu:104-130), the triCount == 1 branch of BuildLBVH (buildBVH.cuh:31-38).  The reference
+    writes that node to bvhNodes[0] BEFORE the per-batch offset, racing batch 0's own root and
+    leaving batch 1's root unwritten; here it is written to the batch's own node 0 (DESIGN.md §5,
+    deviation 12).  Batch 0 (1,024 triangles), batch 1's root, the 2-leaf TLAS, Morton codes and
+    traversal hits on the lone triangle are bit-exact vs the oracle, and a full frame renders."""
+    tris = terrain_patch(23, 23)[:1025]
+    path = write_bin(str(tmp_path / "n1025.bin"), tris)
+    w, h = 96, 64
+    rt = make(rtx, tmp_path, path, w, h)
+    info = rt.info()
+    assert (info.triCount, info.triCountPadded, info.batchCount) == (1025, 1028, 2)
+    b, _, _, n = bin_bvh(oracle, path)
+    rt.build_bvh()
+    nodes = rt.download("NODES").view(rtx.NODE_DTYPE)
+    assert nodes[:1023].tobytes() == b["nodes"][:1023].tobytes()  # batch 0 keeps its own root
+    root1 = nodes[1024]
+    assert root1.tobytes() == b["nodes"][1024].tobytes()
+    assert (int(root1["idxLeft"]), int(root1["idxRight"]), int(root1["isLeftLeaf"]), int(root1["isRightLeaf"])) == (0, 0, 1, 1)
+    tl = rt.download("TLAS_NODES").view(rtx.NODE_DTYPE)[:1]
+    assert tl.tobytes() == b["tlas_nodes"][:1].tobytes()
+    assert np.array_equal(rt.download("MORTON", np.uint32)[:2048], b["morton"])
+    assert np.array_equal(rt.download("REORDER", np.uint32)[:2048], b["reorder"])
+    # rays straight down onto the centroids of the last triangles (1,024 is the lone one of batch 1)
+    c = tris[1016:1025].mean(axis=1)
+    org = np.stack([c[:, 0], np.full(len(c), 20.0, np.float32), c[:, 2]], axis=1).astype(np.float32)
+    dirs = np.tile(np.array([0.0, -1.0, 0.0], np.float32), (len(c), 1))
+    t, tri, u, v, ms = rt.trace_rays(org, dirs)
+    o = oracle.intersect(b, np.concatenate([org, dirs], axis=1))
+    assert int(tri[-1]) == 1024
+    assert np.array_equal(tri, o["objectIdx"]) and np.array_equal(t.view(np.uint32), o["t"].view(np.uint32))
+    rgba = np.zeros((h, w, 4), np.uint8)
+    cam = rtx.Camera()
+    cam.pos[:] = (5.5, 4.0, -3.0)
+    cam.yaw, cam.pitch, cam.focal, cam.aperture, cam.fovX = 0.0, -0.55, 5.0, 0.001, np.float32(90.0) * np.float32(0.01745329251)
+    rt.camera = cam
+    rt.draw(rgba)
+    oc = oracle.default_camera(w, h)
+    oc.pos[:] = (5.5, 4.0, -3.0)
+    oc.pitch = -0.55
+    gb = oracle.pathtrace(b, w, h, frame_num=1, spp=1, cam=oc, hist_cam=oc, sky_out=oracle.sky(), tex=oracle.textures())
+    assert np.array_equal(rgba.reshape(-1, 4), oracle.Denoiser(w, h).draw(gb, 1, delta_time=16.667)["rgba"])
+    rt.cleanup()

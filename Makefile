@@ -20,7 +20,7 @@ HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.hip.o,$(HIP_SRCS))
 CPP_OBJS := $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.cpp.o,$(CPP_SRCS))
 
 ORC_SRCS := $(wildcard oracle/*.cpp)
-ORC_HDRS := $(wildcard oracle/*.h) $(CSRC)/rtmath.h $(CSRC)/scene_gen.h
+ORC_HDRS := $(wildcard oracle/*.h) $(CSRC)/rtmath.h $(CSRC)/soil_textures.h
 
 all: $(LIBDIR)/librtx.so oracle/_build/liboracle.so oracle/_build/liboracle_libm.so
 
@@ -35,14 +35,14 @@ $(OBJDIR)/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
 $(LIBDIR)/librtx.so: $(HIP_OBJS) $(CPP_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^ -ldl
 
-oracle/_build/liboracle.so: $(ORC_SRCS) $(ORC_HDRS) $(CSRC)/scene_gen.cpp
+oracle/_build/liboracle.so: $(ORC_SRCS) $(ORC_HDRS) $(CSRC)/soil_textures.cpp
 	@mkdir -p oracle/_build
-	$(CXX) $(CXXFLAGS) -shared -o $@ $(ORC_SRCS) $(CSRC)/scene_gen.cpp -lpthread
+	$(CXX) $(CXXFLAGS) -shared -o $@ $(ORC_SRCS) $(CSRC)/soil_textures.cpp -lpthread
 
 # the same restatement with host-libm transcendentals (parity metric, ocommon.h ORC_LIBM)
-oracle/_build/liboracle_libm.so: $(ORC_SRCS) $(ORC_HDRS) $(CSRC)/scene_gen.cpp
+oracle/_build/liboracle_libm.so: $(ORC_SRCS) $(ORC_HDRS) $(CSRC)/soil_textures.cpp
 	@mkdir -p oracle/_build
-	$(CXX) $(CXXFLAGS) -DORC_LIBM -shared -o $@ $(ORC_SRCS) $(CSRC)/scene_gen.cpp -lpthread
+	$(CXX) $(CXXFLAGS) -DORC_LIBM -shared -o $@ $(ORC_SRCS) $(CSRC)/soil_textures.cpp -lpthread
 
 clean:
 	rm -rf $(LIBDIR) oracle/_build

@@ -35,9 +35,13 @@ typedef struct rt_context rt_context;
  * chunkDim (VoxelsGenerator::kChunkDim, terrain.h:42), [render] spp, [render] device. */
 int rt_create(int screen_width, int screen_height, const char* config_toml, rt_context** out);
 
-/* RayTracer::init, init.cu:53-410: builds the procedural default scene (or loads
- * [file] inputMeshFileName when it is a meshProcessor .bin), allocates every device
- * resource, uploads blue-noise/sky tables, runs the frame-1 smooth normals. */
+/* RayTracer::init, init.cu:53-410: builds the procedural default scene, allocates every device
+ * resource, uploads blue-noise/sky tables, runs the frame-1 smooth normals.  Like the reference it
+ * ignores [file] inputMeshFileName (its LoadTrianglesFromFile call is commented out, init.cu:78-82);
+ * the extension [scene] meshFile loads a meshProcessor .bin instead (u32 count + count 128-B
+ * Triangle records, init.cu:28-50; a shorter file is refused with RT_ERR_IO).  The scene is built
+ * and checked before any device call (RT_ERR_IO / RT_ERR_ARG on any machine), then the device
+ * (RT_ERR_NO_DEVICE without a gfx950). */
 int rt_init(rt_context* ctx);
 
 /* RayTracer::draw, kernel.cu:259-398 (with UpdateFrame, kernel.cu:61-137): one synchronous
@@ -162,6 +166,11 @@ int rt_save_image(rt_context* ctx, const char* path, int kind);
 #define RT_TEX_SOIL_NORMAL_ROUGHNESS 1
 #define RT_TEX_SOIL_HEIGHT 2
 int rt_upload_texture(rt_context* ctx, int which, const uint16_t* texels, int width, int height, int channels);
+
+/* Scene input (host only, no device needed): Perlin::noise3D (perlin.h:50-78) with the reference
+ * permutation, the source of the procedural terrain's voxel heights (Chunk::Generate,
+ * terrain.cpp:5-45), at n points (xyz triples). */
+int rt_scene_noise3d(const float* xyz, size_t n, float* out);
 
 /* Determinism hooks the reference lacks: the frame counter is a function static
  * (kernel.cu:64) and AutoExposure reads wall-clock deltaTime (postprocessing.cu:46-51). */

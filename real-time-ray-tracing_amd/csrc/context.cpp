@@ -81,7 +81,15 @@ bool load_triangle_bin(const std::string& path, rtscene::SceneMesh& m, std::stri
     if (!read_file(path, blob) || blob.size() < 4) { err = "cannot read mesh file " + path; return false; }
     uint32_t n = 0;
     memcpy(&n, blob.data(), 4);
-    if (n < 2 || blob.size() < 4 + (size_t)n * 128) { err = "malformed mesh file " + path; return false; }
+    // exactly u32 count + count Triangle records of 128 B: the reference reads count * 128 bytes
+    // into an uninitialised buffer without checking the read (init.cu:33-43), so a short file
+    // (e.g. resources/models/test.bin: 32,768 records of 64 B, the older 4-vertex Triangle) would
+    // render uninitialised memory there; it is refused here
+    if (n < 2 || blob.size() < 4 + (size_t)n * 128) {
+        err = "malformed mesh file " + path + " (" + std::to_string(blob.size()) + " bytes for " + std::to_string(n) +
+              " triangles of 128 B)";
+        return false;
+    }
     m.vertices.resize((size_t)n * 9);
     m.indices.resize((size_t)n * 3);
     for (uint32_t t = 0; t < n; ++t) {
@@ -241,6 +249,12 @@ extern "C" {
 
 const char* rt_last_error(const rt_context* ctx) { return ctx ? ctx->err.c_str() : g_createError.c_str(); }
 
+int rt_scene_noise3d(const float* xyz, size_t n, float* out) {
+    if (n > 0 && (!xyz || !out)) return RT_ERR_ARG;
+    for (size_t k = 0; k < n; ++k) out[k] = rtscene::noise3d(xyz[3 * k], xyz[3 * k + 1], xyz[3 * k + 2]);
+    return RT_OK;
+}
+
 int rt_create(int screen_width, int screen_height, const char* config_toml, rt_context** out) {
     if (!out) return RT_ERR_ARG;
     *out = nullptr;
@@ -318,20 +332,8 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
 int rt_init(rt_context* ctx) {
     if (!ctx) return RT_ERR_ARG;
     if (ctx->inited) { ctx->err = "rt_init called twice"; return RT_ERR_STATE; }
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { ctx->err = "no HIP device visible"; return RT_ERR_NO_DEVICE; }
-    if (ctx->device >= 0) HIP_TRY(ctx, hipSetDevice(ctx->device));
-    int dev = 0;
-    HIP_TRY(ctx, hipGetDevice(&dev));
-    ctx->device = dev;
-    hipDeviceProp_t prop;
-    HIP_TRY(ctx, hipGetDeviceProperties(&prop, dev));
-    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-        ctx->err = std::string("librtx is built for gfx950, device is ") + prop.gcnArchName;
-        return RT_ERR_NO_DEVICE;
-    }
-
-    // ---- scene (init.cu:78-130)
+    // ---- scene (init.cu:78-130), built and checked on the host before any device call, so a bad
+    // input is reported as such on any machine
     std::string err;
     const std::string dataDir = rt_data_dir();
     if (!ctx->meshFile.empty()) {
@@ -345,10 +347,26 @@ int rt_init(rt_context* ctx) {
         }
     }
     const uint32_t N = ctx->mesh.triCount, NP = ctx->mesh.triCountPadded;
-    if (N < 2 || N > 1024u * 1024u) { ctx->err = "triangle count out of range"; return RT_ERR_ARG; }
+    // MIN_TRIANGLE_COUNT_ALLOWED 2 / MAX_TRIANGLE_COUNT_ALLOWED 1024 * 1024 (kernel.cuh:54-55), which
+    // init.cu:89-90 asserts; the reference's LBVH needs two triangles for a BLAS (buildBVH.cuh:30)
+    if (N < 2 || N > 1024u * 1024u) { ctx->err = "triangle count out of range [2, 1048576] (kernel.cuh:54-55)"; return RT_ERR_ARG; }
     ctx->B = (N + 1023) / 1024;
     if (ctx->B >= 1024) { ctx->err = "batch count must stay below 1024 (init.cu:126)"; return RT_ERR_ARG; }
     ctx->nv = (uint32_t)(ctx->mesh.vertices.size() / 3);
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { ctx->err = "no HIP device visible"; return RT_ERR_NO_DEVICE; }
+    if (ctx->device >= 0) HIP_TRY(ctx, hipSetDevice(ctx->device));
+    int dev = 0;
+    HIP_TRY(ctx, hipGetDevice(&dev));
+    ctx->device = dev;
+    hipDeviceProp_t prop;
+    HIP_TRY(ctx, hipGetDeviceProperties(&prop, dev));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        ctx->err = std::string("librtx is built for gfx950, device is ") + prop.gcnArchName;
+        return RT_ERR_NO_DEVICE;
+    }
+
 
     // the trace chain is a frame's critical path: it outranks the pipelined denoise and the next
     // frame's camera rays, whose streams are created at the lowest priority

@@ -10,6 +10,7 @@
 #include "bvh_kernels.h"
 #include "frame_kernels.h"
 #include "scene_gen.h"
+#include "soil_textures.h"
 
 struct HostCamera {  // Camera::update outputs (kernel.cuh:103-121)
     float pos[3], dir[3], left[3], up[3];

@@ -139,6 +139,7 @@ SIGNATURES = {
     "rt_load_camera": (C.c_int, [C.c_void_p, C.c_char_p]),
     "rt_save_image": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
     "rt_upload_texture": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]),
+    "rt_scene_noise3d": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p]),
 }
 IMAGE_PPM_RGBA8, IMAGE_PFM_HDR = 0, 1
 DRAW_ASYNC = 1  # rt_draw_device flag

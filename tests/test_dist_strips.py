@@ -145,7 +145,7 @@ def denoise_worker(rank, world, port, result_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        Wd, Hd = 40, 200  # 4 blocks of 64 rows (the last one short)
+        Wd, Hd = 40, (200 if world < 4 else 600)  # 4 / 10 blocks of 64 rows (the last one short)
         sd = StripDenoise(Wd, Hd, world, rank, torch.device("cpu"))
         rng = np.random.default_rng(11)
         full = dict(accum=rng.integers(0, 256, Wd * Hd * 8, dtype=np.uint8),
@@ -167,7 +167,7 @@ def denoise_worker(rank, world, port, result_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_strip_denoise_exchange(tmp_path, world):
     """StripDenoise (the strip-local denoise's collectives) with gloo on CPU: after the histogram
     all-reduce and the rows all-gather every rank holds the whole frame's accumulation, history
@@ -189,7 +189,7 @@ def test_strip_denoise_exchange(tmp_path, world):
         assert np.array_equal(d["hist"], np.arange(64) * sum(range(1, world + 1)))
 
 
-def exchange_worker(rank, world, port, result_dir):
+def exchange_worker(rank, world, port, result_dir, He=1080):
     import torch
     import torch.distributed as dist
 
@@ -199,7 +199,7 @@ def exchange_worker(rank, world, port, result_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        We, He = 8, 1080
+        We = 8
         sg = StripGather(We, He, world, rank, torch.device("cpu"), sets=2)
         need = [gbuffer_rows(He, world, r) for r in range(world)]
         full = {}
@@ -222,19 +222,21 @@ def exchange_worker(rank, world, port, result_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_strip_exchange_delivers_the_rows_each_rank_reads(tmp_path, world):
+@pytest.mark.parametrize("He,world", [(1080, 2), (1080, 3), (1080, 4), (1080, 8), (2160, 8)])
+def test_strip_exchange_delivers_the_rows_each_rank_reads(tmp_path, He, world):
     """StripGather.exchange (gloo, CPU): after the all-to-all every rank holds the whole frame's
     G-buffers in the rows gbuffer_rows says its strip-local denoise reads, its own blocks
     everywhere, and nothing else was written; the other G-buffer set is untouched; each rank
-    receives well under the all-gather's (N - 1) / N of the frame."""
+    receives well under the all-gather's (N - 1) / N of the frame.  (2160, 8) is config 5's split:
+    34 denoise blocks over 8 ranks."""
     import torch.multiprocessing as mp
 
     from rtx.dist import gbuffer_rows
 
     assert gbuffer_rows(1080, 8, 0) == (0, 208) and gbuffer_rows(1080, 8, 7) == (816, 1080)
-    mp.start_processes(exchange_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
-    We, He = 8, 1080
+    mp.start_processes(exchange_worker, args=(world, free_port(), str(tmp_path), He), nprocs=world,
+                       start_method="spawn")
+    We = 8
     for r in range(world):
         d = np.load(tmp_path / ("x%d.npz" % r))
         lo, hi = gbuffer_rows(He, world, r)

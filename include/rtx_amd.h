@@ -295,11 +295,21 @@ typedef struct rt_strip_exchange {
     int32_t frameNum;
     int32_t rowBegin, rowEnd;   /* this rank's rows */
     int32_t historySet;         /* history buffer (0 / 1) TemporalFilter2 wrote this frame */
+    int32_t gbufferSet;         /* G-buffer set the frame was traced into (RT_HOOK_GBUFFERS) */
+    int32_t stripLocal;         /* 1: the denoise is strip-local (rt_info.stripLocalDenoise) */
 } rt_strip_exchange;
 #define RT_HOOK_HISTOGRAM 0
 #define RT_HOOK_ROWS 1
+/* Optional third stage (rt_set_hook_stages): before the denoise, give every rank the G-buffer rows its
+ * denoise reads (rt_info.gbufferRowBegin/End of each rank; the whole frame when stripLocal is 0) from
+ * the ranks that traced them, in G-buffer set gbufferSet — what rtx/dist.py's StripGather does outside
+ * the renderer.  With it, rt_draw and rt_draw_device run a multi-GPU frame by themselves
+ * (include/rtx_dist.h implements all three stages). */
+#define RT_HOOK_GBUFFERS 2
 typedef int (*rt_collective_fn)(void* arg, int stage, void* stream, const rt_strip_exchange* x);
 int rt_set_collective_hook(rt_context* ctx, rt_collective_fn fn, void* arg);
+/* which stages the hook is called for: bit (1 << RT_HOOK_*); default HISTOGRAM | ROWS */
+int rt_set_hook_stages(rt_context* ctx, uint32_t stage_mask);
 
 /* Use caller-owned device memory (>= the buffer's size at the largest render size, i.e.
  * maxWidth x maxHeight with dynamic resolution, else rt_buffer_bytes; 16-B aligned) as one of the path-trace

@@ -176,6 +176,7 @@ struct rt_context {
     hipEvent_t ptDone[kGbSets] = {}, postDone[kGbSets] = {}, overlapEv = nullptr;
     rt_collective_fn hook = nullptr;     // multi-GPU strip-local denoise exchanges (rt_set_collective_hook)
     void* hookArg = nullptr;
+    uint32_t hookStages = (1u << RT_HOOK_HISTOGRAM) | (1u << RT_HOOK_ROWS);  // rt_set_hook_stages
     hipStream_t gatherStream = nullptr;  // optional: the caller's G-buffer gathers (rt_set_gather_stream)
     bool gatherOn = false;               // gatherStream is set (it may be the null stream)
     hipEvent_t gatherDone[kGbSets] = {};

@@ -221,7 +221,14 @@ bool strip_local_denoise(const rt_context* ctx, uint32_t& a, uint32_t& b) {
 }
 
 int run_denoise(rt_context* ctx, DenoisePostParams& p, hipStream_t s) {
-    rt_strip_exchange x{p.frameNum, (int32_t)p.rowA, (int32_t)p.rowB, p.histOutSet};
+    rt_strip_exchange x{p.frameNum, (int32_t)p.rowA, (int32_t)p.rowB, p.histOutSet, p.gbSet, p.stripLocal};
+    // the G-buffer rows this rank's denoise reads, from the ranks that traced them (opt-in stage:
+    // rtx/dist.py's FramePipeline moves them itself, rtx_dist.h's rtd_hook through this call)
+    if (ctx->stripCount > 1 && ctx->hook && (ctx->hookStages & (1u << RT_HOOK_GBUFFERS)) &&
+        ctx->hook(ctx->hookArg, RT_HOOK_GBUFFERS, (void*)s, &x) != 0) {
+        ctx->err = "collective hook failed (G-buffers)";
+        return RT_ERR_STATE;
+    }
     HIP_TRY(ctx, rtk_denoise_phase(&p, s, 0));
     // the histogram is recomputed only with the post chain on; summing a stale one again would
     // multiply it by the rank count every frame
@@ -687,6 +694,7 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.histColor = fr.histBuf[fr.histIdx];
     p.histColorOut = fr.histBuf[fr.histIdx ^ 1];
     p.histOutSet = fr.histIdx ^ 1;
+    p.gbSet = fr.gbSet;
     p.ty0 = 0;
     p.ty1 = (int)((p.H + 15) / 16);
     {  // multi-GPU strip-local denoise: only with a collective hook, and for the passes it covers
@@ -862,6 +870,12 @@ int rt_set_collective_hook(rt_context* ctx, rt_collective_fn fn, void* arg) {
     if (rc != RT_OK) return rc;
     ctx->hook = fn;
     ctx->hookArg = arg;
+    return RT_OK;
+}
+
+int rt_set_hook_stages(rt_context* ctx, uint32_t stage_mask) {
+    if (!ctx || (stage_mask & ~7u) != 0) return RT_ERR_ARG;
+    ctx->hookStages = stage_mask;
     return RT_OK;
 }
 

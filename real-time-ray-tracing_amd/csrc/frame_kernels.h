@@ -201,6 +201,7 @@ struct DenoisePostParams {
     int stripLocal;             // multi-GPU: compute only what rows [rowA, rowB) need (rtk_denoise_phase)
     uint32_t rowA, rowB;        // this context's output rows (64-row aligned; [0, H) when not strip-local)
     int histOutSet;             // which buffer of the history pair histColorOut is (the hook reports it)
+    int gbSet;                  // G-buffer set the frame was traced into (the hook reports it)
     uint32_t* rgbaTarget;       // strip-local: the caller's draw target, filled from `rgba` after the rows
     uint32_t rgbaTargetPitch;   // exchange (rgba is then the exchanged buffer); pitch in pixels
     int ty0, ty1;               // per launch (set by the launcher): tile rows of the 16x16-tile kernels

@@ -89,11 +89,12 @@ class Info(C.Structure):
 
 class StripExchange(C.Structure):
     """rt_strip_exchange: what a strip-local denoise asks the host to exchange (rt_set_collective_hook)."""
-    _fields_ = [("frameNum", C.c_int32), ("rowBegin", C.c_int32), ("rowEnd", C.c_int32), ("historySet", C.c_int32)]
+    _fields_ = [("frameNum", C.c_int32), ("rowBegin", C.c_int32), ("rowEnd", C.c_int32), ("historySet", C.c_int32),
+                ("gbufferSet", C.c_int32), ("stripLocal", C.c_int32)]
 
 
 COLLECTIVE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.POINTER(StripExchange))
-HOOK_HISTOGRAM, HOOK_ROWS = 0, 1
+HOOK_HISTOGRAM, HOOK_ROWS, HOOK_GBUFFERS = 0, 1, 2
 
 
 # every entry point declared in include/rtx_amd.h, with its ctypes signature
@@ -125,6 +126,7 @@ SIGNATURES = {
     "rt_set_gather_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "rt_bind_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]),
     "rt_set_collective_hook": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rt_set_hook_stages": (C.c_int, [C.c_void_p, C.c_uint32]),
     "rt_get_ray_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
     "rt_build_bvh": (C.c_int, [C.c_void_p]),
     "rt_trace_primary": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
@@ -338,6 +340,13 @@ class RayTracer:
         self._hook = COLLECTIVE_FN(tramp)  # keep the thunk alive as long as the context
         self._check(self.lib.rt_set_collective_hook(self.h, C.cast(self._hook, C.c_void_p), None),
                     "rt_set_collective_hook")
+
+    def set_hook_stages(self, *stages):
+        """The hook stages the renderer calls (HOOK_HISTOGRAM, HOOK_ROWS, HOOK_GBUFFERS)."""
+        mask = 0
+        for st in stages:
+            mask |= 1 << int(st)
+        self._check(self.lib.rt_set_hook_stages(self.h, mask), "rt_set_hook_stages")
 
     def bind_buffer(self, name: str, device_ptr: int, nbytes: int, gbuffer_set: int = 0):
         what = BUF[name] | (int(gbuffer_set) << 8)  # RT_BUF_SET1 / RT_BUF_SET2

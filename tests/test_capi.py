@@ -16,6 +16,17 @@ def declared_symbols():
     return sorted(set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", text)))
 
 
+def test_dist_header_symbols_exported_and_bound(rtx):
+    """include/rtx_dist.h (the C-ABI multi-GPU split) is exported by librtx.so and mirrored by rtx.cdist."""
+    from rtx.cdist import DIST_SIGNATURES, lib
+
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "rtx_dist.h")).read(), flags=re.S)
+    syms = sorted(set(re.findall(r"\b(rtd_[a-z_0-9]+)\s*\(", text)))
+    L = lib()
+    assert syms and not [s for s in syms if not hasattr(L, s)]
+    assert set(syms) == set(DIST_SIGNATURES)
+
+
 def test_header_declares_the_renderer_api():
     syms = declared_symbols()
     for s in ("rt_create", "rt_init", "rt_draw", "rt_destroy", "rt_build_bvh", "rt_trace_primary",

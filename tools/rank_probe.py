@@ -36,7 +36,8 @@ def full_frame(W, H, spp):
     return _FULL[key]
 
 
-def run(n, frames=int(os.environ.get("FRAMES", "30")), warm=3, W=1920, H=1080, spp=4, pipeline=True, denoise=True):
+def run(n, frames=int(os.environ.get("FRAMES", "30")), warm=3, W=int(os.environ.get("W", "1920")),
+        H=int(os.environ.get("H", "1080")), spp=4, pipeline=True, denoise=True):
     d = tempfile.mkdtemp()
     rt = rtx.RayTracer(W, H, rtx.write_config(os.path.join(d, "c.toml"), W, H, spp=spp,
                                               extra=strip_config(n, 0))).init()
@@ -71,9 +72,9 @@ def run(n, frames=int(os.environ.get("FRAMES", "30")), warm=3, W=1920, H=1080, s
     rt.sync()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / frames
-    if os.environ.get("STAGES"):  # serial stage times of this rank's share (LBVH, path trace, denoise)
+    if os.environ.get("STAGES"):  # serial stage times of this rank's share (primary rays, path trace, denoise)
         st = [rt.time_stage(k, 20) / 20 for k in (1, 2, 4)]
-        print("  N=%d stages serial: lbvh %.3f  path trace %.3f  denoise %.3f ms" % (n, *st), flush=True)
+        print("  N=%d stages serial: primary rays %.3f  path trace %.3f  denoise %.3f ms" % (n, *st), flush=True)
     rt.cleanup()
     return ms
 
@@ -82,6 +83,8 @@ if __name__ == "__main__":
     for n in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
         variants = ((True, True), (False, True), (True, False), (False, False))
         for pipe, dn in variants[:1] if os.environ.get("QUICK") else variants:
-            print("N=%d rank-0 strip, %s, %s: %.3f ms/frame" % (n, "pipelined" if pipe else "serial",
+            print("N=%d rank-0 strip (%sx%s), %s, %s: %.3f ms/frame" % (n, os.environ.get("W", "1920"),
+                                                                       os.environ.get("H", "1080"),
+                                                                       "pipelined" if pipe else "serial",
                                                               "with denoise" if dn else "no denoise",
                                                               run(n, pipeline=pipe, denoise=dn)), flush=True)

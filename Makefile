@@ -22,7 +22,7 @@ CPP_OBJS := $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.cpp.o,$(CPP_SRCS))
 ORC_SRCS := $(wildcard oracle/*.cpp)
 ORC_HDRS := $(wildcard oracle/*.h) $(CSRC)/rtmath.h $(CSRC)/soil_textures.h
 
-all: $(LIBDIR)/librtx.so oracle/_build/liboracle.so oracle/_build/liboracle_libm.so
+all: $(LIBDIR)/librtx.so $(LIBDIR)/librtx_rccl.so oracle/_build/liboracle.so oracle/_build/liboracle_libm.so
 
 $(OBJDIR)/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -34,6 +34,11 @@ $(OBJDIR)/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
 
 $(LIBDIR)/librtx.so: $(HIP_OBJS) $(CPP_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^ -ldl
+
+# the RCCL communicator of include/rtx_dist.h, separate so that librtx.so does not need librccl
+$(LIBDIR)/librtx_rccl.so: $(CSRC)/rccl/dist_rccl.cpp include/rtx_dist_rccl.h include/rtx_dist.h $(LIBDIR)/librtx.so
+	$(HIPCC) $(filter-out --offload-arch=gfx950,$(HIPFLAGS)) -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -x c++ -shared \
+	    -o $@ $< -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle/_build/liboracle.so: $(ORC_SRCS) $(ORC_HDRS) $(CSRC)/soil_textures.cpp
 	@mkdir -p oracle/_build

@@ -119,3 +119,11 @@ def test_camera_file_round_trip(rtx, tmp_path):
         b.load_camera(str(tmp_path / "nope.bin"))
     a.cleanup()
     b.cleanup()
+
+
+def test_rccl_communicator_library_exports():
+    """lib/librtx_rccl.so (include/rtx_dist_rccl.h) loads and exports its four entry points."""
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "rtx_dist_rccl.h")).read(), flags=re.S)
+    syms = sorted(set(re.findall(r"\b(rtd_[a-z_0-9]+)\s*\(", text)))
+    L = C.CDLL(os.path.join(ROOT, "real-time-ray-tracing_amd", "lib", "librtx_rccl.so"))
+    assert len(syms) == 4 and all(hasattr(L, s) for s in syms)

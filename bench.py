@@ -30,11 +30,17 @@ fixed as N grows ("strong" scaling).  Timing: barrier + device sync on both side
 K frames, max over ranks; value = rays of all ranks / that time.
 
 Roofline: per path-trace kernel, algorithmic bytes from the GPU's own work
-counters (node visits x 64 B, triangle tests x 48 B, texel taps, queue records) over its
-HIP-event duration inside pipelined frames (rt_time_frame_kernels).  The BVH and textures are
-cache-resident, so the memory ceiling that applies is L2 (MI355X_MICROARCH.md: 34.5 TB/s) and the
-measured HBM traffic (rocprofv3 PMC passes, profiles/r02_pmc_kernels.json) sits far below the
-algorithmic bytes; the limiter the SQ counters show is latency (SQ_WAIT_INST_ANY).
+counters (node visits x 64 B, triangle tests x 48 B, texel taps, queue records) over its average
+duration in the TIMED frames themselves: every path-trace kernel of the K timed frames is bracketed
+by HIP events on the stream it runs on (rt_frame_marks_begin / _read).  The roofline's top-level
+kernel is the longest kernel of the frame's critical (context) stream; the camera kernel runs on
+a side stream overlapped with the previous frame's chain (its duration there measures the overlap)
+and is listed with the others.  The process running the timed frames launches nothing else of the
+frame's path-trace kernels (the side measurements run in a child process), so a rocprofv3
+--kernel-trace --stats of this command gives, in this process's stats file, averages over exactly
+the warm-up + timed + detail frames.  The BVH and textures are cache-resident, so the memory
+ceiling that applies is L2 (MI355X_MICROARCH.md: 34.5 TB/s) and the measured HBM traffic (rocprofv3
+PMC passes) sits far below the algorithmic bytes; the limiter the SQ counters show is latency.
 """
 import argparse
 import json
@@ -54,7 +60,7 @@ for p in (ROOT, PKG):
 HBM_PEAK_GBS = 8000.0   # /opt/skills/guides/MI355X_MICROARCH.md (spec peak)
 L2_PEAK_GBS = 34500.0   # MI355X_MICROARCH.md, L2 (per XCD) section: aggregate L2 bandwidth
 DELTA_MS = 16.667       # fixed AutoExposure step (SURVEY §8d determinism settings)
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_kernels.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_kernels.json")
 TERRAIN_CAM = dict(pos=(8.0, 15.0, -6.0), yaw=0.0, pitch=-0.7)  # ~50 % primary hits (tests' camera)
 
 # algorithmic bytes: per node visit the 64-B node record, per triangle test the
@@ -79,6 +85,11 @@ def parse():
                     help="gloo: rehearse the multi-rank path with ranks sharing a GPU (not a measurement)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="serial frames (no post stream): denoise of frame f does not overlap the trace of f+1")
+    ap.add_argument("--no-marks", action="store_true",
+                    help="no HIP events in the timed frames (A/B of their cost; the roofline then has no kernel ms)")
+    ap.add_argument("--extras-child", action="store_true", help=argparse.SUPPRESS)  # side legs, own process
+    ap.add_argument("--check-file", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--check-frames", type=int, default=0, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -213,7 +224,7 @@ def kernel_roofline(q, W, rows, S, kernels_ms, pmc, workload_matches):
         "k_pt_resume<4>": (QREC_B + HIT_B) * n4,
         "k_pt_resolve": 16 * S * surf + 8 * surf,
     }
-    work = {"k_pt_camera": {"node_visits": vc, "tri_tests": tc, "samples": px * S},
+    work = {"k_pt_camera": {"node_visits": vc, "tri_tests": tc, "samples": px * S, "culled": int(q[22])},
             "k_pt_shade0": {"diffuse_events": ds, "surface_pixels": surf, "node_visits": vs, "tri_tests": ts},
             "k_trace_queue<3>": {"rays": n3, "node_visits": v3, "tri_tests": t3, "max_iterations": int(q[8])},
             "k_pt_resume<3>": {"rays": n3, "diffuse_events": d3},
@@ -231,6 +242,20 @@ def kernel_roofline(q, W, rows, S, kernels_ms, pmc, workload_matches):
                     e[f] = pk[f]
         out[k] = e
     return out
+
+
+def iteration_histogram(rt, frame):
+    """TraverseBvh iterations of the frame's camera rays (rt_trace_primary detail: 1 spp, frame
+    index `frame`): distribution, mean, max, and how many rays the scene cull settled (1 iteration)."""
+    rt.trace_primary(frame, detail=True)
+    rt.sync()
+    hs = rt.download("HIT_STATS", np.uint32).reshape(-1, 4)
+    it = hs[:, 3].astype(np.int64)
+    edges = [1, 2, 8, 16, 32, 48, 64, 96, 128, 192, 256, 512, 1025]
+    h, _ = np.histogram(it, bins=edges)
+    return {"rays": int(it.size), "mean": round(float(it.mean()), 2), "p99": int(np.percentile(it, 99)),
+            "max": int(it.max()), "dropped_pushes": int(hs[:, 2].sum()),
+            "hist": {("%d" % a if b - a == 1 else "%d-%d" % (a, b - 1)): int(c) for a, b, c in zip(edges, edges[1:], h)}}
 
 
 def time_draw(rtx, torch, dev, W, H, S, tmp, frames=20):
@@ -257,8 +282,143 @@ def time_draw(rtx, torch, dev, W, H, S, tmp, frames=20):
     return out
 
 
+def self_check(rtx, W, H, S, tmp, last, final):
+    """Serial re-render of frames 1..last in a fresh single-GPU context, compared with the timed
+    sequence's last frame (RGBA8, final HDR, exposure state)."""
+    ref = rtx.RayTracer(W, H, rtx.write_config(os.path.join(tmp, "check.toml"), W, H, dynamic=False, spp=S)).init()
+    ref.set_delta_time(DELTA_MS)
+    ref.set_stream(None)
+    for f in range(1, last + 1):
+        ref.build_bvh()
+        ref.path_trace(f)
+        ref.denoise_post(f)
+    ref.sync()
+    same = {"rgba8": bool(np.array_equal(ref.download("RGBA8", np.uint8), final["rgba"])),
+            "hdr": bool(np.array_equal(ref.get_buffer("RENDER_COLOR"), final["color"])),
+            "exposure": bool(np.array_equal(ref.download("EXPOSURE", np.uint8), final["exposure"]))}
+    ref.cleanup()
+    return dict(same, frames=last, against="serial single-GPU re-render of frames 1..%d" % last, ok=all(same.values()))
+
+
+def extras_child(args):
+    """The side measurements, in a process of their own (so that the timed process's rocprofv3 stats
+    hold only the timed workload): traversal under load (the terrain camera, pipelined, with its own
+    kernel split, work counters and camera-ray iteration histogram), serial stage and kernel times,
+    rt_draw_device sync / async, the 1M-triangle LBVH rebuild (config 4), and the self-check."""
+    import torch
+
+    import rtx
+    from rtx.frames import FramePipeline
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    W, H, S = args.width, args.height, args.spp
+    tmp = tempfile.mkdtemp(prefix="rtxextras")
+    out = {}
+    cfg = rtx.write_config(os.path.join(tmp, "x.toml"), W, H, dynamic=False, chunk_dim=1, spp=S)
+    rt = rtx.RayTracer(W, H, cfg).init()
+    rt.set_delta_time(DELTA_MS)
+    out["camera_iterations_default_view"] = iteration_histogram(rt, 4)
+    fp = FramePipeline(rt, dev, pipelined=True)
+    cam = rt.camera
+    cam.pos[:] = TERRAIN_CAM["pos"]
+    cam.yaw, cam.pitch = TERRAIN_CAM["yaw"], TERRAIN_CAM["pitch"]
+    rt.camera = cam
+    for f in range(1, 4):
+        fp.frame(f)
+    fp.finish()
+    rt.ray_count(reset=True)
+    nt = 20
+    rt.frame_marks_begin(nt)
+    torch.cuda.synchronize()
+    ta = time.perf_counter()
+    for k in range(nt):
+        fp.frame(4 + k)
+    fp.finish()
+    torch.cuda.synchronize()
+    tdt = time.perf_counter() - ta
+    kms, _ = rt.frame_marks_read()
+    trays = rt.ray_count()
+    f = 4 + nt
+    rt.path_trace(f, detail=True)
+    q = rt.download("PT_QUEUE", np.uint32).copy()
+    st = rt.download("PT_STATS", np.uint32).reshape(-1, 4).astype(np.uint64)
+    rays_detail = int(st[:, 0].sum())
+    per = kernel_roofline(q, W, H, S, kms, None, False)
+    culled = int(q[22])
+    out["terrain_camera"] = {
+        "camera": TERRAIN_CAM, "frames": nt, "ms_per_frame": round(tdt * 1e3 / nt, 4),
+        "mray_s": round(trays / tdt / 1e6, 2), "rays_per_frame": int(trays // nt),
+        "mray_s_traversed": round(trays * (1.0 - culled / max(rays_detail, 1)) / tdt / 1e6, 2),
+        "culled_camera_rays_per_frame": culled,
+        "roofline": {"kernel": max((k for k in per if k != "k_pt_camera"), key=lambda k: per[k]["ms"]),
+                     "kernels": per, "peak": L2_PEAK_GBS, "unit": "GB/s",
+                     "timing": "HIP events around each kernel of the %d timed terrain frames" % nt},
+        "camera_iterations": iteration_histogram(rt, f + 1)}
+    rt.cleanup()
+    # serial stages and kernels of the default view (rt_draw's mode: trace<3> .. resume<4> fused)
+    sr = rtx.RayTracer(W, H, rtx.write_config(os.path.join(tmp, "s.toml"), W, H, dynamic=False, spp=S)).init()
+    sr.set_delta_time(DELTA_MS)
+    for f in range(1, 4):
+        sr.build_bvh()
+        sr.path_trace(f)
+        sr.denoise_post(f)
+    sr.sync()
+    build_ms = sr.time_stage(0, 50) / 50
+    out["lbvh_build_ms"] = round(build_ms, 5)
+    out["lbvh_build_tris"] = int(sr.info().triCount)
+    out["stage_ms_serial"] = {"lbvh_build": round(build_ms, 5), "path_trace": round(sr.time_stage(2, 20) / 20, 5),
+                              "denoise_post": round(sr.time_stage(4, 20) / 20, 5),
+                              "primary_rays_1spp": round(sr.time_stage(1, 20) / 20, 5)}
+    out["primary_mray_s"] = round(W * H / (out["stage_ms_serial"]["primary_rays_1spp"] * 1e-3) / 1e6, 2)
+    sk = sr.time_path_trace_kernels(20)
+    names = list(sk)
+    if all(sk[k] < 0.02 for k in names[3:6]):  # the fused chain k_pt_chain ran in kernel slot 2
+        sk = {("k_pt_chain" if i == 2 else k): v for i, (k, v) in enumerate(sk.items()) if not 3 <= i <= 5}
+    out["serial_kernels_ms"] = {k: round(v, 5) for k, v in sk.items()}
+    out["serial_kernels_ms"]["sum"] = round(sum(sk.values()), 5)
+    sr.cleanup()
+    # the reference host's entry point, RayTracer::draw(SurfObj*) (kernel.cu:259): rt_draw_device into
+    # a caller-owned device RGBA8 target, synchronous and asynchronous (RT_DRAW_ASYNC)
+    out["draw_device"] = time_draw(rtx, torch, dev, W, H, S, tmp)
+    # BASELINE config 4: per-frame rebuild of the ~1M-triangle variant (chunkDim 4)
+    r4 = rtx.RayTracer(256, 144, rtx.write_config(os.path.join(tmp, "c4.toml"), 256, 144, chunk_dim=4)).init()
+    r4.build_bvh()
+    r4.sync()
+    ms4 = r4.time_stage(0, 30) / 30
+    n4 = r4.info().triCount
+    r4.cleanup()
+    a4 = 348 * n4 / (ms4 * 1e-3) / 1e9
+    out["lbvh_build_1m"] = {"tris": int(n4), "ms": round(ms4, 5),
+                            "roofline": {"bound": "hbm", "achieved": round(a4, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                         "frac": round(a4 / HBM_PEAK_GBS, 5), "traffic": None, "bytes_per_tri": 348}}
+    if args.check_file:
+        fin = np.load(args.check_file)
+        out["self_check"] = self_check(rtx, W, H, S, tmp, args.check_frames,
+                                       {k: fin[k] for k in ("rgba", "color", "exposure")})
+    print("EXTRAS " + json.dumps(out), flush=True)
+
+
+def run_extras(args, check_file, check_frames):
+    """extras_child in a fresh process (started before or after this one used the GPU: a child, not an
+    exec); returns its JSON, or an error record."""
+    import subprocess
+
+    cmd = [sys.executable, os.path.abspath(__file__), "--extras-child", "--width", str(args.width), "--height",
+           str(args.height), "--spp", str(args.spp)]
+    if check_file:
+        cmd += ["--check-file", check_file, "--check-frames", str(check_frames)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    for line in r.stdout.splitlines():
+        if line.startswith("EXTRAS "):
+            return json.loads(line[7:])
+    return {"extras_error": "rc %d: %s" % (r.returncode, r.stderr[-2000:])}
+
+
 def main():
     args = parse()
+    if args.extras_child:
+        return extras_child(args)
     import torch
     import torch.distributed as dist
 
@@ -294,6 +454,9 @@ def main():
     fp.finish()
     rt.ray_count(reset=True)
 
+    # ---- the timed region: K frames, each path-trace kernel bracketed by HIP events on its stream
+    if not args.no_marks:
+        rt.frame_marks_begin(args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -306,6 +469,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = t1 - t0
+    kernels_ms, marked = rt.frame_marks_read() if not args.no_marks else (None, 0)
     rays = rt.ray_count()
     last = args.warmup + args.steps
     final = None
@@ -350,12 +514,15 @@ def main():
         "rays_per_frame": int(rays // args.steps),
     }
 
-    # ---- per-kernel roofline of the path-trace stage over this rank's strip: work counters of one
-    # detail launch, kernel durations inside pipelined frames (HIP events on each kernel's stream)
+    # ---- per-kernel roofline over this rank's strip: work counters of one detail launch (after the
+    # timed frames), kernel durations from the timed frames' events
     rt.path_trace(last + 1, detail=True)
     st = rt.download("PT_STATS", np.uint32).reshape(-1, 4).astype(np.uint64)  # zero outside this rank's rows
     n_rays, visits, tests, diffuse = (int(st[:, k].sum()) for k in range(4))
     counters = rt.download("PT_QUEUE", np.uint32).copy()  # per-kernel work of this detail launch
+    culled = int(counters[22])
+    result["mray_s_traversed"] = round(value * (1.0 - culled / max(n_rays, 1)), 3)
+    result["rays_traversed_fraction"] = round(1.0 - culled / max(n_rays, 1), 4)
     pmc = pmc_kernels()
     matches = pmc is not None and pmc.get("workload_key") == "%dx%dx%d" % (W, H, S) and world == 1
     if world > 1:  # what each rank receives per frame over the collectives (the G-buffer rows its
@@ -364,10 +531,13 @@ def main():
         r_ = fp.denoise.bytes_per_frame() if fp.denoise else 0
         result["comm_bytes_per_rank_per_frame"] = {"gbuffer_rows": int(g), "denoise_rows": int(r_),
                                                    "gbuffer_allgather_would_be": int(fp.gather.bytes_per_frame())}
-    fk_iters = 20
-    kernels_ms = rt.time_frame_kernels(last + 2, fk_iters)
+    if kernels_ms is None:  # --no-marks: the split from separate pipelined frames after the timed ones
+        kernels_ms = rt.time_frame_kernels(last + 2, 20)
     per = kernel_roofline(counters, W, rows, S, kernels_ms, pmc, matches)
-    dom = max(per, key=lambda k: per[k]["ms"])
+    # the longest kernel of the frame's critical (context) stream; pipelined, the camera kernel runs
+    # on the side stream beside the previous frame's chain (listed in kernels)
+    crit = [k for k in per if not (pipeline and k == "k_pt_camera")]
+    dom = max(crit, key=lambda k: per[k]["ms"])
     d = per[dom]
     stage_bytes = sum(e["algorithmic_bytes"] for e in per.values())
     stage_ms = sum(e["ms"] for e in per.values())
@@ -377,112 +547,38 @@ def main():
         "achieved": d["achieved_GBs"], "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": d["frac_l2"],
         "traffic": d.get("hbm_bytes"),
         "traffic_source": os.path.relpath(PMC_FILE, ROOT) if matches else None,
-        "note": "BVH nodes, triangles and textures (~34 MB) stay in L2 / Infinity Cache: the applicable memory "
-                "ceiling is L2 bandwidth, HBM traffic is far below the algorithmic bytes, and the kernels wait on "
-                "dependent node loads (latency), not on bandwidth",
+        "note": "kernel = the longest kernel on the frame's critical (context) stream; BVH nodes, triangles and "
+                "textures (~34 MB) stay in L2 / Infinity Cache: the applicable memory ceiling is L2 bandwidth, HBM "
+                "traffic is far below the algorithmic bytes, and the kernels wait on dependent node loads "
+                "(latency), not on bandwidth",
         "kernels": per,
         "stage": {"kernels": " -> ".join(per), "algorithmic_bytes": stage_bytes, "sum_kernel_ms": round(stage_ms, 5),
                   "achieved_GBs": round(stage_bytes / (stage_ms * 1e-3) / 1e9, 1),
                   "frac_l2": round(stage_bytes / (stage_ms * 1e-3) / 1e9 / L2_PEAK_GBS, 4),
                   "rays": n_rays, "node_visits": visits, "tri_tests": tests, "diffuse_events": diffuse,
                   "hbm_bytes": pmc.get("stage_hbm_bytes") if matches else None},
-        "timing": "kernel ms: HIP events around each kernel on its own stream over %d pipelined frames "
-                  "(rt_time_frame_kernels); rocprofv3 --stats of the bench: profiles/r02_kernel_stats.csv" % fk_iters,
+        "timing": "kernel ms: HIP events right before / after each kernel on the stream it runs on, in every one "
+                  "of the %d timed frames (rt_frame_marks); rocprofv3 --stats of this command: "
+                  "profiles/r03_kernel_stats.csv (this process's launches: warm-up + timed + 1 detail frame)" % marked,
     }
-
-    if not args.no_extras:
-        # traversal under load: the tests' terrain camera (~50 % primary hits), same pipeline
-        cam = rt.camera
-        cam0 = rtx.Camera()
-        cam0.pos[:], cam0.yaw, cam0.pitch = cam.pos[:], cam.yaw, cam.pitch
-        cam0.focal, cam0.aperture, cam0.fovX = cam.focal, cam.aperture, cam.fovX
-        cam.pos[:] = TERRAIN_CAM["pos"]
-        cam.yaw, cam.pitch = TERRAIN_CAM["yaw"], TERRAIN_CAM["pitch"]
-        rt.camera = cam
-        f0 = last + 2 + fk_iters
-        for k in range(3):
-            fp.frame(f0 + k)
-        fp.finish()
-        rt.ray_count(reset=True)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        ta = time.perf_counter()
-        nt = 20
-        for k in range(nt):
-            fp.frame(f0 + 3 + k)
-        fp.finish()
-        torch.cuda.synchronize()
-        tdt = time.perf_counter() - ta
-        trays = rt.ray_count()
-        tk = rt.time_frame_kernels(f0 + 3 + nt, 10)
-        result["terrain_camera"] = {"camera": TERRAIN_CAM, "frames": nt, "ms_per_frame": round(tdt * 1e3 / nt, 4),
-                                    "mray_s": round(trays / tdt / 1e6, 2), "rays_per_frame": int(trays // nt),
-                                    "kernels_ms": {k: round(v, 5) for k, v in tk.items()}}
-        rt.camera = cam0
-        build_ms = rt.time_stage(0, 50) / 50
-        info = rt.info()
-        result["lbvh_build_ms"] = round(build_ms, 5)
-        result["lbvh_build_tris"] = int(info.triCount)
-        result["stage_ms_serial"] = {"lbvh_build": round(build_ms, 5),
-                                     "path_trace": round(rt.time_stage(2, 20) / 20, 5),
-                                     "denoise_post": round(rt.time_stage(4, 20) / 20, 5),
-                                     "primary_rays_1spp": round(rt.time_stage(1, 20) / 20, 5)}
-        result["primary_mray_s"] = round(W * rows / (result["stage_ms_serial"]["primary_rays_1spp"] * 1e-3) / 1e6, 2)
-        # serial frames (no post stream: rt_draw's mode) run trace<3> .. resume<4> as one fused
-        # launch, k_pt_chain, in kernel slot 2 (slots 3-5 stay empty)
-        sk = rt.time_path_trace_kernels(20)
-        names = list(sk)
-        if all(sk[k] < 0.02 for k in names[3:6]):
-            sk = {("k_pt_chain" if i == 2 else k): v for i, (k, v) in enumerate(sk.items()) if not 3 <= i <= 5}
-        result["serial_kernels_ms"] = {k: round(v, 5) for k, v in sk.items()}
-        result["serial_kernels_ms"]["sum"] = round(sum(sk.values()), 5)
     rt.cleanup()
 
-    if final is not None:
-        # serial re-render of the timed sequence in a fresh single-GPU context, outside the timed region
-        ref = rtx.RayTracer(W, H, rtx.write_config(os.path.join(tmp, "check.toml"), W, H, dynamic=False, spp=S)).init()
-        ref.set_delta_time(DELTA_MS)
-        ref.set_stream(None)
-        for f in range(1, last + 1):
-            ref.build_bvh()
-            ref.path_trace(f)
-            ref.denoise_post(f)
-        ref.sync()
-        same = {"rgba8": bool(np.array_equal(ref.download("RGBA8", np.uint8), final["rgba"])),
-                "hdr": bool(np.array_equal(ref.get_buffer("RENDER_COLOR"), final["color"])),
-                "exposure": bool(np.array_equal(ref.download("EXPOSURE", np.uint8), final["exposure"]))}
-        ref.cleanup()
-        result["self_check"] = dict(same, frames=last, against="serial single-GPU re-render of frames 1..%d" % last,
-                                    ok=all(same.values()))
-
-    if not args.no_extras and rank == 0 and world == 1:
-        # the reference host's entry point, RayTracer::draw(SurfObj*) (kernel.cu:259): rt_draw_device
-        # into a caller-owned device RGBA8 target, synchronous (serial frames, fused bounce chain)
-        # and asynchronous (RT_DRAW_ASYNC: the frame pipeline), in a fresh context
-        result["draw_device"] = time_draw(rtx, torch, dev, W, H, S, tmp)
-
-    if not args.no_extras and rank == 0:
-        # BASELINE config 4: per-frame rebuild of the ~1M-triangle variant (chunkDim 4)
-        cfg4 = rtx.write_config(os.path.join(tmp, "c4.toml"), 256, 144, chunk_dim=4)
-        r4 = rtx.RayTracer(256, 144, cfg4).init()
-        r4.build_bvh()
-        r4.sync()
-        ms4 = r4.time_stage(0, 30) / 30
-        n4 = r4.info().triCount
-        r4.cleanup()
-        a4 = 348 * n4 / (ms4 * 1e-3) / 1e9
-        result["lbvh_build_1m"] = {"tris": int(n4), "ms": round(ms4, 5),
-                                   "roofline": {"bound": "hbm", "achieved": round(a4, 2), "peak": HBM_PEAK_GBS,
-                                                "unit": "GB/s", "frac": round(a4 / HBM_PEAK_GBS, 5),
-                                                "traffic": None, "bytes_per_tri": 348}}
+    if rank == 0 and world == 1 and not args.no_extras:
+        cf = None
+        if final is not None:
+            cf = os.path.join(tmp, "final.npz")
+            np.savez(cf, **final)
+        result.update(run_extras(args, cf, last))
+    elif final is not None:
+        result["self_check"] = self_check(rtx, W, H, S, tmp, last, final)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(W, H, S)
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
         dist.destroy_process_group()
-    if rank == 0 and final is not None and not result["self_check"]["ok"]:
+    sc = result.get("self_check")
+    if rank == 0 and sc is not None and not sc["ok"]:
         sys.exit("bench self-check failed: the timed frames differ from a serial re-render")
 
 

@@ -341,6 +341,13 @@ int rt_time_path_trace_kernels(rt_context* ctx, int iters, float* kernel_ms, int
  * work.  Waits for the frames.  Measurement aid for bench.py's per-kernel roofline. */
 int rt_time_frame_kernels(rt_context* ctx, int first_frame, int iters, float* kernel_ms, int n);
 
+/* The same split recorded inside the caller's own frames: the next `frames` path traces bracket
+ * each of their kernels with HIP events on the stream it runs on (two events per kernel, no
+ * synchronisation); rt_frame_marks_read waits, writes the per-kernel average milliseconds over the
+ * frames recorded (n >= 7, order as above) and stops recording.  bench.py's timed region uses it. */
+int rt_frame_marks_begin(rt_context* ctx, int frames);
+int rt_frame_marks_read(rt_context* ctx, float* kernel_ms, int n, int* frames_recorded);
+
 /* Copies device arrays to host (debug dumps of bvh.cu:15-96, traversal outputs). */
 enum rt_array_name {
     RT_ARR_VERTICES = 0,         /* float[nv][3] */
@@ -382,7 +389,8 @@ enum rt_array_name {
                                     also: node visits / triangle tests of [12,13] the camera
                                     kernel, [14,15] the shade kernel (inline glossy traces),
                                     [16,17] the step-3 and [18,19] the step-4 queue tracers,
-                                    diffuse events of [20] the shade and [21] the resume<3> kernel */
+                                    diffuse events of [20] the shade and [21] the resume<3> kernel,
+                                    [22] camera rays settled by the scene cull (no traversal) */
     RT_ARR_PT_Q3_ORIGINS = 33,   /* float4[cap] step-3 queue rays of the last launch: origin xyz, pixel bits */
     RT_ARR_PT_Q3_DIRS = 34,      /* float4[cap] direction xyz, flags bits ([0] of RT_ARR_PT_QUEUE are valid) */
     RT_ARR_PT_Q4_ORIGINS = 35,   /* float4[cap] step-4 queue, same layout ([1] valid) */

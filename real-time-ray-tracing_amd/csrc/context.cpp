@@ -452,6 +452,8 @@ void rt_destroy(rt_context* ctx) {
     if (ctx->sideStream) (void)hipStreamDestroy(ctx->sideStream);
     if (ctx->ownPostStream) (void)hipStreamDestroy(ctx->ownPostStream);
     for (void* p : ctx->allocations) (void)hipFree(p);
+    for (hipEvent_t e : ctx->markRing)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->ownStream) {
@@ -702,6 +704,40 @@ int rt_time_path_trace_kernels(rt_context* ctx, int iters, float* kernel_ms, int
 
 int rt_time_frame_kernels(rt_context* ctx, int first_frame, int iters, float* kernel_ms, int n) {
     return time_kernels(ctx, first_frame, iters, kernel_ms, n, true);
+}
+
+int rt_frame_marks_begin(rt_context* ctx, int frames) {
+    if (!ctx || frames < 0 || frames > 100000) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_frame_marks_begin before rt_init"; return RT_ERR_STATE; }
+    if (int rc = sync_streams(ctx)) return rc;  // the events of earlier frames are complete
+    const size_t need = (size_t)frames * 2 * kPtKernels;
+    while (ctx->markRing.size() < need) {
+        hipEvent_t e = nullptr;
+        HIP_TRY(ctx, hipEventCreate(&e));
+        ctx->markRing.push_back(e);
+    }
+    ctx->markFrames = frames;
+    ctx->markNext = 0;
+    return RT_OK;
+}
+
+int rt_frame_marks_read(rt_context* ctx, float* kernel_ms, int n, int* frames_recorded) {
+    if (!ctx || !kernel_ms || n < kPtKernels) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_frame_marks_read before rt_init"; return RT_ERR_STATE; }
+    if (int rc = sync_streams(ctx)) return rc;
+    const int frames = ctx->markNext;
+    for (int k = 0; k < kPtKernels; ++k) kernel_ms[k] = 0.0f;
+    for (int i = 0; i < frames; ++i)
+        for (int k = 0; k < kPtKernels; ++k) {
+            const hipEvent_t* m = ctx->markRing.data() + (size_t)i * 2 * kPtKernels;
+            float ms = 0.0f;
+            HIP_TRY(ctx, hipEventElapsedTime(&ms, m[2 * k], m[2 * k + 1]));
+            kernel_ms[k] += ms / (float)frames;
+        }
+    if (frames_recorded) *frames_recorded = frames;
+    ctx->markFrames = 0;
+    ctx->markNext = 0;
+    return RT_OK;
 }
 
 size_t rt_array_bytes(const rt_context* ctx, int what) {

@@ -198,6 +198,9 @@ struct rt_context {
     bool cameraGated = false;
     DenoisePostParams postParams{};
     hipEvent_t* ptMarks = nullptr;  // set only inside rt_time_path_trace_kernels
+    // rt_frame_marks_begin: events around every path-trace kernel of the next markFrames path traces
+    std::vector<hipEvent_t> markRing;
+    int markFrames = 0, markNext = 0;
     float* dVerts = nullptr;
     float* dNormals = nullptr;
     uint32_t* dIdx = nullptr;

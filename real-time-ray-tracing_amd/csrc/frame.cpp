@@ -613,6 +613,15 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     } else if ((rc = wait_bvh(ctx)) != RT_OK) {
         return rc;
     }
+    // rt_frame_marks_begin: this path trace's kernels are bracketed by events (caller's timed frames)
+    hipEvent_t* const savedMarks = ctx->ptMarks;
+    if (!ctx->ptMarks && ctx->markNext < ctx->markFrames)
+        ctx->ptMarks = ctx->markRing.data() + (size_t)(ctx->markNext++) * 2 * kPtKernels;
+    struct MarksReset {  // every return path leaves ptMarks as it found it
+        rt_context* c;
+        hipEvent_t* m;
+        ~MarksReset() { c->ptMarks = m; }
+    } marksReset{ctx, savedMarks};
     HIP_TRY(ctx, rtk_launch_pt_camera(&p, cs, ctx->ptMarks));
     if (side) {
         HIP_TRY(ctx, hipEventRecord(ctx->camDone[g], cs));

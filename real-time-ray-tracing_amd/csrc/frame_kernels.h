@@ -77,12 +77,12 @@ struct PtQueue {
 // [12..21]: per-kernel traversal / shading work of detail launches (statsOut set), for the
 // per-kernel roofline (bench.py): node visits and triangle tests of the camera kernel, the
 // shade kernel's inline (glossy) traces and the two queue tracers; diffuse events of the shade
-// and resume<3> kernels
+// and resume<3> kernels; [22] camera rays the scene cull settled without a traversal
 enum PtCounter : int { kCntQ3 = 0, kCntQ4 = 1, kCntFetch3 = 2, kCntFetch4 = 3, kCntPending = 4, kCntResume3 = 5,
                        kCntResume4 = 6, kCntResolve = 7, kCntMaxIter3 = 8, kCntMaxIter4 = 9, kCntError = 10,
                        kCntSurface = 11, kCntVisCam = 12, kCntTstCam = 13, kCntVisShade = 14, kCntTstShade = 15,
                        kCntVisQ3 = 16, kCntTstQ3 = 17, kCntVisQ4 = 18, kCntTstQ4 = 19, kCntDiffShade = 20,
-                       kCntDiffRes3 = 21, kCntSlots = 22 };
+                       kCntDiffRes3 = 21, kCntCulledCam = 22, kCntSlots = 23 };
 constexpr int kWsCounterWords = 64 + 2 * 8 * 16;  // counters | fetch, zeroed together
 
 struct PtWorkspace {

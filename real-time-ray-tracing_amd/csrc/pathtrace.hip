@@ -455,7 +455,7 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
     bool anyHit = false;
     float4 rec = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float recErr = 0.0f;
-    uint32_t rays = 0, camV = 0, camT = 0;
+    uint32_t rays = 0, camV = 0, camT = 0, camCull = 0;
 #pragma unroll 1
     for (int r = 0; r < rounds; ++r) {  // uniform trip count: every thread reaches the barriers
         const int s = r * nSW + sw;
@@ -469,6 +469,7 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
             TravState st;
             if (root_surely_missed(sc, org, dir)) {  // most sky rays: settled without the ray-box helper
                 trav_root_miss(st);
+                ++camCull;
             } else {
                 TravRay tr;
                 trav_setup(sc, org, dir, tr);
@@ -538,6 +539,7 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
     if (P.statsOut) {
         wave_add(camV, &P.ws.counters[kCntVisCam]);
         wave_add(camT, &P.ws.counters[kCntTstCam]);
+        wave_add(camCull, &P.ws.counters[kCntCulledCam]);
     }
     const uint32_t slot = wave_append(sw == 0 && surface, &P.ws.counters[kCntSurface]);
     if (sw == 0 && active) {

@@ -5,7 +5,10 @@
 
 namespace rtd {
 
-constexpr int kRefillMin = 16;  // idle lanes that trigger a refill
+#ifndef RTX_REFILL_MIN
+#define RTX_REFILL_MIN 16
+#endif
+constexpr int kRefillMin = RTX_REFILL_MIN;  // idle lanes that trigger a refill (ablation: -DRTX_REFILL_MIN)
 constexpr int kParts = 8;       // fetch counters (one per XCD by blockIdx % 8): spreads the atomics
 
 // Work distribution.  Wave g first takes items [64 g, 64 g + 64) with no atomic: a short queue

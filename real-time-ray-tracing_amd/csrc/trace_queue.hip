@@ -25,6 +25,10 @@ namespace {
 
 constexpr int kTraceBlock = 256;
 constexpr uint32_t kTrace3Short = 1u << 20;  // queue-3 length below which trace3ShortBlocks apply
+#ifndef RTX_LEAF_BATCH
+#define RTX_LEAF_BATCH 1
+#endif
+constexpr bool kLeafBatch = RTX_LEAF_BATCH != 0;  // ablation: -DRTX_LEAF_BATCH=0
 
 template <int kStep>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) {
@@ -86,12 +90,12 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
         // leaf batching (a wave in the tail has few lanes left, and its iteration latency is the
         // kernel's tail).  Each ray's steps are unchanged.
         const bool tail = f.resLo == f.resHi && f.drained == (1u << kParts) - 1u;
-        if (tail ? active : trav_lane_steps(active, s)) {
+        if (tail || !kLeafBatch ? active : trav_lane_steps(active, s)) {
             bool done = false;
             do {  // two steps per trip: the loop's refill / exec-mask bookkeeping once per two
                 done = trav_step(sc, r, s, stk + tid, kTraceBlock) || s.iters >= 1024u ||
                        (occlusion && s.hitIdx >= 0);
-                if (!done && (tail || trav_lane_steps(true, s)))
+                if (!done && (tail || !kLeafBatch || trav_lane_steps(true, s)))
                     done = trav_step(sc, r, s, stk + tid, kTraceBlock) || s.iters >= 1024u ||
                            (occlusion && s.hitIdx >= 0);
             } while (tail && !done);

@@ -318,6 +318,7 @@ def extras_child(args):
     cfg = rtx.write_config(os.path.join(tmp, "x.toml"), W, H, dynamic=False, chunk_dim=1, spp=S)
     rt = rtx.RayTracer(W, H, cfg).init()
     rt.set_delta_time(DELTA_MS)
+    rt.build_bvh()
     out["camera_iterations_default_view"] = iteration_histogram(rt, 4)
     fp = FramePipeline(rt, dev, pipelined=True)
     cam = rt.camera
@@ -449,14 +450,30 @@ def main():
     pipeline = not args.no_pipeline
     fp = FramePipeline(rt, dev, pipelined=pipeline, world=world, rank=rank, backend=args.dist_backend)
 
-    for k in range(args.warmup):
-        fp.frame(1 + k)
-    fp.finish()
+    # warm-up; frames 2..W with every path-trace kernel bracketed by HIP events, which picks the
+    # roofline's kernel: the longest on the frame's critical (context) stream (pipelined, the camera
+    # kernel runs on the side stream beside the previous frame's chain)
+    crit = [k for k in rtx.RayTracer.PT_KERNELS if not (pipeline and k == "k_pt_camera")]
+    dom = "k_trace_queue<3>"
+    if args.warmup >= 2:
+        fp.frame(1)
+        fp.finish()
+        rt.frame_marks_begin(args.warmup - 1)
+        for k in range(1, args.warmup):
+            fp.frame(1 + k)
+        fp.finish()
+        warm_ms, _ = rt.frame_marks_read()
+        dom = max(crit, key=lambda k: warm_ms[k])
+    else:
+        for k in range(args.warmup):
+            fp.frame(1 + k)
+        fp.finish()
     rt.ray_count(reset=True)
 
-    # ---- the timed region: K frames, each path-trace kernel bracketed by HIP events on its stream
+    # ---- the timed region: K frames; that kernel is bracketed by HIP events on its stream in every
+    # one of them (two events per frame: bracketing all seven kernels measured +2.4 % per frame)
     if not args.no_marks:
-        rt.frame_marks_begin(args.steps)
+        rt.frame_marks_begin(args.steps, [dom])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -531,13 +548,13 @@ def main():
         r_ = fp.denoise.bytes_per_frame() if fp.denoise else 0
         result["comm_bytes_per_rank_per_frame"] = {"gbuffer_rows": int(g), "denoise_rows": int(r_),
                                                    "gbuffer_allgather_would_be": int(fp.gather.bytes_per_frame())}
-    if kernels_ms is None:  # --no-marks: the split from separate pipelined frames after the timed ones
-        kernels_ms = rt.time_frame_kernels(last + 2, 20)
-    per = kernel_roofline(counters, W, rows, S, kernels_ms, pmc, matches)
-    # the longest kernel of the frame's critical (context) stream; pipelined, the camera kernel runs
-    # on the side stream beside the previous frame's chain (listed in kernels)
-    crit = [k for k in per if not (pipeline and k == "k_pt_camera")]
-    dom = max(crit, key=lambda k: per[k]["ms"])
+    # the other kernels: the same split over 20 pipelined frames right after (every kernel marked)
+    split = rt.time_frame_kernels(last + 2, 20)
+    split_dom = split[dom]
+    timed_dom = (kernels_ms or {}).get(dom)
+    if timed_dom is not None:
+        split = dict(split, **{dom: timed_dom})
+    per = kernel_roofline(counters, W, rows, S, split, pmc, matches)
     d = per[dom]
     stage_bytes = sum(e["algorithmic_bytes"] for e in per.values())
     stage_ms = sum(e["ms"] for e in per.values())
@@ -557,9 +574,13 @@ def main():
                   "frac_l2": round(stage_bytes / (stage_ms * 1e-3) / 1e9 / L2_PEAK_GBS, 4),
                   "rays": n_rays, "node_visits": visits, "tri_tests": tests, "diffuse_events": diffuse,
                   "hbm_bytes": pmc.get("stage_hbm_bytes") if matches else None},
-        "timing": "kernel ms: HIP events right before / after each kernel on the stream it runs on, in every one "
-                  "of the %d timed frames (rt_frame_marks); rocprofv3 --stats of this command: "
-                  "profiles/r03_kernel_stats.csv (this process's launches: warm-up + timed + 1 detail frame)" % marked,
+        "timing": ("%s: HIP events right before / after it on the stream it runs on, in every one of the %d "
+                   "timed frames (rt_frame_marks); chosen as the longest critical-stream kernel of warm-up frames "
+                   "2..%d; the other kernels: the same events over 20 pipelined frames after the timed ones "
+                   "(rt_time_frame_kernels); rocprofv3 --kernel-trace --stats of this command: "
+                   "profiles/r03_kernel_stats.csv (this process: warm-up, timed, 1 detail and the 20 split frames)"
+                   % (dom, marked, args.warmup)),
+        "kernel_ms_split_frames": round(split_dom, 5),
     }
     rt.cleanup()
 

@@ -342,10 +342,11 @@ int rt_time_path_trace_kernels(rt_context* ctx, int iters, float* kernel_ms, int
 int rt_time_frame_kernels(rt_context* ctx, int first_frame, int iters, float* kernel_ms, int n);
 
 /* The same split recorded inside the caller's own frames: the next `frames` path traces bracket
- * each of their kernels with HIP events on the stream it runs on (two events per kernel, no
- * synchronisation); rt_frame_marks_read waits, writes the per-kernel average milliseconds over the
- * frames recorded (n >= 7, order as above) and stops recording.  bench.py's timed region uses it. */
-int rt_frame_marks_begin(rt_context* ctx, int frames);
+ * the kernels whose bit is set in kernel_mask (bit k = kernel k, order as above) with HIP events on
+ * the stream each runs on (two events per kernel, no synchronisation); rt_frame_marks_read waits,
+ * writes the per-kernel average milliseconds over the frames recorded (n >= 7; -1 for kernels not
+ * marked) and stops recording.  bench.py's warm-up and timed frames use it. */
+int rt_frame_marks_begin(rt_context* ctx, int frames, uint32_t kernel_mask);
 int rt_frame_marks_read(rt_context* ctx, float* kernel_ms, int n, int* frames_recorded);
 
 /* Copies device arrays to host (debug dumps of bvh.cu:15-96, traversal outputs). */

@@ -452,7 +452,7 @@ void rt_destroy(rt_context* ctx) {
     if (ctx->sideStream) (void)hipStreamDestroy(ctx->sideStream);
     if (ctx->ownPostStream) (void)hipStreamDestroy(ctx->ownPostStream);
     for (void* p : ctx->allocations) (void)hipFree(p);
-    for (hipEvent_t e : ctx->markRing)
+    for (hipEvent_t e : ctx->markPool)
         if (e) (void)hipEventDestroy(e);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -706,16 +706,20 @@ int rt_time_frame_kernels(rt_context* ctx, int first_frame, int iters, float* ke
     return time_kernels(ctx, first_frame, iters, kernel_ms, n, true);
 }
 
-int rt_frame_marks_begin(rt_context* ctx, int frames) {
-    if (!ctx || frames < 0 || frames > 100000) return RT_ERR_ARG;
+int rt_frame_marks_begin(rt_context* ctx, int frames, uint32_t kernel_mask) {
+    if (!ctx || frames < 0 || frames > 100000 || (kernel_mask & ~((1u << kPtKernels) - 1u)) != 0) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_frame_marks_begin before rt_init"; return RT_ERR_STATE; }
     if (int rc = sync_streams(ctx)) return rc;  // the events of earlier frames are complete
     const size_t need = (size_t)frames * 2 * kPtKernels;
-    while (ctx->markRing.size() < need) {
+    while (ctx->markPool.size() < need) {
         hipEvent_t e = nullptr;
         HIP_TRY(ctx, hipEventCreate(&e));
-        ctx->markRing.push_back(e);
+        ctx->markPool.push_back(e);
     }
+    ctx->markRing.assign(need, nullptr);  // unmarked kernels keep null entries (no event recorded)
+    for (size_t i = 0; i < need; ++i)
+        if (kernel_mask & (1u << ((i % (2 * kPtKernels)) / 2))) ctx->markRing[i] = ctx->markPool[i];
+    ctx->markMask = kernel_mask;
     ctx->markFrames = frames;
     ctx->markNext = 0;
     return RT_OK;
@@ -726,9 +730,10 @@ int rt_frame_marks_read(rt_context* ctx, float* kernel_ms, int n, int* frames_re
     if (!ctx->inited) { ctx->err = "rt_frame_marks_read before rt_init"; return RT_ERR_STATE; }
     if (int rc = sync_streams(ctx)) return rc;
     const int frames = ctx->markNext;
-    for (int k = 0; k < kPtKernels; ++k) kernel_ms[k] = 0.0f;
+    for (int k = 0; k < kPtKernels; ++k) kernel_ms[k] = (ctx->markMask & (1u << k)) ? 0.0f : -1.0f;
     for (int i = 0; i < frames; ++i)
         for (int k = 0; k < kPtKernels; ++k) {
+            if (!(ctx->markMask & (1u << k))) continue;
             const hipEvent_t* m = ctx->markRing.data() + (size_t)i * 2 * kPtKernels;
             float ms = 0.0f;
             HIP_TRY(ctx, hipEventElapsedTime(&ms, m[2 * k], m[2 * k + 1]));

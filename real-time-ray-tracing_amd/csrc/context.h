@@ -199,7 +199,8 @@ struct rt_context {
     DenoisePostParams postParams{};
     hipEvent_t* ptMarks = nullptr;  // set only inside rt_time_path_trace_kernels
     // rt_frame_marks_begin: events around every path-trace kernel of the next markFrames path traces
-    std::vector<hipEvent_t> markRing;
+    std::vector<hipEvent_t> markPool, markRing;  // ring: pool entries of the marked kernels, else null
+    uint32_t markMask = 0;
     int markFrames = 0, markNext = 0;
     float* dVerts = nullptr;
     float* dNormals = nullptr;

@@ -1052,13 +1052,13 @@ extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t
     if ((size_t)p->rows * p->width >= (1u << 26) || (size_t)p->rows * p->width * p->spp > p->ws.cap)
         return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
-    if (e == hipSuccess && marks) e = hipEventRecord(marks[0], stream);  // begin / end of kernel 0
+    if (e == hipSuccess && marks && marks[0]) e = hipEventRecord(marks[0], stream);  // begin / end of kernel 0
     if (e != hipSuccess) return e;
     const int nSW = cam_sample_waves(p->spp);
     const int BW = nSW == 4 ? 8 : 16, BH = nSW == 1 ? 16 : 8;
     const dim3 grid((p->width + BW - 1) / BW, (p->rows + BH - 1) / BH);
     hipLaunchKernelGGL(k_pt_camera, grid, dim3(256), 0, stream, *p);
-    if (marks && (e = hipEventRecord(marks[1], stream)) != hipSuccess) return e;
+    if (marks && marks[1] && (e = hipEventRecord(marks[1], stream)) != hipSuccess) return e;
     return hipGetLastError();
 }
 
@@ -1068,9 +1068,10 @@ extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t s
                                          const PtLaunchHook* hook) {
     hipError_t e = hipSuccess;  // the counters were zeroed before the camera kernel (rtk_launch_pt_camera)
     int k = 1;  // kernel 1 = shade; marks[2k] / marks[2k + 1] bracket kernel k on this stream
-    auto begin = [&]() { return marks ? hipEventRecord(marks[2 * k], stream) : hipSuccess; };
+    // a null entry: that kernel is not bracketed (rt_frame_marks_begin's kernel mask)
+    auto begin = [&]() { return marks && marks[2 * k] ? hipEventRecord(marks[2 * k], stream) : hipSuccess; };
     auto end = [&]() {  // the mark first: a hook that blocks the host must not delay it
-        const hipError_t me = marks ? hipEventRecord(marks[2 * k + 1], stream) : hipSuccess;
+        const hipError_t me = marks && marks[2 * k + 1] ? hipEventRecord(marks[2 * k + 1], stream) : hipSuccess;
         if (me != hipSuccess) return me;
         if (hook && hook->fn) {
             const hipError_t he = hook->fn(hook->arg, k);

@@ -142,7 +142,7 @@ SIGNATURES = {
     "rt_save_image": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
     "rt_upload_texture": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]),
     "rt_scene_noise3d": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p]),
-    "rt_frame_marks_begin": (C.c_int, [C.c_void_p, C.c_int]),
+    "rt_frame_marks_begin": (C.c_int, [C.c_void_p, C.c_int, C.c_uint32]),
     "rt_frame_marks_read": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]),
 }
 IMAGE_PPM_RGBA8, IMAGE_PFM_HDR = 0, 1
@@ -386,16 +386,19 @@ class RayTracer:
         self._check(self.lib.rt_time_frame_kernels(self.h, first_frame, iters, ms, len(ms)), "rt_time_frame_kernels")
         return dict(zip(self.PT_KERNELS, (float(v) for v in ms)))
 
-    def frame_marks_begin(self, frames: int):
-        """Bracket each path-trace kernel of the next `frames` path traces with HIP events."""
-        self._check(self.lib.rt_frame_marks_begin(self.h, frames), "rt_frame_marks_begin")
+    def frame_marks_begin(self, frames: int, kernels=None):
+        """Bracket the path-trace kernels named in `kernels` (all when None) of the next `frames`
+        path traces with HIP events on the streams they run on."""
+        names = self.PT_KERNELS if kernels is None else kernels
+        mask = sum(1 << self.PT_KERNELS.index(k) for k in names)
+        self._check(self.lib.rt_frame_marks_begin(self.h, frames, mask), "rt_frame_marks_begin")
 
     def frame_marks_read(self):
-        """(average ms per path-trace kernel over the recorded frames, frames recorded); waits."""
+        """({kernel: average ms over the recorded frames} for the marked kernels, frames recorded); waits."""
         ms = (C.c_float * len(self.PT_KERNELS))()
         n = C.c_int()
         self._check(self.lib.rt_frame_marks_read(self.h, ms, len(ms), C.byref(n)), "rt_frame_marks_read")
-        return dict(zip(self.PT_KERNELS, (float(v) for v in ms))), n.value
+        return {k: float(v) for k, v in zip(self.PT_KERNELS, ms) if v >= 0.0}, n.value
 
     # ---- camera file I/O and offscreen image dumps
     def save_camera(self, path: str):

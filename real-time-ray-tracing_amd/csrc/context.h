@@ -101,6 +101,7 @@ struct FrameResources {
     uint16_t* histDepth = nullptr; // HistoryDepthBuffer
     uint16_t* noise8 = nullptr;
     uint16_t* noise16 = nullptr;
+    uint32_t* chainCounter = nullptr;  // k_downscale_chain's finished-workgroup count (re-armed by its last one)
     uint2* c4 = nullptr;
     uint2* c16 = nullptr;
     uint2* c64 = nullptr;

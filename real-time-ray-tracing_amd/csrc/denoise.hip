@@ -25,6 +25,37 @@ namespace {
 
 constexpr float kRayMaxF = 10e10f;
 
+// ablation switches for profiling builds only (tools/abl_build.sh); the product build defines none
+#ifdef RTX_ABL_DN_NOPOW
+#define DN_POW(a, b) (a)
+#else
+#define DN_POW(a, b) rt_powf(a, b)
+#endif
+#ifdef RTX_ABL_DN_NOEXP
+#define DN_EXP(a) (a)
+#else
+#define DN_EXP(a) rt_expf(a)
+#endif
+#ifndef RTX_DN_BATCH
+#define RTX_DN_BATCH 5
+#endif
+constexpr int kDnBatch = RTX_DN_BATCH;  // SpatialFilterGlobal5x5 taps per load batch
+#if defined(RTX_DN5_WAVES) && RTX_DN5_WAVES > 0
+#define DN5_BOUNDS __launch_bounds__(256, RTX_DN5_WAVES)
+#else
+#define DN5_BOUNDS __launch_bounds__(256)
+#endif
+#ifndef RTX_DN7_UNROLL
+#define RTX_DN7_UNROLL 6
+#endif
+#define DN_PRAGMA(x) _Pragma(#x)
+#define DN_UNROLL(n) DN_PRAGMA(unroll n)
+#ifdef RTX_ABL_DN_GATEALL
+constexpr bool kDnGateAll = true;
+#else
+constexpr bool kDnGateAll = false;
+#endif
+
 // gaussian.cuh:12-47 (double literals converted to float, as the reference's float arrays)
 __constant__ float cG3[9] = {(float)0.0578968, (float)0.0921378, (float)0.0584323, (float)0.0921378, (float)0.146629,
                              (float)0.09299,   (float)0.0584322, (float)0.0929898, (float)0.0589727};
@@ -80,7 +111,13 @@ struct View1 {
     RT_DEV float at(int x, int y) const { return h2f(p[(size_t)clampi(y, 0, H - 1) * W + clampi(x, 0, W - 1)]); }
 };
 
-RT_DEV F3 bicubic_smooth(const View2& im, F2 uv) {
+// SampleBicubicSmoothStep: the footprint (first texel, weights) of uv, and the weighted sum of the
+// four texels q[i] = im.at(t0x + (i & 1), t0y + (i >> 1)); split so callers can issue the loads early
+struct SmoothTaps {
+    int t0x, t0y;
+    float wt[4];
+};
+RT_DEV SmoothTaps smooth_taps(const View2& im, F2 uv) {
     const F2 UV = {uv.x * (float)im.W, uv.y * (float)im.H};
     const float fx0 = floorf(UV.x - 0.5f), fy0 = floorf(UV.y - 0.5f);
     const F2 f = {UV.x - (fx0 + 0.5f), UV.y - (fy0 + 0.5f)};
@@ -88,16 +125,24 @@ RT_DEV F3 bicubic_smooth(const View2& im, F2 uv) {
     const F2 f3v = {f2.x * f.x, f2.y * f.y};
     const F2 w1 = {f3v.x * -2.0f + f2.x * 3.0f, f3v.y * -2.0f + f2.y * 3.0f};
     const F2 w0 = {1.0f - w1.x, 1.0f - w1.y};
-    const int t0x = (int)fx0, t0y = (int)fy0;
-    const float wt[4] = {w0.x * w0.y, w1.x * w0.y, w0.x * w1.y, w1.x * w1.y};
+    return SmoothTaps{(int)fx0, (int)fy0, {w0.x * w0.y, w1.x * w0.y, w0.x * w1.y, w1.x * w1.y}};
+}
+RT_DEV F3 smooth_sum(const SmoothTaps& t, const uint2* q) {
     F3 o = f3(0.0f);
     float sw = 0.0f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        sw += wt[i];
-        o = o + rgb_of(im.at(t0x + (i & 1), t0y + (i >> 1))) * wt[i];
+        sw += t.wt[i];
+        o = o + rgb_of(q[i]) * t.wt[i];
     }
     return o / sw;
+}
+RT_DEV F3 bicubic_smooth(const View2& im, F2 uv) {
+    const SmoothTaps t = smooth_taps(im, uv);
+    uint2 q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = im.at(t.t0x + (i & 1), t.t0y + (i >> 1));
+    return smooth_sum(t, q);
 }
 
 // 16-row tile row of this workgroup: launches may cover tile rows [P.ty0, P.ty1) only
@@ -115,17 +160,16 @@ RT_DEV T tree_sum32(T v) {
 // one per 8x8 tile, with k_tile_noise's lane layout and shuffle-tree order; thread 0 then
 // averages the four half-rounded tile values into the 16x16 noise level.  Reads outside the
 // image clamp to its edge, which always lands inside this workgroup's tile.
-RT_DEV void noise_epilogue(const DenoisePostParams& P, const uint2* sOut, uint16_t* sN8) {
+RT_DEV void noise_epilogue(const DenoisePostParams& P, const uint2* sOut, uint16_t* sN8, int BX, int TY) {
     const int W = (int)P.W, H = (int)P.H;
     const int W8 = (W + 7) / 8, H8 = (H + 7) / 8, W16 = (W + 15) / 16, H16 = (H + 15) / 16;
     const int tid = threadIdx.x;
-    const int TY = tile_y(P);
-    const int x0 = blockIdx.x * 16, y0 = TY * 16;
+    const int x0 = BX * 16, y0 = TY * 16;
     if (tid < 128) {
         const int t = tid >> 5, lane = tid & 31;
-        const int tx8 = 2 * blockIdx.x + (t & 1), ty8 = 2 * TY + (t >> 1);
+        const int tx8 = 2 * BX + (t & 1), ty8 = 2 * TY + (t >> 1);
         const bool valid = tx8 < W8 && ty8 < H8;
-        const int x = clampi((valid ? tx8 : 2 * (int)blockIdx.x) * 8 + (lane & 7), 0, W - 1);
+        const int x = clampi((valid ? tx8 : 2 * BX) * 8 + (lane & 7), 0, W - 1);
         const int ya = clampi((valid ? ty8 : 2 * TY) * 8 + 2 * (lane >> 3), 0, H - 1);
         const int yb = clampi((valid ? ty8 : 2 * TY) * 8 + 2 * (lane >> 3) + 1, 0, H - 1);
         const F3 ca = rgb_of(sOut[(ya - y0) * 16 + (x - x0)]), cb = rgb_of(sOut[(yb - y0) * 16 + (x - x0)]);
@@ -151,11 +195,11 @@ RT_DEV void noise_epilogue(const DenoisePostParams& P, const uint2* sOut, uint16
         }
     }
     __syncthreads();
-    if (tid == 0 && (int)blockIdx.x < W16 && TY < H16) {
+    if (tid == 0 && BX < W16 && TY < H16) {
         // n8.at(2x + i, 2y + j) clamped to the tile grid: tile i/j falls back to 0 past its edge
-        const int i1 = 2 * (int)blockIdx.x + 1 < W8 ? 1 : 0, j1 = 2 * TY + 1 < H8 ? 2 : 0;
+        const int i1 = 2 * BX + 1 < W8 ? 1 : 0, j1 = 2 * TY + 1 < H8 ? 2 : 0;
         const float v1 = h2f(sN8[0]), v2 = h2f(sN8[i1]), v3 = h2f(sN8[j1]), v4 = h2f(sN8[i1 + j1]);
-        P.noise16[TY * W16 + blockIdx.x] = (uint16_t)f2h((v1 + v2 + v3 + v4) / 4);
+        P.noise16[TY * W16 + BX] = (uint16_t)f2h((v1 + v2 + v3 + v4) / 4);
     }
 }
 
@@ -173,10 +217,11 @@ __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uin
         const uint2 res = temporal_pixel(P, in, x, y);
         out[(size_t)y * W + x] = res;
         if (kNoise) sOut[threadIdx.x] = res;
+        if (P.histDepthInTemporal) P.histDepth[(size_t)y * W + x] = P.depth[(size_t)y * W + x];
     }
     if (kNoise) {
         __syncthreads();
-        noise_epilogue(P, sOut, sN8);
+        noise_epilogue(P, sOut, sN8, (int)blockIdx.x, tile_y(P));
     }
 }
 
@@ -197,18 +242,27 @@ RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, 
         F3 nMax = ycocg(cV), nMin = ycocg(cV);
         F3 filt = f3(0.0f);
         float wsum = 0.0f;
+        // the nine taps' loads issued together (see k_spatial5's batches)
+        uint2 qv[9], nq[9];
+        float dv[9];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            const int sx = x + j % 3 - 1, sy = y + j / 3 - 1;
+            qv[j] = col.at(sx, sy);
+            dv[j] = dep.at(sx, sy);
+            nq[j] = nrm.at(sx, sy);
+        }
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
             const int xo = j % 3, yo = j / 3;
-            const int sx = x + xo - 1, sy = y + yo - 1;
-            const uint2 q = col.at(sx, sy);
+            const uint2 q = qv[j];
             const F3 cc = rgb_of(q);
-            const float d = dep.at(sx, sy);
-            const F3 n = rgb_of(nrm.at(sx, sy));
+            const float d = dv[j];
+            const F3 n = rgb_of(nq[j]);
             float w = 1.0f;
-            w *= rt_powf(fmaxf(dot(nV, n), 0.0f), P.dn.temporal_denoise_sigma_normal);
+            w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.temporal_denoise_sigma_normal);
             const float dd = (dV - d) / P.dn.temporal_denoise_sigma_depth;
-            w *= rt_expf(-0.5f * dd * dd);
+            w *= DN_EXP(-0.5f * dd * dd);
             w *= (mV != mask_of(q)) ? 1.0f / P.dn.temporal_denoise_sigma_material : 1.0f;
             w *= cG3[xo + yo * 3];
             filt = filt + cc * w;
@@ -316,6 +370,7 @@ __global__ __launch_bounds__(256) void k_noise_visualize(DenoisePostParams P, ui
 // 16x16 tile + 3-pixel apron staged in LDS (22 x 22 entries of colour, normal, depth).
 struct Tap7 { uint2 c; uint2 n; float d; };
 
+template <int kParity>
 RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD, int tx,
                             int ty);
 
@@ -331,7 +386,7 @@ __global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uin
     const int TY = tile_y(P);
     const int x = blockIdx.x * 16 + tx, y = TY * 16 + ty;
     const int W16 = (W + 15) / 16;
-    const bool gated = h2f(P.noise16[TY * W16 + blockIdx.x]) < P.dn.noise_threshold_local;
+    const bool gated = kDnGateAll || h2f(P.noise16[TY * W16 + blockIdx.x]) < P.dn.noise_threshold_local;
     const View2 col{in, W, H}, nrm{P.normal, W, H};
     const View1 dep{P.depth, W, H};
     if (!gated) {
@@ -345,16 +400,20 @@ __global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uin
     __syncthreads();
     if (x < W && y < H) {
         const size_t p = (size_t)y * W + x;
-        const uint2 res = gated ? in[p] : spatial7_pixel(P, sC, sN, sD, tx, ty);
+        // the tap set alternates with the frame parity: both sets compiled with constant offsets
+        const uint2 res = gated ? in[p]
+                          : (P.frameNum % 2 == 0 ? spatial7_pixel<0>(P, sC, sN, sD, tx, ty)
+                                                 : spatial7_pixel<1>(P, sC, sN, sD, tx, ty));
         out[p] = res;
         if (kNoise) sOut[threadIdx.x] = res;
     }
     if (kNoise) {
         __syncthreads();
-        noise_epilogue(P, sOut, sN8);
+        noise_epilogue(P, sOut, sN8, (int)blockIdx.x, tile_y(P));
     }
 }
 
+template <int kParity>
 RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD, int tx,
                             int ty) {
     const int ci = (tx + 3) + (ty + 3) * 22;
@@ -369,10 +428,10 @@ RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const u
     if (!isnan3(cV) && dV < kRayMaxF) {
         F3 sum = f3(0.0f);
         float sw = 0.0f;
-        int j = P.frameNum % 2;
+DN_UNROLL(RTX_DN7_UNROLL)
         for (int i = 0; i < 24; ++i) {
+            const int j = kParity + 2 * i;  // P.frameNum % 2 + 2i
             const int xo = j % 7, yo = j / 7;
-            j += 2;
             const int li = (tx + xo) + (ty + yo) * 22;
             const uint2 q = sC[li];
             F3 cc = rgb_of(q);
@@ -382,9 +441,9 @@ RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const u
             if (d != d) d = 0.0f;
             if (isnan3(n)) n = f3(0.0f);
             float w = 1.0f;
-            w *= rt_powf(fmaxf(dot(nV, n), 0.0001f), P.dn.local_denoise_sigma_normal);
+            w *= DN_POW(fmaxf(dot(nV, n), 0.0001f), P.dn.local_denoise_sigma_normal);
             const float dd = (dV - d) / P.dn.local_denoise_sigma_depth;
-            w *= rt_expf(-0.5f * dd * dd);
+            w *= DN_EXP(-0.5f * dd * dd);
             w *= (mV != mask_of(q)) ? 1.0f / P.dn.local_denoise_sigma_material : 1.0f;
             w *= cG7[xo + yo * 7];
             sum = sum + cc * w;
@@ -402,7 +461,7 @@ RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const u
 // ------------------------------------------------------------------ SpatialFilterGlobal5x5<S>
 // kAlbedo: ApplyAlbedo (denoising.cu:160-171) fused into the store of the last wide pass
 template <int S, bool kAlbedo>
-__global__ __launch_bounds__(256) void k_spatial5(DenoisePostParams P, const uint2* in, uint2* out) {
+__global__ DN5_BOUNDS void k_spatial5(DenoisePostParams P, const uint2* in, uint2* out) {
     const int W = (int)P.W, H = (int)P.H;
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= W || y >= H) return;
@@ -410,7 +469,7 @@ __global__ __launch_bounds__(256) void k_spatial5(DenoisePostParams P, const uin
     const int W16 = (W + 15) / 16;
     const uint2 c0 = in[p];
     uint2 res = c0;
-    if (!(h2f(P.noise16[tile_y(P) * W16 + blockIdx.x]) < P.dn.noise_threshold_large)) {
+    if (!kDnGateAll && !(h2f(P.noise16[tile_y(P) * W16 + blockIdx.x]) < P.dn.noise_threshold_large)) {
         const View2 col{in, W, H}, nrm{P.normal, W, H};
         const View1 dep{P.depth, W, H};
         F3 nV = rgb_of(P.normal[p]);
@@ -423,23 +482,40 @@ __global__ __launch_bounds__(256) void k_spatial5(DenoisePostParams P, const uin
         if (dV < 10e9f) {
             F3 sum = f3(0.0f);
             float sw = 0.0f;
-#pragma unroll 5
-            for (int k = 0; k < 25; ++k) {
-                const int i = k % 5, j = k / 5;
-                const int sx = x + (i - 2) * S, sy = y + (j - 2) * S;
-                const uint2 q = col.at(sx, sy);
-                F3 cc = rgb_of(q);
-                const float d = dep.at(sx, sy);
-                const F3 n = rgb_of(nrm.at(sx, sy));
-                float w = 1.0f;
-                w *= rt_powf(fmaxf(dot(nV, n), 0.0f), P.dn.large_denoise_sigma_normal);
-                const float dd = (dV - d) / P.dn.large_denoise_sigma_depth;
-                w *= rt_expf(-0.5f * dd * dd);
-                w *= (mV != mask_of(q)) ? 1.0f / P.dn.large_denoise_sigma_material : 1.0f;
-                w *= cG5[i + j * 5];
-                if (isnan3(cc)) { cc = f3(0.0f); w = 0.0f; }
-                sum = sum + cc * w;
-                sw += w;
+            // taps in batches of kDnBatch: a batch's loads are issued together, then its weights
+            // computed (the branches of rt_powf otherwise keep the compiler from hoisting the next
+            // tap's loads, one memory round trip per tap)
+#pragma unroll
+            for (int k0 = 0; k0 < 25; k0 += kDnBatch) {
+                uint2 qv[kDnBatch], nq[kDnBatch];
+                float dv[kDnBatch];
+#pragma unroll
+                for (int m = 0; m < kDnBatch; ++m) {
+                    const int k = k0 + m < 25 ? k0 + m : 24;
+                    const int sx = x + (k % 5 - 2) * S, sy = y + (k / 5 - 2) * S;
+                    qv[m] = col.at(sx, sy);
+                    dv[m] = dep.at(sx, sy);
+                    nq[m] = nrm.at(sx, sy);
+                }
+#pragma unroll
+                for (int m = 0; m < kDnBatch; ++m) {
+                    const int k = k0 + m;
+                    if (k >= 25) break;
+                    const int i = k % 5, j = k / 5;
+                    const uint2 q = qv[m];
+                    F3 cc = rgb_of(q);
+                    const float d = dv[m];
+                    const F3 n = rgb_of(nq[m]);
+                    float w = 1.0f;
+                    w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.large_denoise_sigma_normal);
+                    const float dd = (dV - d) / P.dn.large_denoise_sigma_depth;
+                    w *= DN_EXP(-0.5f * dd * dd);
+                    w *= (mV != mask_of(q)) ? 1.0f / P.dn.large_denoise_sigma_material : 1.0f;
+                    w *= cG5[i + j * 5];
+                    if (isnan3(cc)) { cc = f3(0.0f); w = 0.0f; }
+                    sum = sum + cc * w;
+                    sw += w;
+                }
             }
             if (isnan3(sum)) sum = f3(0.0f);
             if (sw != sw) sw = 0.0f;
@@ -468,8 +544,30 @@ __global__ __launch_bounds__(256) void k_temporal2(DenoisePostParams P, const ui
     if (x >= W || y >= H) return;
     const size_t p = (size_t)y * W + x;
     const View2 col{in, W, H}, hc{P.histColor, (int)P.histW, (int)P.histH};
-    const uint2 c0 = in[p];
-    out[p] = c0;
+    // Loads in two batches — the 3x3 neighbourhood with the motion vector, then the history texels
+    // it points at — and the reference's early-outs (history off screen, every history texel of
+    // another material) as one select of the output.  Written as branches, the compiler split each
+    // neighbour load into a mask read and a dependent colour read and sank the history reads below
+    // the discard test: ~13 dependent round trips per pixel instead of 2.
+    uint2 qs[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) qs[j] = col.at(x + j % 3 - 1, y + j / 3 - 1);  // qs[4]: the pixel
+    const uint32_t mvq = P.motion[p];
+    const F2 mv = {h2f(mvq & 0xFFFFu) - 0.5f, h2f(mvq >> 16) - 0.5f};
+    const F2 inv = {1.0f / (float)W, 1.0f / (float)H};
+    const F2 uv = {((float)x + 0.5f) * inv.x, ((float)y + 0.5f) * inv.y};
+    const F2 huv = {uv.x + mv.x, uv.y + mv.y};
+    const bool onScreen = !(huv.x < 0 || huv.y < 0 || huv.x > 1.0f || huv.y > 1.0f);
+    const SmoothTaps ht = smooth_taps(hc, huv);  // clamped reads: safe off screen too
+    const int hx = (int)floorf(huv.x * (float)hc.W), hy = (int)floorf(huv.y * (float)hc.H);
+    uint2 hq[4];
+    uint32_t hm[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        hq[i] = hc.at(ht.t0x + (i & 1), ht.t0y + (i >> 1));
+        hm[i] = mask_of(hc.at(hx + i % 2, hy + i / 2));
+    }
+    const uint2 c0 = qs[4];
     const F3 cV = ycocg_inv(ycocg(rgb_of(c0)));
     const int mV = (int)mask_of(c0);
     const float FLTMIN = 1.17549435e-38f, FLTMAX = 3.402823466e+38f;
@@ -477,35 +575,25 @@ __global__ __launch_bounds__(256) void k_temporal2(DenoisePostParams P, const ui
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
         const int xo = j % 3, yo = j / 3;
-        const uint2 q = col.at(x + xo - 1, y + yo - 1);
-        if ((int)mask_of(q) == mV) {
-            const F3 cc = ycocg(rgb_of(q));
-            nMax = fmax3(nMax, cc);
-            nMin = fmin3(nMin, cc);
-            if (abs(xo - 1) + abs(yo - 1) <= 1) {
-                nMax2 = fmax3(nMax2, cc);
-                nMin2 = fmin3(nMin2, cc);
-            }
+        const bool same = (int)mask_of(qs[j]) == mV;
+        const F3 cc = ycocg(rgb_of(qs[j]));
+        nMax = same ? fmax3(nMax, cc) : nMax;
+        nMin = same ? fmin3(nMin, cc) : nMin;
+        if (abs(xo - 1) + abs(yo - 1) <= 1) {
+            nMax2 = same ? fmax3(nMax2, cc) : nMax2;
+            nMin2 = same ? fmin3(nMin2, cc) : nMin2;
         }
     }
     nMax = (nMax + nMax2) / 2.0f;
     nMin = (nMin + nMin2) / 2.0f;
-    const uint32_t mvq = P.motion[p];
-    const F2 mv = {h2f(mvq & 0xFFFFu) - 0.5f, h2f(mvq >> 16) - 0.5f};
-    const F2 inv = {1.0f / (float)W, 1.0f / (float)H};
-    const F2 uv = {((float)x + 0.5f) * inv.x, ((float)y + 0.5f) * inv.y};
-    const F2 huv = {uv.x + mv.x, uv.y + mv.y};
-    if (huv.x < 0 || huv.y < 0 || huv.x > 1.0f || huv.y > 1.0f) return;
-    F3 cH = bicubic_smooth(hc, huv);
+    F3 cH = smooth_sum(ht, hq);
     const F3 cHy = clamp3(ycocg(cH), nMin, nMax);
     cH = ycocg_inv(cHy);
     const float lumaMin = nMin.x, lumaMax = nMax.x, lumaC = ycocg(cV).x;
     float discard = 0.0f;
-    const int hx = (int)floorf(huv.x * (float)hc.W), hy = (int)floorf(huv.y * (float)hc.H);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) discard += (mV != (int)mask_of(hc.at(hx + i % 2, hy + i / 2))) ? 1.0f : 0.0f;
+    for (int i = 0; i < 4; ++i) discard += (mV != (int)hm[i]) ? 1.0f : 0.0f;
     discard /= 4.0f;
-    if (discard == 1.0f) return;
     cH = cH * (1.0f - discard) + cV * discard;
     const float lumaH = ycocg(cH).x;
     float blend = 3.0f / 4.0f;
@@ -518,7 +606,8 @@ __global__ __launch_bounds__(256) void k_temporal2(DenoisePostParams P, const ui
     wB *= ws;
     F3 o = cV * wA + cH * wB;
     if (isnan3(o)) o = f3(0.0f);
-    out[p] = pack_color(o, (uint32_t)mV & 0xFFFFu);
+    const uint2 blended = pack_color(o, (uint32_t)mV & 0xFFFFu);
+    out[p] = onScreen && discard != 1.0f ? blended : c0;
 }
 
 // ------------------------------------------------------------------ post
@@ -528,15 +617,8 @@ RT_DEV H4 add4(H4 a, H4 b) { return H4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.
 RT_DEV uint2 pack_h4(H4 v) { return make_uint2(f2h(v.x) | (f2h(v.y) << 16), f2h(v.z) | (f2h(v.w) << 16)); }
 
 // DownScale4: output texel = 4x4 box of inputs, summed as the reference's 2x2-of-2x2 tree
-// output rows [oy0, oy1) only (a strip-local denoise computes its own rows)
-__global__ __launch_bounds__(256) void k_downscale4(const uint2* in, int Wi, int Hi, uint2* out, int Wo, int Ho,
-                                                    int oy0, int oy1) {
-    int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= Wo * (oy1 - oy0)) return;
-    const int ox = i % Wo, oy = oy0 + i / Wo;
-    if (oy >= Ho) return;
-    i = oy * Wo + ox;
-    const View2 im{in, Wi, Hi};
+template <class Img>
+RT_DEV uint2 down4(const Img& im, int ox, int oy) {
     H4 q[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -552,7 +634,26 @@ __global__ __launch_bounds__(256) void k_downscale4(const uint2* in, int Wi, int
                 }
             q[a][b] = add4(add4(add4(s[0][0], s[1][0]), s[0][1]), s[1][1]);
         }
-    out[i] = pack_h4(add4(add4(add4(q[0][0], q[1][0]), q[0][1]), q[1][1]));
+    return pack_h4(add4(add4(add4(q[0][0], q[1][0]), q[0][1]), q[1][1]));
+}
+
+// output rows [oy0, oy1) only (a strip-local denoise computes its own rows)
+__global__ __launch_bounds__(256) void k_downscale4(const uint2* in, int Wi, int Hi, uint2* out, int Wo, int Ho,
+                                                    int oy0, int oy1) {
+    int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= Wo * (oy1 - oy0)) return;
+    const int ox = i % Wo, oy = oy0 + i / Wo;
+    if (oy >= Ho) return;
+    out[oy * Wo + ox] = down4(View2{in, Wi, Hi}, ox, oy);
+}
+
+// Histogram2's bin of one 1/64 texel
+RT_DEV uint32_t histogram_bin(uint2 q) {
+    const H4 v = h4_of(q);
+    const float lum = dot(f3(v.x, v.y, v.z), f3((float)0.3, (float)0.6, (float)0.1));
+    const float logL = (float)((double)rt_log2f(lum) * 0.1 + 0.75);
+    const float sc = (float)((double)(clampf(logL, 0.0f, 1.0f) * 63) * 0.99999);
+    return (uint32_t)rintf(sc);
 }
 
 // Histogram2: one 32x32 workgroup over the top-left min(W64,32) x min(H64,32) texels
@@ -563,44 +664,46 @@ __global__ __launch_bounds__(1024) void k_histogram(const uint2* c64, int W64, i
     __syncthreads();
     const int x = threadIdx.x & 31, y = threadIdx.x >> 5;
     const int tw = W64 < 32 ? W64 : 32, th = H64 < 32 ? H64 : 32;
-    if (x < tw && y < th && y >= y0 && y < y1) {
-        const H4 v = h4_of(c64[y * W64 + x]);
-        const float lum = dot(f3(v.x, v.y, v.z), f3((float)0.3, (float)0.6, (float)0.1));
-        const float logL = (float)((double)rt_log2f(lum) * 0.1 + 0.75);
-        const float sc = (float)((double)(clampf(logL, 0.0f, 1.0f) * 63) * 0.99999);
-        atomicAdd(&h[(uint32_t)rintf(sc)], 1u);
-    }
+    if (x < tw && y < th && y >= y0 && y < y1) atomicAdd(&h[histogram_bin(c64[y * W64 + x])], 1u);
     __syncthreads();
     if (threadIdx.x < 64) hist[threadIdx.x] = h[threadIdx.x];
 }
 
 RT_DEV float bin_to_lum(int i) { return rt_exp2f((float)(((double)(float)i / (63 * 0.99999) - 0.75) / 0.1)); }
 
-__global__ void k_auto_exposure(float* e, const uint32_t* hist, float area, float deltaTime, float gain, int enabled,
-                                float fixedExposure) {
-    if (threadIdx.x != 0) return;
+// AutoExposure (postprocessing.cu:5-44) by the first wave of the workgroup (the caller's threads
+// 0..63 all call it): lane i evaluates bin i's share and luminance, then every lane walks the
+// bins in order with the reference's running sums, reading bin i from lane i (v_readlane, no
+// memory round trip per bin), and lane 0 stores the state.
+RT_DEV void auto_exposure_wave(float* e, const uint32_t* hist, float area, float deltaTime, float gain, int enabled,
+                               float fixedExposure) {
+    const int lane = (int)threadIdx.x;
     if (!enabled) {
-        e[0] = fixedExposure;
-        e[1] = e[2] = e[3] = 1.0f;
+        if (lane == 0) {
+            e[0] = fixedExposure;
+            e[1] = e[2] = e[3] = 1.0f;
+        }
         return;
     }
+    const float myFh = (float)hist[lane] / area, myLum = bin_to_lum(lane);
+    auto fh = [&](int i) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(myFh), i)); };
+    auto lumOf = [&](int i) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(myLum), i)); };
     const float darkT = (float)0.4, brightT = (float)0.9;
     float lumiSum = 0, lumiSumArea = 0, accu = 0, brightLum = 0;
     int i = 0;
     for (; i < 64; ++i) {
-        const float fHist = (float)hist[i] / area;
-        const float lum = bin_to_lum(i);
+        const float fHist = fh(i);
         accu += fHist;
         const float dark = accu - darkT;
         if (dark > 0) {
             lumiSumArea += dark;
-            lumiSum += dark * lum;
+            lumiSum += dark * lumOf(i);
             break;
         }
     }
     for (; i < 64; ++i) {
-        const float fHist = (float)hist[i] / area;
-        const float lum = bin_to_lum(i);
+        const float fHist = fh(i);
+        const float lum = lumOf(i);
         accu += fHist;
         const float bright = accu - brightT;
         if (bright > 0) {
@@ -614,6 +717,7 @@ __global__ void k_auto_exposure(float* e, const uint32_t* hist, float area, floa
             lumiSum += fHist * lum;
         }
     }
+    if (lane != 0) return;
     float aveLum = clampf(lumiSum / lumiSumArea, 0.1f, 100.0f);
     float lumTemp = e[1], lumBright = e[2];
     const float k = 1.0f - rt_expf(-deltaTime * 0.001f);
@@ -624,6 +728,78 @@ __global__ void k_auto_exposure(float* e, const uint32_t* hist, float area, floa
     e[1] = lumTemp;
     e[2] = lumBright;
     e[3] = brightLum;
+}
+
+__global__ __launch_bounds__(64) void k_auto_exposure(float* e, const uint32_t* hist, float area, float deltaTime,
+                                                      float gain, int enabled, float fixedExposure) {
+    auto_exposure_wave(e, hist, area, deltaTime, gain, enabled, fixedExposure);
+}
+
+// DownScale4 x 3 + Histogram2 + AutoExposure in one launch (full frame, every pass enabled).
+// Workgroup (X, Y) of the W64 x H64 grid takes the 64x64 render block under 1/64 texel (X, Y): its
+// 16x16 quarter texels (one per thread, from the colour), 4x4 sixteenth texels and the 1/64 texel
+// from LDS, each level's clamped reads landing inside the block (the level's last texel is in the
+// block that covers the edge).  The last workgroup to finish — a device-scope counter after a
+// release fence, an acquire fence before reading — counts the histogram over the 1/64 image and
+// runs the exposure update, and re-arms the counter.
+struct LdsLevel {  // clamped reads of an image level, of the block staged in LDS
+    const uint2* s;
+    int W, H, x0, y0, pitch;
+    RT_DEV uint2 at(int x, int y) const {
+        return s[(clampi(y, 0, H - 1) - y0) * pitch + (clampi(x, 0, W - 1) - x0)];
+    }
+};
+
+__global__ __launch_bounds__(256) void k_downscale_chain(DenoisePostParams P, const uint2* in, uint32_t* counter) {
+    __shared__ uint2 s4[16 * 16];
+    __shared__ uint2 s16[4 * 4];
+    __shared__ uint32_t sHist[64];
+    __shared__ int sLast;
+    const int W = (int)P.W, H = (int)P.H;
+    const int W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16 = (W4 + 3) / 4, H16 = (H4 + 3) / 4, W64 = (W16 + 3) / 4,
+              H64 = (H16 + 3) / 4;
+    const int X = (int)blockIdx.x, Y = (int)blockIdx.y, t = (int)threadIdx.x;
+    {
+        const int ox = X * 16 + (t & 15), oy = Y * 16 + (t >> 4);
+        if (ox < W4 && oy < H4) {
+            const uint2 v = down4(View2{in, W, H}, ox, oy);
+            s4[t] = v;
+            P.c4[oy * W4 + ox] = v;
+        }
+    }
+    __syncthreads();
+    if (t < 16) {
+        const int ox = X * 4 + (t & 3), oy = Y * 4 + (t >> 2);
+        if (ox < W16 && oy < H16) {
+            const uint2 v = down4(LdsLevel{s4, W4, H4, X * 16, Y * 16, 16}, ox, oy);
+            s16[t] = v;
+            P.c16[oy * W16 + ox] = v;
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        P.c64[Y * W64 + X] = down4(LdsLevel{s16, W16, H16, X * 4, Y * 4, 4}, X, Y);
+        __threadfence();
+        sLast = atomicAdd(counter, 1u) == gridDim.x * gridDim.y - 1;
+    }
+    __syncthreads();
+    if (!sLast) return;
+    __threadfence();
+    if (t < 64) sHist[t] = 0u;
+    __syncthreads();
+    const int tw = W64 < 32 ? W64 : 32, th = H64 < 32 ? H64 : 32;
+    for (int i = t; i < 32 * 32; i += 256) {
+        const int x = i & 31, y = i >> 5;
+        if (x < tw && y < th) atomicAdd(&sHist[histogram_bin(P.c64[y * W64 + x])], 1u);
+    }
+    __syncthreads();
+    if (t < 64) {
+        P.histogram[t] = sHist[t];
+        if (t == 0) *counter = 0u;
+        if (P.postProcess)
+            auto_exposure_wave(P.exposure, sHist, (float)(W64 * H64), P.deltaTime, P.gain, P.autoExposure,
+                               P.fixedExposure);
+    }
 }
 
 // BicubicScale with SampleBicubicCatmullRom (16 taps, clamped)
@@ -1009,9 +1185,11 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
     if (phase == 1) {
         uint2* cur = P->finalColor;
         if (P->postProcess) {
-            hipLaunchKernelGGL(k_auto_exposure, dim3(1), dim3(64), 0, s, P->exposure, (const uint32_t*)P->histogram,
-                               (float)(W64 * H64), P->deltaTime, P->gain, P->autoExposure, P->fixedExposure);
-            LAUNCH_CHECK();
+            if (!P->exposureDone) {
+                hipLaunchKernelGGL(k_auto_exposure, dim3(1), dim3(64), 0, s, P->exposure, (const uint32_t*)P->histogram,
+                                   (float)(W64 * H64), P->deltaTime, P->gain, P->autoExposure, P->fixedExposure);
+                LAUNCH_CHECK();
+            }
             // Bloom and LensFlare modify RenderColorBuffer, which here may be the next frame's
             // history (TemporalFilter2's output): both write a colour buffer instead (full frame only).
             uint2* post = cur == P->colorA ? P->colorB : P->colorA;
@@ -1072,11 +1250,14 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         return hipSuccess;
     };
     // ---- TemporalSpatialDenoising (denoising.cu:51-188)
-    bool noise1 = false;
+    bool noise1 = false, histDepthDone = false;
     if (P->temporal && P->frameNum != 1) {
         noise1 = P->localSpatial && !P->visualize;
         uint2* dst = spare;
         if (tiles(4, Q, g)) {
+            // the whole frame without the debug outlines (which rewrite depth): TemporalFilter2's
+            // HistoryDepthBuffer copy rides on this pass's depth reads
+            Q.histDepthInTemporal = histDepthDone = P->temporal2 && !P->stripLocal && !P->visualize;
             if (noise1) hipLaunchKernelGGL(k_temporal<true>, g, b256, 0, s, Q, (const uint2*)cur, dst);
             else hipLaunchKernelGGL(k_temporal<false>, g, b256, 0, s, Q, (const uint2*)cur, dst);
             LAUNCH_CHECK();
@@ -1089,8 +1270,11 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         noise2 = P->wideSpatial && !P->visualize;
         uint2* dst = P->temporal ? P->accum : spare;
         if (tiles(3, Q, g)) {
-            if (noise2) hipLaunchKernelGGL(k_spatial7<true>, g, b256, 0, s, Q, (const uint2*)cur, dst);
-            else hipLaunchKernelGGL(k_spatial7<false>, g, b256, 0, s, Q, (const uint2*)cur, dst);
+            if (noise2) {
+                hipLaunchKernelGGL(k_spatial7<true>, g, b256, 0, s, Q, (const uint2*)cur, dst);
+            } else {
+                hipLaunchKernelGGL(k_spatial7<false>, g, b256, 0, s, Q, (const uint2*)cur, dst);
+            }
             LAUNCH_CHECK();
         }
         next_from(dst);
@@ -1139,7 +1323,9 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
             return e;
         }
         cur = P->histColorOut;
-        if ((e = hipMemcpyAsync(P->histDepth, P->depth, Pn * 2, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+        if (!histDepthDone &&
+            (e = hipMemcpyAsync(P->histDepth, P->depth, Pn * 2, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+            return e;
     }
     P->finalColor = cur;
     if (P->hdrOut && !P->stripLocal) {  // strip-local: after the rows exchange (rtk_hdr_out, frame.cpp)
@@ -1148,7 +1334,13 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
     }
     // ---- PostProcessing (postprocessing.cu:5-161) up to the histogram: the DownScale4 chain and
     // the histogram over this context's rows (64-row aligned strips keep each level's texels local)
-    if (P->postProcess) {
+    if (P->postProcess && P->downScale && P->histogramOn && !P->stripLocal) {
+        // the whole frame with every pass on: the three DownScale4 levels, Histogram2 and
+        // AutoExposure in one launch
+        hipLaunchKernelGGL(k_downscale_chain, dim3(W64, H64), b256, 0, s, *P, (const uint2*)cur, P->chainCounter);
+        LAUNCH_CHECK();
+        P->exposureDone = 1;
+    } else if (P->postProcess) {
         const int ra = P->stripLocal ? (int)P->rowA : 0, rb = P->stripLocal ? (int)P->rowB : H;
         auto span = [](int a, int b, int f, int n, int& o0, int& o1) {
             o0 = a / f;

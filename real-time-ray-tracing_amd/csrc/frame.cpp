@@ -437,6 +437,8 @@ int rt_frame_init(rt_context* ctx) {
     const size_t W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16 = (W4 + 3) / 4, H16 = (H4 + 3) / 4;
     ALLOC(fr.noise8, ((W + 7) / 8) * ((H + 7) / 8) * 2);
     ALLOC(fr.noise16, ((W + 15) / 16) * ((H + 15) / 16) * 2);
+    ALLOC(fr.chainCounter, 4);
+    HIP_TRY(ctx, hipMemset(fr.chainCounter, 0, 4));
     ALLOC(fr.c4, W4 * H4 * 8);
     ALLOC(fr.c16, W16 * H16 * 8);
     ALLOC(fr.c64, ((W16 + 3) / 4) * ((H16 + 3) / 4) * 8);
@@ -543,6 +545,8 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.tanHalfFov[1] = hc.tanHalfFov[1];
     p.res[0] = hc.res[0];
     p.res[1] = hc.res[1];
+    p.halfRes[0] = hc.res[0] / 2;
+    p.halfRes[1] = hc.res[1] / 2;
     p.hist = fr.hist;
     p.width = (uint32_t)ctx->renderW;
     p.height = (uint32_t)ctx->renderH;
@@ -715,6 +719,9 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.histDepth = fr.histDepth;
     p.noise8 = fr.noise8;
     p.noise16 = fr.noise16;
+    p.chainCounter = fr.chainCounter;
+    p.exposureDone = 0;
+    p.histDepthInTemporal = 0;
     p.c4 = fr.c4;
     p.c16 = fr.c16;
     p.c64 = fr.c64;

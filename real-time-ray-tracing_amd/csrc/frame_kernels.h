@@ -120,6 +120,7 @@ struct PathTraceParams {
     TraceCamera cam;
     float tanHalfFov[2];
     float res[2];
+    float halfRes[2];           // res / 2 (exact), from the host: a kernel argument, not a VGPR pair
     HistCamera hist;
     uint32_t width, height;     // full render size (strides)
     uint32_t y0, rows;          // strip rows (row_of): contiguous [y0, y0 + rows) when nStrips = 1
@@ -205,6 +206,9 @@ struct DenoisePostParams {
     uint32_t* rgbaTarget;       // strip-local: the caller's draw target, filled from `rgba` after the rows
     uint32_t rgbaTargetPitch;   // exchange (rgba is then the exchanged buffer); pitch in pixels
     int ty0, ty1;               // per launch (set by the launcher): tile rows of the 16x16-tile kernels
+    uint32_t* chainCounter;     // k_downscale_chain's workgroup counter (zero between launches)
+    int exposureDone;           // set by phase 0 when k_downscale_chain ran AutoExposure
+    int histDepthInTemporal;    // k_temporal also copies depth into the history depth (per launch)
 };
 
 extern "C" hipError_t rtk_denoise_post(DenoisePostParams* p, hipStream_t stream);

@@ -257,7 +257,7 @@ RT_DEV void diffuse(PathCtx& c, int bounce, RayState& rs, F3& beta) {
 
 // GetRayConeWidth (raygen.cuh:45-63)
 RT_DEV float ray_cone_width(const PathTraceParams& P, int ix, int iy) {
-    const F2 pc = {((float)ix + 0.5f) - P.res[0] / 2, ((float)iy + 0.5f) - P.res[1] / 2};
+    const F2 pc = {((float)ix + 0.5f) - P.halfRes[0], ((float)iy + 0.5f) - P.halfRes[1]};  // res / 2
     const F2 po = {copysignf(0.5f, pc.x), copysignf(0.5f, pc.y)};
     const F2 un = {(pc.x - po.x) * P.cam.invRes[0] * 2, (pc.y - po.y) * P.cam.invRes[1] * 2};
     const F2 uf = {(pc.x + po.x) * P.cam.invRes[0] * 2, (pc.y + po.y) * P.cam.invRes[1] * 2};

@@ -561,12 +561,16 @@ RT_HD float rt_powf(float xf, float yf) {
     // NaN.  None of the special cases below applies to it, so this is the same computation as
     // the tail of the general path, without its double-precision classification.
     if (xf > 0.0f && xf < rtm::bits_to_float(0x7F800000u) && yf == yf) {
+        if (xf == 1.0f) return 1.0f;  // exact (the denoiser's equal normals: a whole wave skips the log)
         float lh, ll;
         rtm::log2_pair(xf, lh, ll);
         const float th = yf * lh;
         const float tl = rtm::f_fma(yf, lh, -th) + yf * ll;
         return rtm::exp2_pair(th, tl);
     }
+    // +0 to a positive power (the denoiser's clamped normal weights at right angles): the general
+    // path's answer, without its double-precision classification
+    if (rtm::float_to_bits(xf) == 0u && yf > 0.0f) return 0.0f;
     double x = (double)xf, y = (double)yf;
     if (y == 0.0) return 1.0f;
     if (x == 1.0) return 1.0f;
@@ -604,13 +608,15 @@ RT_HD float rt_powf(float xf, float yf) {
 //
 // On gfx950 both conversions are the hardware v_cvt_f16_f32 / v_cvt_f32_f16 (round to nearest
 // even, half denormals preserved in the default float mode): the same bits as the integer
-// restatement below for every non-NaN input; NaNs are canonicalised to sign | 0x7E00 after
-// the hardware conversion so the two stay identical there too.
+// restatements below for every non-NaN input.  NaNs are canonicalised to sign | 0x7E00 after the
+// hardware float -> half conversion, by a select (a branch here costs a dozen instructions per
+// conversion in the per-tap loops); half -> float quiets a NaN and keeps its payload, as IEEE 754
+// conversion does on both sides.
 RT_HD uint16_t rt_f2h(float f) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (f != f) return (uint16_t)(((rtm::float_to_bits(f) >> 16) & 0x8000u) | 0x7E00u);
-    const _Float16 hv = (_Float16)f;
-    return __builtin_bit_cast(uint16_t, hv);
+    const uint16_t hv = __builtin_bit_cast(uint16_t, (_Float16)f);
+    const uint16_t qn = (uint16_t)(((rtm::float_to_bits(f) >> 16) & 0x8000u) | 0x7E00u);
+    return f != f ? qn : hv;
 #endif
     uint32_t x = rtm::float_to_bits(f);
     uint32_t sign = (x >> 16) & 0x8000u;
@@ -635,12 +641,12 @@ RT_HD uint16_t rt_f2h(float f) {
 
 RT_HD float rt_h2f(uint16_t h) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    if ((h & 0x7C00u) != 0x7C00u) return (float)__builtin_bit_cast(_Float16, h);  // exact
+    return (float)__builtin_bit_cast(_Float16, h);
 #endif
     uint32_t sign = ((uint32_t)h & 0x8000u) << 16;
     uint32_t e = ((uint32_t)h >> 10) & 0x1Fu;
     uint32_t m = (uint32_t)h & 0x3FFu;
-    if (e == 0x1F) return rtm::bits_to_float(sign | 0x7F800000u | (m << 13));
+    if (e == 0x1F) return rtm::bits_to_float(sign | 0x7F800000u | (m << 13) | (m ? 0x00400000u : 0u));  // NaN quieted
     if (e == 0) {
         if (m == 0) return rtm::bits_to_float(sign);
         // subnormal: m * 2^-24

@@ -45,11 +45,6 @@ constexpr int kDnBatch = RTX_DN_BATCH;  // SpatialFilterGlobal5x5 taps per load 
 #else
 #define DN5_BOUNDS __launch_bounds__(256)
 #endif
-#ifndef RTX_DN7_UNROLL
-#define RTX_DN7_UNROLL 6
-#endif
-#define DN_PRAGMA(x) _Pragma(#x)
-#define DN_UNROLL(n) DN_PRAGMA(unroll n)
 #ifdef RTX_ABL_DN_GATEALL
 constexpr bool kDnGateAll = true;
 #else
@@ -428,26 +423,39 @@ RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const u
     if (!isnan3(cV) && dV < kRayMaxF) {
         F3 sum = f3(0.0f);
         float sw = 0.0f;
-DN_UNROLL(RTX_DN7_UNROLL)
-        for (int i = 0; i < 24; ++i) {
-            const int j = kParity + 2 * i;  // P.frameNum % 2 + 2i
-            const int xo = j % 7, yo = j / 7;
-            const int li = (tx + xo) + (ty + yo) * 22;
-            const uint2 q = sC[li];
-            F3 cc = rgb_of(q);
-            float d = sD[li];
-            F3 n = rgb_of(sN[li]);
-            if (isnan3(cc)) cc = f3(0.0f);
-            if (d != d) d = 0.0f;
-            if (isnan3(n)) n = f3(0.0f);
-            float w = 1.0f;
-            w *= DN_POW(fmaxf(dot(nV, n), 0.0001f), P.dn.local_denoise_sigma_normal);
-            const float dd = (dV - d) / P.dn.local_denoise_sigma_depth;
-            w *= DN_EXP(-0.5f * dd * dd);
-            w *= (mV != mask_of(q)) ? 1.0f / P.dn.local_denoise_sigma_material : 1.0f;
-            w *= cG7[xo + yo * 7];
-            sum = sum + cc * w;
-            sw += w;
+        // LDS reads in batches of six taps (as k_spatial5's loads)
+#pragma unroll
+        for (int i0 = 0; i0 < 24; i0 += 6) {
+            uint2 qv[6], nq[6];
+            float dv[6];
+#pragma unroll
+            for (int m = 0; m < 6; ++m) {
+                const int j = kParity + 2 * (i0 + m);  // P.frameNum % 2 + 2i
+                const int li = (tx + j % 7) + (ty + j / 7) * 22;
+                qv[m] = sC[li];
+                dv[m] = sD[li];
+                nq[m] = sN[li];
+            }
+#pragma unroll
+            for (int m = 0; m < 6; ++m) {
+                const int j = kParity + 2 * (i0 + m);
+                const int xo = j % 7, yo = j / 7;
+                const uint2 q = qv[m];
+                F3 cc = rgb_of(q);
+                float d = dv[m];
+                F3 n = rgb_of(nq[m]);
+                if (isnan3(cc)) cc = f3(0.0f);
+                if (d != d) d = 0.0f;
+                if (isnan3(n)) n = f3(0.0f);
+                float w = 1.0f;
+                w *= DN_POW(fmaxf(dot(nV, n), 0.0001f), P.dn.local_denoise_sigma_normal);
+                const float dd = (dV - d) / P.dn.local_denoise_sigma_depth;
+                w *= DN_EXP(-0.5f * dd * dd);
+                w *= (mV != mask_of(q)) ? 1.0f / P.dn.local_denoise_sigma_material : 1.0f;
+                w *= cG7[xo + yo * 7];
+                sum = sum + cc * w;
+                sw += w;
+            }
         }
         if (isnan3(sum)) sum = f3(0.0f);
         if (sw != sw) sw = 0.0f;

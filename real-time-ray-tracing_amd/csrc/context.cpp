@@ -550,6 +550,8 @@ int rt_build_bvh(rt_context* ctx) {
     if (!ctx) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_build_bvh before rt_init"; return RT_ERR_STATE; }
     hipStream_t stream = ctx->stream;
+    ctx->bvhPrebuilt = false;  // an explicit build supersedes a synchronous draw's prebuild
+    if (!ctx->postStream) ctx->buildOnSide[ctx->bvhSet] = false;
     if (ctx->postStream) {  // frame pipelining: build into the other set, on the side stream
         const int k = ctx->bvhSet ^ 1;
         if (ctx->bvhInFlight[k]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->sideStream, ctx->bvhFree[k], 0));
@@ -586,7 +588,7 @@ int rt_build_bvh(rt_context* ctx) {
 
 // a context-stream user of the current LBVH waits for its build on the side stream
 int wait_bvh(rt_context* ctx) {
-    if (ctx->postStream && ctx->buildOnSide[ctx->bvhSet])
+    if (ctx->buildOnSide[ctx->bvhSet])
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->buildDone[ctx->bvhSet], 0));
     return RT_OK;
 }

@@ -186,6 +186,7 @@ struct rt_context {
     bool bvhInFlight[2] = {false, false}, buildOnSide[2] = {false, false};
     BvhBufs bvh[2];
     int bvhSet = 0;
+    bool bvhPrebuilt = false;  // synchronous draws: the next frame's LBVH is being built into set bvhSet ^ 1
     // frame pipelining: rt_denoise_post(f) is enqueued on the post stream only once the next
     // path trace has enqueued kernel `overlapAfter` (so it fills the trace stages' idle tails), or
     // at the next host read / denoise call, whichever comes first
@@ -253,6 +254,7 @@ int dalloc(rt_context* ctx, T** p, size_t bytes) {
     return rc;
 }
 int rt_create_stream(rt_context* ctx, hipStream_t* s, bool high);  // context.cpp: renderer streams
+extern "C" int ensure_bvh_pair(rt_context* ctx);  // frame.cpp: second LBVH set, side stream, build events
 int rt_frame_init(rt_context* ctx);  // frame.cpp: sky tables, textures, G-buffers
 int sync_streams(rt_context* ctx);   // frame.cpp: context, post and side streams
 bool strip_local_denoise(const rt_context* ctx, uint32_t& a, uint32_t& b);  // frame.cpp: next denoise's rows

@@ -812,6 +812,32 @@ int copy_rgba_out(rt_context* ctx, void* dst) {
 }
 
 namespace {
+// Synchronous draws: the next frame's LBVH rebuild (BuildBvhLevel1/2, one per frame as in the
+// reference) goes into the other set on the side stream, where it runs beside this frame's
+// denoise instead of ahead of the next frame's path trace.  The geometry is fixed after rt_init,
+// so the build depends on nothing this frame computes; the other set was last read by the
+// previous frame, which has finished.
+int prebuild_next_bvh(rt_context* ctx) {
+    int rc;
+    if ((rc = ensure_bvh_pair(ctx)) != RT_OK) return rc;
+    const int cur = ctx->bvhSet;
+    bvh_select(ctx, cur ^ 1);
+    hipStream_t keep = ctx->stream;  // no post stream: rt_build_bvh builds on ctx->stream
+    ctx->stream = ctx->sideStream;
+    rc = rt_build_bvh(ctx);
+    ctx->stream = keep;
+    if (rc == RT_OK) {
+        if (hipEventRecord(ctx->buildDone[cur ^ 1], ctx->sideStream) != hipSuccess) {
+            ctx->err = "hipEventRecord (LBVH prebuild)";
+            rc = RT_ERR_HIP;
+        }
+        ctx->buildOnSide[cur ^ 1] = true;
+    }
+    bvh_select(ctx, cur);
+    ctx->bvhPrebuilt = rc == RT_OK;
+    return rc;
+}
+
 // UpdateFrame (kernel.cu:61-137) + BuildBvhLevel1/2 + PathTrace + TemporalSpatialDenoising +
 // PostProcessing + CopyToOutput of one frame, enqueued (draw, kernel.cu:259-398); the RGBA8 image
 // goes to `target` (pitch in pixels) or, when NULL, to the context's own buffer
@@ -823,8 +849,14 @@ int enqueue_frame(rt_context* ctx, uint32_t* target, uint32_t pitch, bool hdr) {
     if (ctx->useDynamicResolution && frame > 1 && ctx->fullFrame) update_dynamic_resolution(ctx, dt);
     rt_input_control_update(ctx, dt);  // UpdateFrame's InputControlUpdate (kernel.cu:117)
     ctx->fr.drawDt = dt;
-    if ((rc = rt_build_bvh(ctx)) != RT_OK) return rc;
+    if (ctx->bvhPrebuilt && !ctx->postStream) {  // built beside the previous synchronous frame
+        ctx->bvhPrebuilt = false;
+        bvh_select(ctx, ctx->bvhSet ^ 1);  // the path trace waits for its build (wait_bvh)
+    } else if ((rc = rt_build_bvh(ctx)) != RT_OK) {
+        return rc;
+    }
     if ((rc = rt_path_trace(ctx, frame, 0)) != RT_OK) return rc;
+    if (!ctx->postStream && (rc = prebuild_next_bvh(ctx)) != RT_OK) return rc;
     ctx->fr.drawTarget = target;
     ctx->fr.drawPitch = pitch;
     rc = rt_denoise_post(ctx, frame, hdr ? 1 : 0);
@@ -907,6 +939,39 @@ int rt_set_gather_stream(rt_context* ctx, void* stream) {
     return RT_OK;
 }
 
+// The second LBVH set, the side stream and the build events: frame f+1's build beside frame f
+// (pipelined frames, and the prebuild of synchronous draws)
+int ensure_bvh_pair(rt_context* ctx) {
+    int rc;
+#define ALLOC(p, bytes) if (!(p) && (rc = dalloc(ctx, &(p), (bytes))) != RT_OK) return rc
+    {
+        const size_t NP = ctx->mesh.triCountPadded, B = ctx->B;
+        BvhBufs& b = ctx->bvh[1];
+        ALLOC(b.triPos, NP * 48);
+        ALLOC(b.triNrm, NP * 48);
+        ALLOC(b.aabbs, NP * 24);
+        ALLOC(b.batchScene, B * 24);
+        ALLOC(b.morton, B * 4096);
+        ALLOC(b.reorder, B * 4096);
+        ALLOC(b.nodes, B * 1024 * 64);
+        ALLOC(b.tlasAabbs, B * 24);
+        ALLOC(b.tlasScene, 24);
+        ALLOC(b.tlasMorton, 4096);
+        ALLOC(b.tlasReorder, 4096);
+        ALLOC(b.tlasNodes, B * 64);
+        if (!b.counter) {
+            ALLOC(b.counter, 64);
+            HIP_TRY(ctx, hipMemset(b.counter, 0, 64));
+        }
+    }
+#undef ALLOC
+    // lowest priority: it should fill what the trace chain leaves idle
+    if (!ctx->sideStream && (rc = rt_create_stream(ctx, &ctx->sideStream, false)) != RT_OK) return rc;
+    for (hipEvent_t* e : {&ctx->buildDone[0], &ctx->buildDone[1], &ctx->bvhFree[0], &ctx->bvhFree[1]})
+        if (!*e) HIP_TRY(ctx, hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return RT_OK;
+}
+
 int rt_set_post_stream(rt_context* ctx, void* stream) {
     if (!ctx) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_set_post_stream before rt_init"; return RT_ERR_STATE; }
@@ -934,31 +999,8 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
         ALLOC(fr.camSurface[k], strip * 4);
         ALLOC(fr.camCount[k], kWsCounterWords * 4);
     }
-    {  // second LBVH set: frame f+1's build and camera rays beside frame f's traces
-        const size_t NP = ctx->mesh.triCountPadded, B = ctx->B;
-        BvhBufs& b = ctx->bvh[1];
-        ALLOC(b.triPos, NP * 48);
-        ALLOC(b.triNrm, NP * 48);
-        ALLOC(b.aabbs, NP * 24);
-        ALLOC(b.batchScene, B * 24);
-        ALLOC(b.morton, B * 4096);
-        ALLOC(b.reorder, B * 4096);
-        ALLOC(b.nodes, B * 1024 * 64);
-        ALLOC(b.tlasAabbs, B * 24);
-        ALLOC(b.tlasScene, 24);
-        ALLOC(b.tlasMorton, 4096);
-        ALLOC(b.tlasReorder, 4096);
-        ALLOC(b.tlasNodes, B * 64);
-        if (!b.counter) {
-            ALLOC(b.counter, 64);
-            HIP_TRY(ctx, hipMemset(b.counter, 0, 64));
-        }
-    }
 #undef ALLOC
-    // lowest priority: it should fill what the trace chain leaves idle
-    if (!ctx->sideStream && (rc = rt_create_stream(ctx, &ctx->sideStream, false)) != RT_OK) return rc;
-    for (hipEvent_t* e : {&ctx->buildDone[0], &ctx->buildDone[1], &ctx->bvhFree[0], &ctx->bvhFree[1]})
-        if (!*e) HIP_TRY(ctx, hipEventCreateWithFlags(e, hipEventDisableTiming));
+    if ((rc = ensure_bvh_pair(ctx)) != RT_OK) return rc;
     for (int k = 0; k < kGbSets; ++k) {
         if (!ctx->camDone[k]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->camDone[k], hipEventDisableTiming));
         if (!ctx->restDone[k]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->restDone[k], hipEventDisableTiming));

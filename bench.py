@@ -378,6 +378,22 @@ def extras_child(args):
         sk = {("k_pt_chain" if i == 2 else k): v for i, (k, v) in enumerate(sk.items()) if not 3 <= i <= 5}
     out["serial_kernels_ms"] = {k: round(v, 5) for k, v in sk.items()}
     out["serial_kernels_ms"]["sum"] = round(sum(sk.values()), 5)
+    # the roofline of the path rt_draw runs (serial frames): the detail launch's work counters over
+    # the serial kernel times; the fused chain carries the bytes of the four stages it runs
+    sr.path_trace(4, detail=True)
+    sq = sr.download("PT_QUEUE", np.uint32).copy()
+    stages = ("k_trace_queue<3>", "k_pt_resume<3>", "k_trace_queue<4>", "k_pt_resume<4>")
+    full = kernel_roofline(sq, W, H, S, {k: 1.0 for k in ("k_pt_camera", "k_pt_shade0", "k_pt_resolve") + stages},
+                           None, False)
+    ser = {}
+    for k, ms in sk.items():
+        b = sum(full[j]["algorithmic_bytes"] for j in stages) if k == "k_pt_chain" else full[k]["algorithmic_bytes"]
+        a = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        ser[k] = {"ms": round(ms, 5), "algorithmic_bytes": int(b), "achieved_GBs": round(a, 1),
+                  "frac_l2": round(a / L2_PEAK_GBS, 4)}
+    out["serial_roofline"] = {"kernels": ser, "peak": L2_PEAK_GBS, "unit": "GB/s",
+                              "kernel": max(ser, key=lambda k: ser[k]["ms"]),
+                              "timing": "HIP events around each kernel of 20 serial frames (rt_time_path_trace_kernels)"}
     sr.cleanup()
     # the reference host's entry point, RayTracer::draw(SurfObj*) (kernel.cu:259): rt_draw_device into
     # a caller-owned device RGBA8 target, synchronous and asynchronous (RT_DRAW_ASYNC)

@@ -155,6 +155,16 @@ extern "C" float orc_rtmath(int fn, float x, float y) {
     }
 }
 
+// the half conversions of the G-buffers and denoise buffers (rtmath.h rt_f2h / rt_h2f, host
+// integer restatements), over arrays: tests/test_gpu_half.py checks the GPU's hardware conversions
+// against them
+extern "C" void orc_f2h_n(const float* f, uint16_t* h, size_t n) {
+    for (size_t i = 0; i < n; ++i) h[i] = rt_f2h(f[i]);
+}
+extern "C" void orc_h2f_n(const uint16_t* h, float* f, size_t n) {
+    for (size_t i = 0; i < n; ++i) f[i] = rt_h2f(h[i]);
+}
+
 // UpdateFrame's dynamic resolution (kernel.cu:77-100), restated: outside the targetFps +-2 band
 // the width is scaled (int *= float) by sqrt(target frame time / dt); it is then snapped to the
 // nearest multiple of 16 (ties of 8 round up), clamped by clampi to [minW, maxW], and the height

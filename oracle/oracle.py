@@ -87,6 +87,10 @@ def lib() -> C.CDLL:
         L.orc_bluenoise.restype = C.c_float
         L.orc_rtmath.argtypes = [C.c_int, C.c_float, C.c_float]
         L.orc_rtmath.restype = C.c_float
+        L.orc_f2h_n.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.orc_f2h_n.restype = None
+        L.orc_h2f_n.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.orc_h2f_n.restype = None
         L.orc_scene_generate.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                          C.POINTER(C.c_uint32)]
         L.orc_scene_generate.restype = C.c_int
@@ -185,6 +189,22 @@ RTMATH = dict(sin=0, cos=1, tan=2, atan=3, atan2=4, acos=5, asin=6, exp=7, exp2=
 
 def rtmath(fn: str, x: float, y: float = 0.0) -> float:
     return lib().orc_rtmath(RTMATH[fn], x, y)
+
+
+def f2h(f: np.ndarray) -> np.ndarray:
+    """rt_f2h over a float32 array: uint16 bit patterns (round to nearest even, NaN -> sign|0x7E00)."""
+    f = np.ascontiguousarray(f, np.float32)
+    h = np.empty(f.shape, np.uint16)
+    lib().orc_f2h_n(f.ctypes.data, h.ctypes.data, f.size)
+    return h
+
+
+def h2f(h: np.ndarray) -> np.ndarray:
+    """rt_h2f over a uint16 array of half bit patterns: float32 (exact; NaN quieted, payload kept)."""
+    h = np.ascontiguousarray(h, np.uint16)
+    f = np.empty(h.shape, np.float32)
+    lib().orc_h2f_n(h.ctypes.data, f.ctypes.data, h.size)
+    return f
 
 
 # ---------------------------------------------------------------- sky (oracle/sky.cpp)

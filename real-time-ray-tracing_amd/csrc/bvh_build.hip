@@ -291,6 +291,14 @@ RT_DEV void tlas_wave(Lds& s, const BvhBuildParams& P, uint32_t B) {
 
 }  // namespace
 
+// t through a VALU move the compiler cannot see through, so an LDS slot address derived from it is
+// recomputed where it is used instead of being kept (and spilled) from an earlier use
+RT_DEV int opaque_lane(int t) {
+    int r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(t));
+    return r;
+}
+
 __global__ __launch_bounds__(kT, 8) void k_build_bvh(BvhBuildParams P) {  // 8 waves/SIMD = 2 workgroups per CU: <= 64 VGPRs
     __shared__ Lds s;
     const int t = threadIdx.x;
@@ -299,7 +307,6 @@ __global__ __launch_bounds__(kT, 8) void k_build_bvh(BvhBuildParams P) {  // 8 w
     const uint32_t start = b * kT;
     const uint32_t cnt = (b + 1 < B) ? (uint32_t)kT : P.triCount - (B - 1) * kT;  // init.cu:129-130
     const uint32_t active = (((cnt - 1) >> 2) + 1) << 2;  // triangles of threads with tid*4 <= cnt-1
-    s.arrive[t] = 0u;
 
     // ---- gather triangles, leaf boxes, centroids (updateGeometry.cuh:104-184)
     Box bx = box_empty();
@@ -334,6 +341,10 @@ __global__ __launch_bounds__(kT, 8) void k_build_bvh(BvhBuildParams P) {  // 8 w
     if (t == 0) store_box(P.batchSceneAabbs + 6 * (size_t)b, scene);
 
     Node* const nodes = (Node*)P.nodes;
+    // the refit's arrival counters, zeroed here (the sort's barriers order it before the refit)
+    // rather than at entry: the slot address would otherwise stay live across the gather, and at
+    // the 64-VGPR bound it was spilled to scratch
+    s.arrive[opaque_lane(t)] = 0u;
     sort_and_build(s, (int)cnt, P.morton + start, P.reorder + start, nodes + start);
 
     // ---- arrival: the last workgroup builds the TLAS
@@ -362,7 +373,7 @@ __global__ __launch_bounds__(kT, 8) void k_build_bvh(BvhBuildParams P) {  // 8 w
 #endif
 
     // ---- TLAS (UpdateTLAS, updateGeometry.cuh:264-364; then sort + Karras over B keys)
-    s.arrive[t] = 0u;
+    s.arrive[opaque_lane(t)] = 0u;
     Box rb = box_empty();
     F3 rc = f3(0.0f);
     if ((uint32_t)t < B) {

@@ -38,6 +38,31 @@ RT_HD double d_inf() { return bits_to_double(0x7FF0000000000000ull); }
 RT_HD double d_nan() { return bits_to_double(0x7FF8000000000000ull); }
 RT_HD double d_abs(double x) { return bits_to_double(double_to_bits(x) & 0x7FFFFFFFFFFFFFFFull); }
 
+// pi/2 in double.  On the device it is materialised where it is used: as a plain constant the
+// compiler hoists it into a VGPR pair for the whole kernel (it serves only the rare double
+// paths below), and in the register-bound path-trace kernels that pair was spilled to scratch.
+RT_HD double d_pio2() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t lo, hi;
+    asm volatile("v_mov_b32 %0, 0x54442d18" : "=v"(lo));
+    asm volatile("v_mov_b32 %0, 0x3ff921fb" : "=v"(hi));
+    return bits_to_double(((uint64_t)hi << 32) | lo);
+#else
+    return 1.57079632679489661923;
+#endif
+}
+
+RT_HD double d_pi() {  // pi in double, materialised at its use on the device like d_pio2
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t lo, hi;
+    asm volatile("v_mov_b32 %0, 0x54442d18" : "=v"(lo));
+    asm volatile("v_mov_b32 %0, 0x400921fb" : "=v"(hi));
+    return bits_to_double(((uint64_t)hi << 32) | lo);
+#else
+    return 3.14159265358979323846;
+#endif
+}
+
 // round-half-away for the reduction index; exact for |x| < 2^52
 RT_HD double d_round(double x) {
     double a = d_abs(x);
@@ -187,32 +212,31 @@ RT_HD double atan_pos(double x) {
     p = d_mad(p, x2, 1.0);
     double a = x * p;
     if (shift) a = 0.52359877559829887308 + a;
-    if (inv) a = 1.57079632679489661923 - a;
+    if (inv) a = d_pio2() - a;
     return a;
 }
 
 RT_HD double atand(double x) {
     if (d_isnan(x)) return x;
-    if (x == d_inf()) return 1.57079632679489661923;
-    if (x == -d_inf()) return -1.57079632679489661923;
+    if (x == d_inf()) return d_pio2();
+    if (x == -d_inf()) return -d_pio2();
     return x < 0 ? -atan_pos(-x) : atan_pos(x);
 }
 
 RT_HD double atan2d(double y, double x) {
     if (d_isnan(x) || d_isnan(y)) return d_nan();
-    const double pi = 3.14159265358979323846;
     bool yneg = (double_to_bits(y) >> 63) != 0;
     bool xneg = (double_to_bits(x) >> 63) != 0;
     double ay = d_abs(y), ax = d_abs(x);
     double r;
-    if (ay == 0.0) r = xneg ? pi : 0.0;
-    else if (ax == 0.0) r = pi * 0.5;
-    else if (ax == d_inf() && ay == d_inf()) r = xneg ? pi * 0.75 : pi * 0.25;
-    else if (ax == d_inf()) r = xneg ? pi : 0.0;
-    else if (ay == d_inf()) r = pi * 0.5;
+    if (ay == 0.0) r = xneg ? d_pi() : 0.0;
+    else if (ax == 0.0) r = d_pio2();
+    else if (ax == d_inf() && ay == d_inf()) r = xneg ? d_pi() * 0.75 : d_pi() * 0.25;
+    else if (ax == d_inf()) r = xneg ? d_pi() : 0.0;
+    else if (ay == d_inf()) r = d_pio2();
     else {
         double a = atan_pos(ay / ax);
-        r = xneg ? pi - a : a;
+        r = xneg ? d_pi() - a : a;
     }
     return yneg ? -r : r;
 }
@@ -261,24 +285,23 @@ RT_HD double atan_ratio(double num, double den) {
     // atan(i / 8), i = 0..8
     const double kAtan8[9] = {0.0, 0.12435499454676144, 0.24497866312686414, 0.35877067027057225, 0.4636476090008061, 0.5585993153435624, 0.6435011087932844, 0.7188299996216245, 0.7853981633974483};
     const double r = kAtan8[i] + at;
-    return swap ? 1.57079632679489661923 - r : r;
+    return swap ? d_pio2() - r : r;
 }
 
 RT_HD double atan2f_core(double y, double x) {
     if (d_isnan(x) || d_isnan(y)) return d_nan();
-    const double pi = 3.14159265358979323846;
     const bool yneg = (double_to_bits(y) >> 63) != 0;
     const bool xneg = (double_to_bits(x) >> 63) != 0;
     const double ay = d_abs(y), ax = d_abs(x);
     double r;
-    if (ay == 0.0) r = xneg ? pi : 0.0;
-    else if (ax == 0.0) r = pi * 0.5;
-    else if (ax == d_inf() && ay == d_inf()) r = xneg ? pi * 0.75 : pi * 0.25;
-    else if (ax == d_inf()) r = xneg ? pi : 0.0;
-    else if (ay == d_inf()) r = pi * 0.5;
+    if (ay == 0.0) r = xneg ? d_pi() : 0.0;
+    else if (ax == 0.0) r = d_pio2();
+    else if (ax == d_inf() && ay == d_inf()) r = xneg ? d_pi() * 0.75 : d_pi() * 0.25;
+    else if (ax == d_inf()) r = xneg ? d_pi() : 0.0;
+    else if (ay == d_inf()) r = d_pio2();
     else {
         const double a = atan_ratio(ay, ax);
-        r = xneg ? pi - a : a;
+        r = xneg ? d_pi() - a : a;
     }
     return yneg ? -r : r;
 }

@@ -114,6 +114,40 @@ def test_pathtrace_bit_exact(rtx, oracle, tmp_path, default_scene, sky_tex, w, h
         assert (o["color"][:, 3] == 3).mean() > 0.3  # material 3 (Lambertian) on the terrain
 
 
+@pytest.mark.parametrize("dist", [1e3, 1e4, 1e5])
+def test_pathtrace_distant_camera_cull(rtx, oracle, tmp_path, default_scene, sky_tex, dist):
+    """The camera kernel's scene cull (`root_surely_missed`, a slab test of the root box grown by
+    0.01 + 1 % of the scene extent) far from the scene: a narrow field of view from 10^3 .. 10^5
+    units away keeps the terrain in the image, so culled and traced rays sit side by side, and the
+    G-buffers stay bit-exact with the oracle, which traces every ray."""
+    import math
+    s, tex = sky_tex
+    w, h = 96, 54
+    centre = np.array([8.0, 8.0, 8.0])  # the default scene spans [-0.5, 16.5] x [5, 11] x [-0.5, 16.5]
+    off = np.array([0.6, 0.35, -0.72])
+    off /= np.linalg.norm(off)
+    pos = centre + dist * off
+    d = -off
+    ocam, rcam = terrain_camera(rtx, oracle, w, h, pos=tuple(np.float32(pos)), yaw=float(np.float32(math.atan2(d[0], d[2]))),
+                                pitch=float(np.float32(math.asin(d[1]))))
+    fov = np.float32(2.0 * math.atan(9.0 / dist))
+    ocam.fovX = fov
+    rcam.fovX = fov
+    rt = make_rt(rtx, tmp_path, w, h)
+    rt.camera = rcam
+    rt.path_trace(1, detail=True)
+    rt.sync()
+    g = gpu_gbuffers(rt, w, h)
+    culled = int(rt.download("PT_QUEUE", np.uint32)[22])
+    rt.cleanup()
+    o = oracle.pathtrace(default_scene["bvh"], w, h, frame_num=1, cam=ocam, sky_out=s, tex=tex)
+    assert_gbuffers_equal(g, o)
+    surface = (o["depth"] != 0x7C00).mean()  # sky depth: half infinity
+    assert 0 < culled < w * h, culled  # both the culled and the traversed branch ran
+    if dist <= 1e4:  # (at 10^5 the traversed rays miss the terrain, on both sides alike)
+        assert 0.05 < surface < 0.95, surface
+
+
 def test_pathtrace_motion_vectors(rtx, oracle, tmp_path, default_scene, sky_tex):
     """Frame 2 after a camera move: motion vectors come from the frame-1 (history) camera."""
     s, tex = sky_tex

@@ -55,6 +55,7 @@ struct FrameResources {
     float* scanSums = nullptr;
     float* skyTree = nullptr;   // light-CDF probe heaps (kSkyTreeNodes / kSunTreeNodes)
     float* sunTree = nullptr;
+    float* lightSel = nullptr;   // [4] SampleLight's per-frame terms (k_light_select)
     bool skyValid = false;
     rt_sky_params lastSky{};
     float sunDir[3] = {0, 1, 0};

@@ -148,6 +148,7 @@ int update_sky(rt_context* ctx) {
     p.scanSums = fr.scanSums;
     p.skyTree = fr.skyTree;
     p.sunTree = fr.sunTree;
+    p.lightSel = fr.lightSel;
     HIP_TRY(ctx, rtk_launch_sky(&p, ctx->stream));
     if (ctx->postStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // before the side stream's camera rays
     fr.sunArea = rt_powf(rt_tanf(sunRadius), 2.0f) * kPi;
@@ -359,6 +360,7 @@ int rt_frame_init(rt_context* ctx) {
     ALLOC(fr.scanSums, 512 * 4);
     ALLOC(fr.skyTree, (size_t)kSkyTreeNodes * 4);
     ALLOC(fr.sunTree, (size_t)kSunTreeNodes * 4);
+    ALLOC(fr.lightSel, 16);
     ALLOC(fr.texAlbedo, (size_t)kTexTexels * 8);
     ALLOC(fr.texNormal, (size_t)kTexTexels * 8);
     ALLOC(fr.texHeight, (size_t)kTexTexels * 2);
@@ -571,8 +573,10 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.sunCdf = fr.sunCdf;
     p.skyTree = fr.skyTree;
     p.sunTree = fr.sunTree;
+    p.lightSel = fr.lightSel;
     memcpy(p.sunDir, fr.sunDir, 12);
     p.cosThetaMax = fr.cosThetaMax;
+    p.oneMinusCosThetaMax = 1.0f - fr.cosThetaMax;
     sun_frame(fr.sunDir, p.sunT, p.sunB);
     p.colorOut = fr.color;
     p.normalOut = fr.normal;

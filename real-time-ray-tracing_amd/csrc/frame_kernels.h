@@ -44,6 +44,7 @@ struct SkyGenParams {
     float* scanSums;      // [>= 512] block totals
     float* skyTree;       // [kSkyTreeNodes] bisection probe tree of skyCdf (cdf_tree)
     float* sunTree;       // [kSunTreeNodes] of sunCdf
+    float* lightSel;      // [4] SampleLight's per-frame terms: pSky, maxSky, maxSun, 2 pi (1 - cosThetaMax)
 };
 
 // The first levels of SampleLight's CDF bisection (light.cuh:9-31) as a heap: node 1 holds the
@@ -142,9 +143,11 @@ struct PathTraceParams {
     const float* sunCdf;
     const float* skyTree;       // [kSkyTreeNodes] (SkyGenParams::skyTree)
     const float* sunTree;       // [kSunTreeNodes]
+    const float* lightSel;      // [4] (SkyGenParams::lightSel): uniform loads instead of per-sample math
     float sunDir[3];
     float sunT[3], sunB[3];     // LocalizeSample(sunDir) frame (sky.cuh:64-87), evaluated once on the host
     float cosThetaMax;
+    float oneMinusCosThetaMax;  // 1 - cosThetaMax (exact on the host): a kernel argument
     uint2* colorOut;            // [W*H] half3 demodulated colour + ushort material mask
     uint2* normalOut;           // [W*H] half4
     uint2* albedoOut;           // [W*H] half4

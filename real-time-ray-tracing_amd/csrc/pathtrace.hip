@@ -343,16 +343,20 @@ RT_DEV void wave_add(uint32_t v, uint32_t* dst) {
     if (__lane_id() == 0 && v) atomicAdd(dst, v);
 }
 
+// set bits of the wave mask m below this lane (v_mbcnt: no per-lane 64-bit mask kept live)
+RT_DEV uint32_t lane_rank(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // wave-aggregated append: one atomic per wave, slots in lane order
 RT_DEV uint32_t wave_append(bool want, uint32_t* counter) {
     const unsigned long long m = __ballot(want);
     if (m == 0ull) return 0u;
-    const int lane = (int)__lane_id();
     const int leader = __ffsll((long long)m) - 1;
     uint32_t base = 0u;
-    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    if ((int)__lane_id() == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
     base = __shfl(base, leader);
-    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    return base + lane_rank(m);
 }
 
 RT_DEV void enqueue(const PtQueue& q, uint32_t slot, const PathVars& v, uint32_t pixel, uint32_t s) {
@@ -376,16 +380,22 @@ RT_DEV SceneView scene_of(const PathTraceParams& P) {
 }
 
 // workgroup sum of traced rays into the frame counter (one atomic per workgroup)
-RT_DEV void add_rays(const PathTraceParams& P, unsigned long long* wgSlots, uint32_t rays) {
+// w: the calling wave's index in the workgroup (wave-uniform); the lane comes from v_mbcnt, so a
+// caller need not keep threadIdx.x live until its end
+RT_DEV void add_rays(const PathTraceParams& P, unsigned long long* wgSlots, uint32_t rays, int w) {
     if (!P.rayCounter) return;
     unsigned long long r = rays;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
-    const int tid = threadIdx.x;
-    if ((tid & 63) == 0) wgSlots[tid >> 6] = r;
+    const bool lane0 = __lane_id() == 0;
+    if (lane0) wgSlots[w] = r;
     __syncthreads();
     const uint32_t slot = (blockIdx.y * gridDim.x + blockIdx.x) % kRayCounterSlots;
-    if (tid == 0) atomicAdd(&P.rayCounter[slot * kRayCounterStride], wgSlots[0] + wgSlots[1] + wgSlots[2] + wgSlots[3]);
+    if (w == 0 && lane0)
+        atomicAdd(&P.rayCounter[slot * kRayCounterStride], wgSlots[0] + wgSlots[1] + wgSlots[2] + wgSlots[3]);
+}
+RT_DEV void add_rays(const PathTraceParams& P, unsigned long long* wgSlots, uint32_t rays) {
+    add_rays(P, wgSlots, rays, __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6));
 }
 
 // per-sample init of PathTrace (pathtrace.cuh:20-60) and GenerateRay (raygen.cuh:7-38)
@@ -579,6 +589,7 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
     __shared__ __align__(16) float sSkyTree[kSkyTreeNodes];
     __shared__ __align__(16) float sSunTree[kSunTreeNodes];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wS = __builtin_amdgcn_readfirstlane(w);  // for add_rays: threadIdx.x need not live to the end
     bn_stage_sobol(P.bluenoise, sob, tid, 256);
     stage_cdf_trees(P, sSkyTree, sSunTree, tid, 256);
     __syncthreads();
@@ -722,7 +733,7 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
         wave_add(shT, &P.ws.counters[kCntTstShade]);
         wave_add(shD, &P.ws.counters[kCntDiffShade]);
     }
-    add_rays(P, wgRays, raysWg);
+    add_rays(P, wgRays, raysWg, wS);
 }
 
 // Entry i of queue kStep (3 or 4): reloads the sample's state, applies the hit the tracer found
@@ -845,8 +856,8 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
     __shared__ uint2 ranges[4][kChainRanges];
     __shared__ uint32_t q4list[4][64];
     __shared__ unsigned long long wgRays[4];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const unsigned long long ltMask = (1ull << lane) - 1ull;
+    // w: the wave's index, wave-uniform (an SGPR); lane ranks come from v_mbcnt (lane_rank)
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     bn_stage_sobol(P.bluenoise, sob, tid, 256);
     __syncthreads();
     const uint32_t n = P.ws.counters[kCntQ3];
@@ -886,7 +897,7 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
                 const uint32_t avail = f.resHi - f.resLo;
                 const bool none = avail == 0u;  // drained, or the reserve list is full
                 if (!active && !exhausted) {
-                    const uint32_t rank = (uint32_t)__popcll(need & ltMask);
+                    const uint32_t rank = lane_rank(need);
                     if (rank < avail) {
                         idx = f.resLo + rank;
                         const float4 o = q.rayO[idx], d = q.rayD[idx];
@@ -1001,7 +1012,7 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
                 if (i4) {
                     ++c.rays;
                     enqueue(P.ws.q4, slot, v, p, smp);
-                    q4list[w][nq4 + (uint32_t)__popcll(m4 & ltMask)] = slot;
+                    q4list[w][nq4 + lane_rank(m4)] = slot;
                 } else {
                     store_path_L(c, v, p, smp);
                 }
@@ -1020,7 +1031,7 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
         }
         if (f.resLo == f.resHi && f.drained == allParts) break;  // queue 3 drained
     }
-    add_rays(P, wgRays, rays);
+    add_rays(P, wgRays, rays, w);
 }
 
 // colour of the pixels with a deferred sample: the fp32 sample average in sample order

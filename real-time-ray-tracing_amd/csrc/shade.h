@@ -186,7 +186,7 @@ RT_DEV F3 env_light(const PathTraceParams& P, F3 sunDir, F3 rd) {
     const float cosTheta = inner3(sunDir.x, rd.x, sunDir.y, rd.y, sunDir.z, rd.z);
     if (cosTheta < cosMax) return color;
     const F3 c = f3(inner3(P.sunT[0], rd.x, P.sunT[1], rd.y, P.sunT[2], rd.z), cosTheta, 0.0f);
-    const float u = (1.0f - cosTheta) / (1.0f - cosMax);
+    const float u = (1.0f - cosTheta) / P.oneMinusCosThetaMax;  // (1 - cosMax), from the host
     const float sinTheta = __builtin_sqrtf(1.0f - cosTheta * cosTheta);
     if (sinTheta < 1e-5f || (c.x / sinTheta) < -1.0f || (c.x / sinTheta) > 1.0f) return color;
     const float v = rt_acosf(c.x / sinTheta) * kInvTwoPi;
@@ -222,10 +222,8 @@ RT_DEV int cdf_search_tree(const float* a, int right, float target, const float*
 
 RT_DEV void sample_light(const PathTraceParams& P, F3 sunDir, F3& dir, float& pdf, int& lightIdx, float r0, float r1,
                          const float* skyTree, const float* sunTree) {
-    const float maxSky = P.skyCdf[kSkySize - 1], maxSun = P.sunCdf[kSunSize - 1];
-    const float totalSky = maxSky * kTwoPi / kSkySize;
-    const float totalSun = maxSun * kTwoPi * (1.0f - P.cosThetaMax) / kSunSize;
-    const float pSky = totalSky / (totalSky + totalSun);
+    // pSky = totalSky / (totalSky + totalSun) and the CDF totals, per frame (sky.hip k_light_select)
+    const float pSky = P.lightSel[0], maxSky = P.lightSel[1], maxSun = P.lightSel[2], sunDen = P.lightSel[3];
     if (pSky > r1) {
         const int idx = cdf_search_tree(P.skyCdf, kSkySize - 2, r0 * maxSky, skyTree, kSkyTreeNodes) + 1;
         float p = (P.skyCdf[idx] - P.skyCdf[idx - 1]) / maxSky;
@@ -237,7 +235,7 @@ RT_DEV void sample_light(const PathTraceParams& P, F3 sunDir, F3& dir, float& pd
     } else {
         const int idx = cdf_search_tree(P.sunCdf, kSunSize - 2, r0 * maxSun, sunTree, kSunTreeNodes) + 1;
         float p = (P.sunCdf[idx] - P.sunCdf[idx - 1]) / maxSun;
-        p = p * kSunSize / (kTwoPi * (1.0f - P.cosThetaMax));
+        p = p * kSunSize / sunDen;  // kTwoPi * (1 - cosThetaMax)
         const float u = ((float)(idx % kSunW) + 0.5f) / kSunW;
         const float v = ((float)(idx / kSunW) + 0.5f) / kSunH;
         dir = equal_area_map_cone(sunDir, f3(P.sunT[0], P.sunT[1], P.sunT[2]), f3(P.sunB[0], P.sunB[1], P.sunB[2]), u,

@@ -212,6 +212,19 @@ __global__ void k_cdf_tree(const float* cdf, int right0, float* tree, int nodes)
     tree[j] = live ? cdf[(left + right) / 2] : __builtin_nanf("");
 }
 
+// SampleLight's terms that depend only on the frame's light tables (shade.h sample_light), in its
+// operation order: pSky = totalSky / (totalSky + totalSun), the CDF totals, and the sun's
+// 2 pi (1 - cosThetaMax); the shading kernels read them as uniform loads
+__global__ void k_light_select(const float* skyCdf, const float* sunCdf, float cosThetaMax, float* out) {
+    const float maxSky = skyCdf[kSkySize - 1], maxSun = sunCdf[kSunSize - 1];
+    const float totalSky = maxSky * kTwoPi / kSkySize;
+    const float totalSun = maxSun * kTwoPi * (1.0f - cosThetaMax) / kSunSize;
+    out[0] = totalSky / (totalSky + totalSun);
+    out[1] = maxSky;
+    out[2] = maxSun;
+    out[3] = kTwoPi * (1.0f - cosThetaMax);
+}
+
 extern "C" hipError_t rtk_launch_sky(const SkyGenParams* p, hipStream_t stream) {
     hipLaunchKernelGGL(k_sky, dim3(kSkySize / 256), dim3(256), 0, stream, *p);
     hipError_t e = rtk_launch_scan(p->skyPdf, p->skyCdf, p->scanSums, kSkySize, kSkyScanBlock, stream);
@@ -223,5 +236,7 @@ extern "C" hipError_t rtk_launch_sky(const SkyGenParams* p, hipStream_t stream) 
                        p->skyTree, kSkyTreeNodes);
     hipLaunchKernelGGL(k_cdf_tree, dim3(kSunTreeNodes / 256), dim3(256), 0, stream, p->sunCdf, kSunSize - 2,
                        p->sunTree, kSunTreeNodes);
+    hipLaunchKernelGGL(k_light_select, dim3(1), dim3(1), 0, stream, (const float*)p->skyCdf, (const float*)p->sunCdf,
+                       p->cosThetaMax, p->lightSel);
     return hipGetLastError();
 }

@@ -564,10 +564,15 @@ def main():
         r_ = fp.denoise.bytes_per_frame() if fp.denoise else 0
         result["comm_bytes_per_rank_per_frame"] = {"gbuffer_rows": int(g), "denoise_rows": int(r_),
                                                    "gbuffer_allgather_would_be": int(fp.gather.bytes_per_frame())}
-    # the other kernels: the same split over 20 pipelined frames right after (every kernel marked)
-    split = rt.time_frame_kernels(last + 2, 20)
-    split_dom = split[dom]
+    # the other kernels: the same split over 20 pipelined frames right after (every kernel marked).
+    # One GPU only: rt_time_frame_kernels runs frames without FramePipeline's row exchanges, so on
+    # a rank of N > 1 its denoise would read stale peer rows; ranks report the timed kernel alone.
     timed_dom = (kernels_ms or {}).get(dom)
+    if world == 1:
+        split = rt.time_frame_kernels(last + 2, 20)
+        split_dom = split[dom]
+    else:
+        split, split_dom = {}, None
     if timed_dom is not None:
         split = dict(split, **{dom: timed_dom})
     per = kernel_roofline(counters, W, rows, S, split, pmc, matches)
@@ -596,7 +601,7 @@ def main():
                    "(rt_time_frame_kernels); rocprofv3 --kernel-trace --stats of this command: "
                    "profiles/r03_kernel_stats.csv (this process: warm-up, timed, 1 detail and the 20 split frames)"
                    % (dom, marked, args.warmup)),
-        "kernel_ms_split_frames": round(split_dom, 5),
+        "kernel_ms_split_frames": round(split_dom, 5) if split_dom is not None else None,
     }
     rt.cleanup()
 

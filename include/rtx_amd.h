@@ -56,7 +56,7 @@ int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out);
  * caller-owned DEVICE memory (row pitch in bytes, 0 = width * 4; 4-byte aligned).  flags 0: returns
  * when the frame is complete, as the reference's draw does (it ends with a device sync).
  * RT_DRAW_ASYNC: returns once the frame is enqueued; frames are pipelined (the denoise/post of
- * frame f overlaps the trace of f+1 on an internal low-priority stream unless rt_set_post_stream
+ * frame f overlaps the trace of f+1 on an internal stream (low priority under RTX_STREAMS=prio) unless rt_set_post_stream
  * named one) and each frame's target must stay valid until rt_sync (or a later synchronous
  * call) has returned.  rt_download(RT_ARR_RGBA8) reads the last frame's target. */
 #define RT_DRAW_ASYNC 1

@@ -134,6 +134,11 @@ int raw_alloc(rt_context* ctx, void** p, size_t bytes) {
 // its streams having landed on one queue.  A stream created with a CU mask gets a hardware queue
 // of its own, so the renderer's streams use a full mask; they then carry no priority, which
 // measured no difference.  RTX_STREAMS=prio: plain streams with priorities.
+// hipExtStreamCreateWithCUMask makes blocking streams (hipStreamDefault): work on the null stream
+// (a framework's default-stream kernels, synchronous hipMemcpy / hipMemset) and the renderer's
+// streams wait for each other.  The renderer itself issues synchronous copies only outside
+// frames (rt_init, rt_bind_buffer, host reads, the ray-counter reset); a host that keeps default-
+// stream work in flight beside pipelined frames should set RTX_STREAMS=prio (non-blocking streams).
 int rt_create_stream(rt_context* ctx, hipStream_t* s, bool high) {
     static const bool prio = [] {
         const char* v = getenv("RTX_STREAMS");
@@ -368,8 +373,9 @@ int rt_init(rt_context* ctx) {
     }
 
 
-    // the trace chain is a frame's critical path: it outranks the pipelined denoise and the next
-    // frame's camera rays, whose streams are created at the lowest priority
+    // the context stream (the trace chain, a frame's critical path); with RTX_STREAMS=prio it is
+    // created at the highest priority and the side / internal post streams at the lowest, otherwise
+    // all are CU-masked streams without priority (rt_create_stream)
     if (int rc = rt_create_stream(ctx, &ctx->ownStream, true)) return rc;
     ctx->stream = ctx->ownStream;
     HIP_TRY(ctx, hipEventCreate(&ctx->ev0));

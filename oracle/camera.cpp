@@ -6,6 +6,7 @@
 //   GenerateRay / GetRayConeWidth   raygen.cuh:7-63, ConcentricSampleDisk bsdf.cuh:9-34
 //   blue-noise sampler              blueNoiseRandGen.h:113-146 (OPTIMIZED_BLUE_NOISE_SPP 4)
 //   GenerateSmoothNormals x2        kernel.cu:228-257, 313-327
+#include <cstring>
 #include <vector>
 
 #include "oracle.h"
@@ -163,6 +164,33 @@ extern "C" void orc_f2h_n(const float* f, uint16_t* h, size_t n) {
 }
 extern "C" void orc_h2f_n(const uint16_t* h, float* f, size_t n) {
     for (size_t i = 0; i < n; ++i) f[i] = rt_h2f(h[i]);
+}
+
+// rt_unorm16 against the IEEE division it replaces, over every 16-bit value: the count of mismatches
+extern "C" int orc_unorm16_mismatches() {
+    int bad = 0;
+    for (uint32_t x = 0; x < 65536u; ++x) {
+        volatile float d = 65535.0f;  // a real division, not a constant-folded product
+        const float ref = (float)x / d, got = rt_unorm16(x);
+        if (memcmp(&ref, &got, 4) != 0) ++bad;
+    }
+    return bad;
+}
+
+// the shading path's x / d by x * RN(1/d) and one fma correction (pt_common.h div_by_const) against
+// the IEEE division, over every stride-th float bit pattern with finite |x| >= 2^-100: mismatches
+extern "C" long orc_div_const_mismatches(float d, uint32_t stride) {
+    volatile float dv = d;
+    const float c = 1.0f / dv;
+    long bad = 0;
+    for (uint64_t u = 0; u < (1ull << 32); u += stride) {
+        const float x = rtm::bits_to_float((uint32_t)u);
+        const float ax = fabsf(x);
+        if (!(ax >= 0x1p-100f && ax <= 0x1.fffffep127f)) continue;
+        const float q = x * c, got = fmaf(fmaf(-q, d, x), c, q), ref = x / dv;
+        if (memcmp(&ref, &got, 4) != 0) ++bad;
+    }
+    return bad;
 }
 
 // UpdateFrame's dynamic resolution (kernel.cu:77-100), restated: outside the targetFps +-2 band

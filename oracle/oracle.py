@@ -87,6 +87,10 @@ def lib() -> C.CDLL:
         L.orc_bluenoise.restype = C.c_float
         L.orc_rtmath.argtypes = [C.c_int, C.c_float, C.c_float]
         L.orc_rtmath.restype = C.c_float
+        L.orc_div_const_mismatches.argtypes = [C.c_float, C.c_uint32]
+        L.orc_div_const_mismatches.restype = C.c_long
+        L.orc_unorm16_mismatches.argtypes = []
+        L.orc_unorm16_mismatches.restype = C.c_int
         L.orc_f2h_n.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.orc_f2h_n.restype = None
         L.orc_h2f_n.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]

@@ -215,9 +215,9 @@ RT_DEV void diffuse(PathCtx& c, int bounce, RayState& rs, F3& beta) {
     float sPdf = 0.0f;
     if (!kMF || rs.matType == LAMBERTIAN) {
         lambertian_sample(F2{r[0], r[1]}, sDir, normal);
-        sBsdf = albedo / kPi;
-        sPdf = fmx(dot(sDir, normal), kSafeCos) / kPi;
-        lBsdf = albedo / kPi;
+        sBsdf = f3(div_pi(albedo.x), div_pi(albedo.y), div_pi(albedo.z));  // albedo / kPi
+        sPdf = div_pi(fmx(dot(sDir, normal), kSafeCos));
+        lBsdf = sBsdf;  // albedo / kPi
     } else {  // MICROFACET
         const F3 F0 = mat_F0(rs.matId);
         const float alpha = mat_alpha(rs.matId), alpha2 = alpha * alpha;

@@ -44,8 +44,7 @@ struct F4 { float x, y, z, w; };
 RT_DEV F4 load_u16x4(const uint2* tex, uint32_t texel) {
     // a 32-bit byte offset from the (uniform) chain base: one VGPR per address, not two
     const uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(tex) + texel * 8u);
-    return F4{(float)(q.x & 0xFFFFu) / 65535.0f, (float)(q.x >> 16) / 65535.0f, (float)(q.y & 0xFFFFu) / 65535.0f,
-              (float)(q.y >> 16) / 65535.0f};
+    return F4{rt_unorm16(q.x & 0xFFFFu), rt_unorm16(q.x >> 16), rt_unorm16(q.y & 0xFFFFu), rt_unorm16(q.y >> 16)};
 }
 
 // BoundaryFuncRepeat, then the surface read's clamp: v % size for v >= size, size - (-v) % size
@@ -174,7 +173,7 @@ RT_DEV F3 bicubic_env(const float4* buf, F2 uv) {
 RT_DEV F3 env_light(const PathTraceParams& P, F3 sunDir, F3 rd) {
     F3 color;
     {
-        const F2 uv = {rt_atan2f(-rd.z, -rd.x) / kTwoPi + 0.5f, fmx(rd.y, 0.05f)};
+        const F2 uv = {div_two_pi(rt_atan2f(-rd.z, -rd.x)) + 0.5f, fmx(rd.y, 0.05f)};
         const F3 sky = bicubic_env<false>(P.skyBuffer, uv);
         const F3 mist = f3(0.2f);
         const float w = clampf((rd.y + 0.4f) * (1.0f / 0.5f));
@@ -227,7 +226,7 @@ RT_DEV void sample_light(const PathTraceParams& P, F3 sunDir, F3& dir, float& pd
     if (pSky > r1) {
         const int idx = cdf_search_tree(P.skyCdf, kSkySize - 2, r0 * maxSky, skyTree, kSkyTreeNodes) + 1;
         float p = (P.skyCdf[idx] - P.skyCdf[idx - 1]) / maxSky;
-        p = p * kSkySize / kTwoPi;
+        p = div_two_pi(p * kSkySize);
         const float u = ((float)(idx % kSkyW) + 0.5f) / kSkyW;
         const float v = ((float)(idx / kSkyW) + 0.5f) / kSkyH;
         dir = equal_area_map(u, v);

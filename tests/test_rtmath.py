@@ -100,3 +100,16 @@ def test_rtmath_atan2_quadrants_and_ratios(oracle):
         y = np.float32(rng.choice([-1, 1]) * 10.0 ** rng.uniform(-3, 3))
         worst = max(worst, ulp_err(oracle.rtmath("atan2", float(y), float(x)), np.arctan2(np.float64(y), np.float64(x))))
     assert worst <= 1, worst
+
+
+def test_unorm16_equals_division(oracle):
+    """rt_unorm16 (x * RN(1/65535) with one fma correction) is the IEEE quotient x / 65535 for all
+    65,536 texel values: the texture path's conversion is exact, not approximate."""
+    assert oracle.lib().orc_unorm16_mismatches() == 0
+
+
+@pytest.mark.parametrize("d", [np.float32(3.1415926535897932), np.float32(6.2831853071795865)])
+def test_div_by_pi_constants_equal_division(oracle, d):
+    """pt_common.h div_pi / div_two_pi: x * RN(1/d) plus one fma correction is the IEEE quotient x / d
+    for finite |x| >= 2^-100 (tools/div_exhaustive.c checks all 2^32 patterns; here every 4,099th)."""
+    assert oracle.lib().orc_div_const_mismatches(float(d), 4099) == 0

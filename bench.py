@@ -468,8 +468,10 @@ def main():
 
     # warm-up; frames 2..W with every path-trace kernel bracketed by HIP events, which picks the
     # roofline's kernel: the longest on the frame's critical (context) stream (pipelined, the camera
-    # kernel runs on the side stream beside the previous frame's chain)
-    crit = [k for k in rtx.RayTracer.PT_KERNELS if not (pipeline and k == "k_pt_camera")]
+    # kernel, and on one GPU the shade kernel behind it, run on the side stream beside the previous
+    # frame's tracers)
+    side = {"k_pt_camera", "k_pt_shade0"} if pipeline and rt.info().shadeOnSide else {"k_pt_camera"}
+    crit = [k for k in rtx.RayTracer.PT_KERNELS if not (pipeline and k in side)]
     dom = "k_trace_queue<3>"
     if args.warmup >= 2:
         fp.frame(1)

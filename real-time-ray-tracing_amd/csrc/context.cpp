@@ -525,6 +525,7 @@ int rt_get_info(const rt_context* ctx, rt_info* out) {
     out->denoiseRowEnd = (int32_t)b;
     uint32_t sa = 0, sb = 0, lo = 0, hi = (uint32_t)ctx->renderH;
     out->stripLocalDenoise = 0;
+    out->shadeOnSide = ctx->postStream && ctx->shadeOnSide ? 1 : 0;
     if (ctx->inited && strip_local_denoise(ctx, sa, sb)) {
         gbuffer_rows((uint32_t)ctx->renderH, sa, sb, lo, hi);
         out->stripLocalDenoise = 1;
@@ -846,10 +847,10 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
         case RT_ARR_TEX_NORMAL_ROUGHNESS: src = ctx->fr.texNormal; break;
         case RT_ARR_TEX_HEIGHT: src = ctx->fr.texHeight; break;
         case RT_ARR_PT_QUEUE: src = ctx->fr.lastCounters ? ctx->fr.lastCounters : ctx->fr.ws.counters; break;
-        case RT_ARR_PT_Q3_ORIGINS: src = ctx->fr.ws.q3.rayO; break;
-        case RT_ARR_PT_Q3_DIRS: src = ctx->fr.ws.q3.rayD; break;
-        case RT_ARR_PT_Q4_ORIGINS: src = ctx->fr.ws.q4.rayO; break;
-        case RT_ARR_PT_Q4_DIRS: src = ctx->fr.ws.q4.rayD; break;
+        case RT_ARR_PT_Q3_ORIGINS: src = ctx->fr.camQ3[ctx->fr.lastSlot].rayO; break;
+        case RT_ARR_PT_Q3_DIRS: src = ctx->fr.camQ3[ctx->fr.lastSlot].rayD; break;
+        case RT_ARR_PT_Q4_ORIGINS: src = ctx->fr.camQ4[ctx->fr.lastSlot].rayO; break;
+        case RT_ARR_PT_Q4_DIRS: src = ctx->fr.camQ4[ctx->fr.lastSlot].rayD; break;
         case RT_ARR_SUN_DIR: {
             if (bytes < 16) { ctx->err = "destination too small"; return RT_ERR_ARG; }
             float* o = (float*)dst;

@@ -92,6 +92,15 @@ struct FrameResources {
     uint32_t* camCount[kGbSets] = {};  // counter block per slot (PtWorkspace::counters)
     uint32_t* lastCounters = nullptr;  // the block of the last path trace (RT_ARR_PT_QUEUE)
     bool camInFlight[kGbSets] = {};
+    // ... and the bounce queues with their hit records, one slot per set when the shade kernel
+    // runs on the side stream (shadeOnSide: frame f+1's shade appends to its queues while frame
+    // f's tracers and resume kernels still read theirs); slot 0 is `ws`'s own buffers
+    PtQueue camQ3[kGbSets] = {}, camQ4[kGbSets] = {};
+    float4* camHitRec[kGbSets] = {};
+    float* camHitErr[kGbSets] = {};
+    float4* camPathL[kGbSets] = {};
+    uint32_t* camPending[kGbSets] = {};
+    int lastSlot = 0;                  // slot of the last path trace (RT_ARR_PT_Q*)
     HistCamera hist{};
     bool histValid = false;
     // denoise + post (denoising.cu, postprocessing.cu)
@@ -199,6 +208,10 @@ struct rt_context {
                            // resume<3> on more (set by rt_set_post_stream)
     hipEvent_t cameraGate = nullptr;
     bool cameraGated = false;
+    // pipelined frames: the shade kernel follows the camera kernel on the side stream (one GPU,
+    // set by rt_set_post_stream), so the next frame's shading runs beside this frame's tracers;
+    // the context stream keeps trace<3> .. resolve
+    bool shadeOnSide = false;
     DenoisePostParams postParams{};
     hipEvent_t* ptMarks = nullptr;  // set only inside rt_time_path_trace_kernels
     // rt_frame_marks_begin: events around every path-trace kernel of the next markFrames path traces

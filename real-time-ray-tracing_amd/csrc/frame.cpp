@@ -272,14 +272,18 @@ namespace {
 // PtLaunchHook of a pipelined frame: after kernel `overlapAfter` the previous frame's denoise
 // is issued (it then runs beside the trace stages' latency-bound tails), and after kernel
 // `cameraAfter` the gate event the next frame's camera rays wait for is recorded
+// the previous frame's deferred denoise, behind everything enqueued so far on the context stream
+hipError_t issue_overlapped_post(rt_context* ctx) {
+    hipError_t e = hipEventRecord(ctx->overlapEv, ctx->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->postStream, ctx->overlapEv, 0);
+    if (e == hipSuccess && issue_pending_post(ctx) != RT_OK) e = hipErrorUnknown;
+    return e;
+}
+
 hipError_t overlap_hook(void* arg, int kernel) {
     rt_context* ctx = (rt_context*)arg;
     hipError_t e = hipSuccess;
-    if (kernel == ctx->overlapAfter && ctx->postPending) {
-        e = hipEventRecord(ctx->overlapEv, ctx->stream);
-        if (e == hipSuccess) e = hipStreamWaitEvent(ctx->postStream, ctx->overlapEv, 0);
-        if (e == hipSuccess && issue_pending_post(ctx) != RT_OK) e = hipErrorUnknown;
-    }
+    if (kernel == ctx->overlapAfter && ctx->postPending) e = issue_overlapped_post(ctx);
     if (e == hipSuccess && kernel == ctx->cameraAfter) {
         e = hipEventRecord(ctx->cameraGate, ctx->stream);
         ctx->cameraGated = e == hipSuccess;
@@ -399,6 +403,12 @@ int rt_frame_init(rt_context* ctx) {
         ALLOC(ws.pending, (size_t)ctx->renderW * ctx->stripRows * 4);
         ALLOC(ws.surface, (size_t)ctx->renderW * ctx->stripRows * 4);
         ALLOC(fr.camCount[0], kWsCounterWords * 4);
+        fr.camQ3[0] = ws.q3;
+        fr.camQ4[0] = ws.q4;
+        fr.camHitRec[0] = ws.hitRec;
+        fr.camHitErr[0] = ws.hitErr;
+        fr.camPathL[0] = ws.pathL;
+        fr.camPending[0] = ws.pending;
         fr.camHit0Rec[0] = ws.hit0Rec;
         fr.camHit0Err[0] = ws.hit0Err;
         fr.camSurface[0] = ws.surface;
@@ -594,6 +604,14 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.ws.counters = fr.camCount[g];
     p.ws.fetch = p.ws.counters + 64;
     fr.lastCounters = p.ws.counters;
+    const int qs = fr.camQ3[g].rayO ? g : 0;  // bounce-queue slot: per set when allocated (shadeOnSide)
+    p.ws.q3 = fr.camQ3[qs];
+    p.ws.q4 = fr.camQ4[qs];
+    p.ws.hitRec = fr.camHitRec[qs];
+    p.ws.hitErr = fr.camHitErr[qs];
+    p.ws.pathL = fr.camPathL[qs];
+    p.ws.pending = fr.camPending[qs];
+    fr.lastSlot = qs;
     {  // material table (init.cu:215-251): only mirror / glass ids make steps 1-2 trace
         const int m = ctx->materialOverride;
         p.ws.glossy = m >= 0 && (m == 1 || m == 5 || m >= 10);
@@ -631,12 +649,20 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
         ~MarksReset() { c->ptMarks = m; }
     } marksReset{ctx, savedMarks};
     HIP_TRY(ctx, rtk_launch_pt_camera(&p, cs, ctx->ptMarks));
+    // one GPU: the shade kernel follows on the side stream, so it runs beside the previous frame's
+    // queue tracers instead of after them (its bounce queues are this set's own, camQ3[g] ..)
+    const bool shadeSide = side && ctx->shadeOnSide && qs == g;
+    if (shadeSide) HIP_TRY(ctx, rtk_launch_pt_shade(&p, cs, ctx->ptMarks));
     if (side) {
         HIP_TRY(ctx, hipEventRecord(ctx->camDone[g], cs));
+        // overlapAfter 0: the previous frame's denoise waits only for that frame's path trace
+        // (everything on the context stream so far), not for this frame's camera rays and shade
+        if (ctx->overlapAfter == 0 && ctx->postPending) HIP_TRY(ctx, issue_overlapped_post(ctx));
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->camDone[g], 0));
     }
     PtLaunchHook hook{overlap_hook, ctx};
-    HIP_TRY(ctx, rtk_launch_pt_rest(&p, ctx->stream, ctx->ptMarks, ctx->postStream ? &hook : nullptr));
+    if (shadeSide) HIP_TRY(ctx, rtk_launch_pt_rest_after_shade(&p, ctx->stream, ctx->ptMarks, &hook));
+    else HIP_TRY(ctx, rtk_launch_pt_rest(&p, ctx->stream, ctx->ptMarks, ctx->postStream ? &hook : nullptr));
     if (ctx->postPending && (rc = issue_pending_post(ctx)) != RT_OK) return rc;
     if (ctx->postStream) {
         HIP_TRY(ctx, hipEventRecord(ctx->restDone[g], ctx->stream));
@@ -1002,6 +1028,24 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
         ALLOC(fr.camHit0Err[k], cap * 4);
         ALLOC(fr.camSurface[k], strip * 4);
         ALLOC(fr.camCount[k], kWsCounterWords * 4);
+    }
+    // one GPU: the shade kernel runs on the side stream (RTX_SHADE_SIDE=0|1 overrides: A/B aid),
+    // with bounce queues per set
+    ctx->shadeOnSide = ctx->stripCount == 1;
+    if (const char* a = getenv("RTX_SHADE_SIDE")) ctx->shadeOnSide = atoi(a) != 0;
+    for (int k = 1; ctx->shadeOnSide && k < kGbSets; ++k) {
+        const size_t cap = fr.ws.cap, strip = (size_t)ctx->allocW * ctx->allocStripRows;
+        for (PtQueue* q : {&fr.camQ3[k], &fr.camQ4[k]}) {
+            ALLOC(q->rayO, cap * 16);
+            ALLOC(q->rayD, cap * 16);
+            ALLOC(q->st0, cap * 16);
+            ALLOC(q->st1, cap * 16);
+            ALLOC(q->st2, cap * 16);
+        }
+        ALLOC(fr.camHitRec[k], cap * 16);
+        ALLOC(fr.camHitErr[k], cap * 4);
+        ALLOC(fr.camPathL[k], cap * 16);
+        ALLOC(fr.camPending[k], strip * 4);
     }
 #undef ALLOC
     if ((rc = ensure_bvh_pair(ctx)) != RT_OK) return rc;

@@ -239,5 +239,11 @@ struct PtLaunchHook {
 extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks);
 extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
                                          const PtLaunchHook* hook);
+// The shade kernel alone (kernel 1, marks[2] / marks[3]), for a caller that runs it behind the
+// camera kernel on another stream; rtk_launch_pt_rest_after_shade then enqueues trace<3> ..
+// resolve and calls the hook for kernel 1 first, with nothing enqueued for it.
+extern "C" hipError_t rtk_launch_pt_shade(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks);
+extern "C" hipError_t rtk_launch_pt_rest_after_shade(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
+                                                     const PtLaunchHook* hook);
 extern "C" int rtk_trace_queue_blocks_per_cu();
 extern "C" hipError_t rtk_launch_trace_queue(const PathTraceParams* p, int step, hipStream_t stream);

@@ -1075,8 +1075,39 @@ extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t
 
 // hook (optional): called on the host right after each kernel is enqueued; the frame pipeline
 // issues the previous frame's denoise and gates the next frame's camera rays there (frame.cpp).
+namespace {
+void launch_shade(const PathTraceParams* p, hipStream_t stream) {
+    const dim3 pg(p->ws.persistBlocks), pb(256);
+    if (p->ws.glossy) hipLaunchKernelGGL((k_pt_shade0<true, false>), pg, pb, 0, stream, *p);
+    else if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_shade0<false, true>), pg, pb, 0, stream, *p);
+    else hipLaunchKernelGGL((k_pt_shade0<false, false>), pg, pb, 0, stream, *p);
+}
+
+hipError_t launch_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks, const PtLaunchHook* hook,
+                       bool withShade);
+}  // namespace
+
+extern "C" hipError_t rtk_launch_pt_shade(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks) {
+    hipError_t e;
+    if (marks && marks[2] && (e = hipEventRecord(marks[2], stream)) != hipSuccess) return e;
+    launch_shade(p, stream);
+    if (marks && marks[3] && (e = hipEventRecord(marks[3], stream)) != hipSuccess) return e;
+    return hipGetLastError();
+}
+
 extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
                                          const PtLaunchHook* hook) {
+    return launch_rest(p, stream, marks, hook, true);
+}
+
+extern "C" hipError_t rtk_launch_pt_rest_after_shade(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
+                                                     const PtLaunchHook* hook) {
+    return launch_rest(p, stream, marks, hook, false);
+}
+
+namespace {
+hipError_t launch_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks, const PtLaunchHook* hook,
+                       bool withShade) {
     hipError_t e = hipSuccess;  // the counters were zeroed before the camera kernel (rtk_launch_pt_camera)
     int k = 1;  // kernel 1 = shade; marks[2k] / marks[2k + 1] bracket kernel k on this stream
     // a null entry: that kernel is not bracketed (rt_frame_marks_begin's kernel mask)
@@ -1091,12 +1122,16 @@ extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t s
         ++k;
         return hipSuccess;
     };
-    if ((e = begin()) != hipSuccess) return e;
     const dim3 pg(p->ws.persistBlocks), pb(256);
-    if (p->ws.glossy) hipLaunchKernelGGL((k_pt_shade0<true, false>), pg, pb, 0, stream, *p);
-    else if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_shade0<false, true>), pg, pb, 0, stream, *p);
-    else hipLaunchKernelGGL((k_pt_shade0<false, false>), pg, pb, 0, stream, *p);
-    if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
+    if (withShade) {
+        if ((e = begin()) != hipSuccess) return e;
+        launch_shade(p, stream);
+        if ((e = end()) != hipSuccess) return e;
+    } else {  // enqueued by the caller on another stream: only the hook runs for kernel 1
+        if (hook && hook->fn && (e = hook->fn(hook->arg, k)) != hipSuccess) return e;
+        ++k;
+    }
+    if ((e = begin()) != hipSuccess) return e;
     if (p->ws.chain && !p->ws.glossy && !p->ws.microfacet) {
         // kernel 2 = the fused bounce chain (trace<3> .. resume<4>); slots 3-5 stay empty, so the
         // hook's kernel numbers and the per-kernel timing slots keep their meaning
@@ -1118,3 +1153,4 @@ extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t s
     if ((e = end()) != hipSuccess) return e;
     return hipGetLastError();
 }
+}  // namespace

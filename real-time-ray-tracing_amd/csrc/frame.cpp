@@ -680,7 +680,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
 int rt_get_ray_count(rt_context* ctx, uint64_t* rays, int reset) {
     if (!ctx || !rays) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_get_ray_count before rt_init"; return RT_ERR_STATE; }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = sync_streams(ctx)) return rc;  // the side stream's camera and shade kernels add rays too
     std::vector<unsigned long long> part((size_t)kRayCounterSlots * kRayCounterStride);
     const size_t bytes = part.size() * 8;
     HIP_TRY(ctx, hipMemcpy(part.data(), ctx->fr.rayCounter, bytes, hipMemcpyDeviceToHost));

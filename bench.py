@@ -468,7 +468,7 @@ def main():
 
     # warm-up; frames 2..W with every path-trace kernel bracketed by HIP events, which picks the
     # roofline's kernel: the longest on the frame's critical (context) stream (pipelined, the camera
-    # kernel, and on one GPU the shade kernel behind it, run on the side stream beside the previous
+    # kernel and the shade kernel behind it run on the side stream beside the previous
     # frame's tracers)
     side = {"k_pt_camera", "k_pt_shade0"} if pipeline and rt.info().shadeOnSide else {"k_pt_camera"}
     crit = [k for k in rtx.RayTracer.PT_KERNELS if not (pipeline and k in side)]
@@ -535,15 +535,15 @@ def main():
         "dtype": "f32",
         "data": "synthetic: the reference's default procedural scene (Perlin terrain, 60,800 triangles), "
                 "default camera and sky, deterministic stand-in soil textures",
-        "config": {"workload": "BASELINE config 3: %dx%d, %d spp path trace + SVGF denoise + auto-exposure/"
-                               "tone map, per-frame LBVH rebuild" % (W, H, S),
+        "config": {"workload": "BASELINE config %s: %dx%d, %d spp path trace + SVGF denoise + auto-exposure/"
+                               "tone map, per-frame LBVH rebuild" % ("5" if (W, H) == (3840, 2160) else "3", W, H, S),
                    "width": W, "height": H, "spp": S,
                    "parallelism": ("interleaved 16-row strips x%d + RCCL all-to-all of the G-buffer rows each "
                                    "rank's strip-local denoise reads (64-row blocks + halo), histogram all-reduce "
                                    "and accumulation/history/RGBA8 row all-gathers" % world if world > 1
                                    else "single GPU")
-                                  + ("; pipelined frames: denoise/post of f-1 and LBVH build + camera rays of "
-                                     "f+1 on their own streams beside the trace kernels of f" if pipeline
+                                  + ("; pipelined frames: denoise/post of f-1 and LBVH build + camera rays + "
+                                     "shading of f+1 on their own streams beside the trace kernels of f" if pipeline
                                      else "; serial frames")},
         "fps": round(1000.0 / ms_per_step, 2),
         "rays_per_frame": int(rays // args.steps),

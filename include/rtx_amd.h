@@ -194,7 +194,7 @@ typedef struct rt_info {
                                                halo when it is strip-local, else the whole frame */
     int32_t stripLocalDenoise;  /* 1: the next denoise is strip-local (the same on every rank) */
     int32_t shadeOnSide;        /* 1: pipelined frames run the shade kernel behind the camera kernel on
-                                   the side stream (one GPU, rt_set_post_stream), not on the context stream */
+                                   the side stream (rt_set_post_stream), not on the context stream */
 } rt_info;
 
 int rt_get_info(const rt_context* ctx, rt_info* out);

@@ -208,8 +208,8 @@ struct rt_context {
                            // resume<3> on more (set by rt_set_post_stream)
     hipEvent_t cameraGate = nullptr;
     bool cameraGated = false;
-    // pipelined frames: the shade kernel follows the camera kernel on the side stream (one GPU,
-    // set by rt_set_post_stream), so the next frame's shading runs beside this frame's tracers;
+    // pipelined frames: the shade kernel follows the camera kernel on the side stream (set by
+    // rt_set_post_stream), so the next frame's shading runs beside this frame's tracers;
     // the context stream keeps trace<3> .. resolve
     bool shadeOnSide = false;
     DenoisePostParams postParams{};

@@ -432,12 +432,18 @@ RT_DEV void start_sample(PathCtx& c, PathVars& v, int x, int y, float coneSpread
 // Pixel block of one k_pt_camera workgroup: four waves = (4 / nSW) 8x8 tiles x nSW sample
 // lanes, nSW = min(spp, 4) rounded down to 1, 2 or 4.
 __host__ __device__ inline int cam_sample_waves(uint32_t spp) { return spp >= 4 ? 4 : (spp >= 2 ? 2 : 1); }
+// one round of nSW sample waves covers every sample (spp 1, 2 and 4)
+inline bool one_round(uint32_t spp) { return spp >= 1 && ((int)spp + cam_sample_waves(spp) - 1) / cam_sample_waves(spp) == 1; }
 
 // Step 0 of every sample: the camera ray's RaySceneIntersect.  A sample that misses is complete
 // right here (its path is GenerateRay -> miss -> EnvLight2, pathtrace.cuh:61-128, with every
 // other step a no-op), so a pixel whose samples all miss — the sky, most of the default view —
 // gets its G-buffer texels from this kernel and never reaches the shading kernels.  The other
 // pixels keep their samples' hit records and are appended to the surface list for k_pt_shade0.
+//
+// kOneRound: every sample wave runs one round (spp <= 4 except 3: the launcher checks), so the
+// round loop and its carried state compile away.
+template <bool kOneRound>
 __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
     __shared__ uint2 stk[16 * 256];
     __shared__ uint32_t sob[256];
@@ -460,7 +466,7 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
     const SceneView sc = scene_of(P);
     PathCtx c{P, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), sob, BnPixel{0u, 0u}, 0, 0u, 0u, 0u, 0u};
     if (active) c.bp = bn_pixel(P.bluenoise, x, y);
-    const int rounds = ((int)P.spp + nSW - 1) / nSW;
+    const int rounds = kOneRound ? 1 : ((int)P.spp + nSW - 1) / nSW;
     F3 L = f3(0.0f), A = f3(0.0f);  // folding thread (sw == 0): running sums of an all-sky pixel
     bool anyHit = false;
     float4 rec = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -579,7 +585,10 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
 // them back to back.  The folding thread (sample wave 0) then combines the round's samples in
 // sample order through LDS — colour and albedo sums, the first deferred sample, the per-sample
 // colours the resolve kernel needs — exactly as the sequential loop of PathTrace's caller does.
-template <bool kGlossy, bool kMF>
+//
+// kOneRound as in k_pt_camera: with one round per sample wave the fold state around the sample loop
+// is not carried across rounds (229 instead of 256 VGPRs; one GPU 0.970 -> 0.945 ms/frame).
+template <bool kGlossy, bool kMF, bool kOneRound>
 __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
     __shared__ uint2 stk[kGlossy ? 16 * 256 : 1];
     __shared__ uint32_t sob[256];
@@ -596,7 +605,7 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
     const uint32_t n = P.ws.counters[kCntSurface];
     const int nSW = cam_sample_waves(P.spp), sw = w % nSW, g = w / nSW;
     const uint32_t perWg = 64u * (uint32_t)(4 / nSW);
-    const int rounds = ((int)P.spp + nSW - 1) / nSW;
+    const int rounds = kOneRound ? 1 : ((int)P.spp + nSW - 1) / nSW;
     const SceneView sc = scene_of(P);
     const size_t plane = (size_t)P.rows * P.width;
     uint32_t raysWg = 0, shV = 0, shT = 0, shD = 0;
@@ -1068,7 +1077,8 @@ extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t
     const int nSW = cam_sample_waves(p->spp);
     const int BW = nSW == 4 ? 8 : 16, BH = nSW == 1 ? 16 : 8;
     const dim3 grid((p->width + BW - 1) / BW, (p->rows + BH - 1) / BH);
-    hipLaunchKernelGGL(k_pt_camera, grid, dim3(256), 0, stream, *p);
+    if (one_round(p->spp)) hipLaunchKernelGGL(k_pt_camera<true>, grid, dim3(256), 0, stream, *p);
+    else hipLaunchKernelGGL(k_pt_camera<false>, grid, dim3(256), 0, stream, *p);
     if (marks && marks[1] && (e = hipEventRecord(marks[1], stream)) != hipSuccess) return e;
     return hipGetLastError();
 }
@@ -1076,11 +1086,17 @@ extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t
 // hook (optional): called on the host right after each kernel is enqueued; the frame pipeline
 // issues the previous frame's denoise and gates the next frame's camera rays there (frame.cpp).
 namespace {
-void launch_shade(const PathTraceParams* p, hipStream_t stream) {
+template <bool kOneRound>
+void launch_shade_rounds(const PathTraceParams* p, hipStream_t stream) {
     const dim3 pg(p->ws.persistBlocks), pb(256);
-    if (p->ws.glossy) hipLaunchKernelGGL((k_pt_shade0<true, false>), pg, pb, 0, stream, *p);
-    else if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_shade0<false, true>), pg, pb, 0, stream, *p);
-    else hipLaunchKernelGGL((k_pt_shade0<false, false>), pg, pb, 0, stream, *p);
+    if (p->ws.glossy) hipLaunchKernelGGL((k_pt_shade0<true, false, kOneRound>), pg, pb, 0, stream, *p);
+    else if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_shade0<false, true, kOneRound>), pg, pb, 0, stream, *p);
+    else hipLaunchKernelGGL((k_pt_shade0<false, false, kOneRound>), pg, pb, 0, stream, *p);
+}
+
+void launch_shade(const PathTraceParams* p, hipStream_t stream) {
+    if (one_round(p->spp)) launch_shade_rounds<true>(p, stream);
+    else launch_shade_rounds<false>(p, stream);
 }
 
 hipError_t launch_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks, const PtLaunchHook* hook,

@@ -797,12 +797,15 @@ __global__ __launch_bounds__(256, kMF ? 2 : 3) void k_pt_resume(PathTraceParams 
     // step 4 ends the path before any diffuse interaction: no light sampling there
     __shared__ __align__(16) float sSkyTree[kStep == 3 ? kSkyTreeNodes : 4];
     __shared__ __align__(16) float sSunTree[kStep == 3 ? kSunTreeNodes : 4];
+    const uint32_t n = P.ws.counters[kStep == 3 ? kCntQ3 : kCntQ4];
+    // a workgroup past the queue (queue 4 holds a few thousand entries against a grid sized for
+    // queue 3) leaves before staging its tables; block-uniform, no ray counted
+    if (blockIdx.x * 256u >= n) return;
     const int tid = threadIdx.x;
     bn_stage_sobol(P.bluenoise, sob, tid, 256);
     if (kStep == 3) stage_cdf_trees(P, sSkyTree, sSunTree, tid, 256);
     __syncthreads();
     const PtQueue& q = kStep == 3 ? P.ws.q3 : P.ws.q4;
-    const uint32_t n = P.ws.counters[kStep == 3 ? kCntQ3 : kCntQ4];
     const SceneView sc = scene_of(P);
     uint32_t rays = 0, rsD = 0;
 #pragma unroll 1

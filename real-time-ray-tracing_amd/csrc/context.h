@@ -101,6 +101,12 @@ struct FrameResources {
     float4* camPathL[kGbSets] = {};
     uint32_t* camPending[kGbSets] = {};
     int lastSlot = 0;                  // slot of the last path trace (RT_ARR_PT_Q*)
+    // queue 3's length after the last serial path trace, copied to pinned host memory behind it
+    // (the fused chain's on/off choice for serial frames)
+    uint32_t* q3Host = nullptr;
+    hipEvent_t q3Ev = nullptr;
+    bool q3Pending = false;
+    uint32_t lastQ3 = 0;
     HistCamera hist{};
     bool histValid = false;
     // denoise + post (denoising.cu, postprocessing.cu)

@@ -537,6 +537,37 @@ int rt_upload_texture(rt_context* ctx, int which, const uint16_t* texels, int wi
     return RT_OK;
 }
 
+namespace {
+// workspace slot k (1 .. kGbSets - 1): the camera outputs, and with `queues` the bounce queues with
+// their hit records (slot 0 is fr.ws's own buffers); allocated once, full size
+int alloc_ws_slot(rt_context* ctx, int k, bool queues) {
+    FrameResources& fr = ctx->fr;
+    int rc = RT_OK;
+#define ALLOC(p, bytes) if (!(p) && (rc = dalloc(ctx, &(p), (bytes))) != RT_OK) return rc
+    const size_t cap = fr.ws.cap, strip = (size_t)ctx->allocW * ctx->allocStripRows;
+    ALLOC(fr.camHit0Rec[k], cap * 16);
+    ALLOC(fr.camHit0Err[k], cap * 4);
+    ALLOC(fr.camSurface[k], strip * 4);
+    ALLOC(fr.camCount[k], kWsCounterWords * 4);
+    if (queues) {
+        for (PtQueue* q : {&fr.camQ3[k], &fr.camQ4[k]}) {
+            ALLOC(q->rayO, cap * 16);
+            ALLOC(q->rayD, cap * 16);
+            ALLOC(q->st0, cap * 16);
+            ALLOC(q->st1, cap * 16);
+            ALLOC(q->st2, cap * 16);
+        }
+        ALLOC(fr.camHitRec[k], cap * 16);
+        ALLOC(fr.camHitErr[k], cap * 4);
+        ALLOC(fr.camPathL[k], cap * 16);
+        ALLOC(fr.camPending[k], strip * 4);
+    }
+#undef ALLOC
+    return rc;
+}
+
+}  // namespace
+
 int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     if (!ctx || frame_num < 1) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_path_trace before rt_init"; return RT_ERR_STATE; }
@@ -621,7 +652,15 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     // beside which the next frame's camera waves fit (k_pt_chain's 168 VGPRs at 3 waves/SIMD leave
     // them no room); on ranks of 8 strips too, since the queue tracers' refill-free tail loops
     // (0.436 vs 0.450 ms per rank frame)
-    p.ws.chain = fr.ws.chain == 2 || (fr.ws.chain == 1 && !ctx->postStream);
+    // ... and only while queue 3 is short: a long queue (the terrain view's 3.85 M rays) runs the
+    // four kernels faster serially too (4.64 against 5.11 ms per synchronous terrain draw).  The
+    // length is the previous serial frame's, read back without waiting (q3Host, copied behind
+    // that frame's kernels; stale by a frame or more only if that frame has not finished).
+    if (fr.q3Host && fr.q3Pending && hipEventQuery(fr.q3Ev) == hipSuccess) {
+        fr.lastQ3 = *fr.q3Host;
+        fr.q3Pending = false;
+    }
+    p.ws.chain = fr.ws.chain == 2 || (fr.ws.chain == 1 && !ctx->postStream && fr.lastQ3 < kChainMaxQ3);
     if (with_detail) {  // per-pixel counters: everything in order on the context stream
         if (ctx->postStream && (rc = sync_streams(ctx)) != RT_OK) return rc;
         HIP_TRY(ctx, hipMemsetAsync(fr.rays, 0, (size_t)ctx->renderW * ctx->renderH * 4, ctx->stream));
@@ -661,8 +700,19 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->camDone[g], 0));
     }
     PtLaunchHook hook{overlap_hook, ctx};
+    if (!side && !fr.q3Pending) {  // serial frames: queue 3's length for the next frame's chain choice
+        if (!fr.q3Host) {
+            HIP_TRY(ctx, hipHostMalloc((void**)&fr.q3Host, sizeof(uint32_t), hipHostMallocDefault));
+            HIP_TRY(ctx, hipEventCreateWithFlags(&fr.q3Ev, hipEventDisableTiming));
+        }
+    }
     if (shadeSide) HIP_TRY(ctx, rtk_launch_pt_rest_after_shade(&p, ctx->stream, ctx->ptMarks, &hook));
     else HIP_TRY(ctx, rtk_launch_pt_rest(&p, ctx->stream, ctx->ptMarks, ctx->postStream ? &hook : nullptr));
+    if (!side && fr.q3Host && !fr.q3Pending) {
+        HIP_TRY(ctx, hipMemcpyAsync(fr.q3Host, p.ws.counters + kCntQ3, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipEventRecord(fr.q3Ev, ctx->stream));
+        fr.q3Pending = true;
+    }
     if (ctx->postPending && (rc = issue_pending_post(ctx)) != RT_OK) return rc;
     if (ctx->postStream) {
         HIP_TRY(ctx, hipEventRecord(ctx->restDone[g], ctx->stream));
@@ -1018,36 +1068,20 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
     const size_t P = (size_t)ctx->allocW * ctx->allocH;
 #define ALLOC(p, bytes) if (!(p) && (rc = dalloc(ctx, &(p), (bytes))) != RT_OK) return rc
     for (int k = 1; k < kGbSets; ++k) {  // further G-buffer sets and camera-output slots
-        const size_t cap = fr.ws.cap, strip = (size_t)ctx->allocW * ctx->allocStripRows;
         ALLOC(fr.gColor[k], P * 8);
         ALLOC(fr.gNormal[k], P * 8);
         ALLOC(fr.gAlbedo[k], P * 8);
         ALLOC(fr.gDepth[k], P * 2);
         ALLOC(fr.gMotion[k], P * 4);
-        ALLOC(fr.camHit0Rec[k], cap * 16);
-        ALLOC(fr.camHit0Err[k], cap * 4);
-        ALLOC(fr.camSurface[k], strip * 4);
-        ALLOC(fr.camCount[k], kWsCounterWords * 4);
+        if ((rc = alloc_ws_slot(ctx, k, false)) != RT_OK) return rc;
     }
     // the shade kernel runs on the side stream, with bounce queues per set (RTX_SHADE_SIDE=0|1
     // overrides: A/B aid); measured: one GPU 1.025 -> 0.970 ms/frame, one rank's
     // share at 2 / 4 / 8 ranks 0.648 -> 0.650 / 0.495 -> 0.482 / 0.453 -> 0.411 ms
     ctx->shadeOnSide = true;
     if (const char* a = getenv("RTX_SHADE_SIDE")) ctx->shadeOnSide = atoi(a) != 0;
-    for (int k = 1; ctx->shadeOnSide && k < kGbSets; ++k) {
-        const size_t cap = fr.ws.cap, strip = (size_t)ctx->allocW * ctx->allocStripRows;
-        for (PtQueue* q : {&fr.camQ3[k], &fr.camQ4[k]}) {
-            ALLOC(q->rayO, cap * 16);
-            ALLOC(q->rayD, cap * 16);
-            ALLOC(q->st0, cap * 16);
-            ALLOC(q->st1, cap * 16);
-            ALLOC(q->st2, cap * 16);
-        }
-        ALLOC(fr.camHitRec[k], cap * 16);
-        ALLOC(fr.camHitErr[k], cap * 4);
-        ALLOC(fr.camPathL[k], cap * 16);
-        ALLOC(fr.camPending[k], strip * 4);
-    }
+    for (int k = 1; ctx->shadeOnSide && k < kGbSets; ++k)
+        if ((rc = alloc_ws_slot(ctx, k, true)) != RT_OK) return rc;
 #undef ALLOC
     if ((rc = ensure_bvh_pair(ctx)) != RT_OK) return rc;
     for (int k = 0; k < kGbSets; ++k) {

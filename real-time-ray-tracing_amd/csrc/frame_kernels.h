@@ -85,6 +85,7 @@ enum PtCounter : int { kCntQ3 = 0, kCntQ4 = 1, kCntFetch3 = 2, kCntFetch4 = 3, k
                        kCntVisQ3 = 16, kCntTstQ3 = 17, kCntVisQ4 = 18, kCntTstQ4 = 19, kCntDiffShade = 20,
                        kCntDiffRes3 = 21, kCntCulledCam = 22, kCntSlots = 23 };
 constexpr int kWsCounterWords = 64 + 2 * 8 * 16;  // counters | fetch, zeroed together
+constexpr uint32_t kChainMaxQ3 = 1u << 20;  // serial frames fuse the bounce chain below this queue-3 length
 
 struct PtWorkspace {
     float4* hit0Rec;            // [spp][rows*W] camera-ray hits (t, triangle index bits, u, v)

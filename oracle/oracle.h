@@ -62,6 +62,7 @@ typedef struct OrcHit {
     uint32_t iterations;     // loop iterations used (cap 1024, traverse.h:132)
     uint32_t intoSurface;    // isRayIntoSurface (traverse.cuh:193)
     float ndr;               // normalDotRayDir after the flip (traverse.cuh:192-198)
+    uint32_t maxDepth;       // most entries the stack held at once (test diagnostics: deep-stack coverage)
 } OrcHit;
 
 // RaySceneIntersect core (traverse.cuh:64-225 without the material bookkeeping) for n rays.

@@ -41,7 +41,8 @@ class Scene(C.Structure):
 HIT_DTYPE = np.dtype([("t", "<f4"), ("objectIdx", "<i4"), ("u", "<f4"), ("v", "<f4"), ("normal", "<f4", 3),
                       ("fakeNormal", "<f4", 3), ("pos", "<f4", 3), ("offset", "<f4"), ("hit", "<u4"),
                       ("nodeVisits", "<u4"), ("triTests", "<u4"), ("droppedPushes", "<u4"),
-                      ("iterations", "<u4"), ("intoSurface", "<u4"), ("ndr", "<f4")])
+                      ("iterations", "<u4"), ("intoSurface", "<u4"), ("ndr", "<f4"),
+                      ("maxDepth", "<u4")])
 
 
 class CameraIn(C.Structure):

@@ -143,7 +143,7 @@ void intersect_one(const OrcScene* sc, F3 org, F3 dir, OrcHit& out) {
     F3 nrm = f3(0.0f), pos = f3(kRayMax), fake = f3(0.0f);
     float u = 0.0f, v = 0.0f;
     float errorP = 1e-7f, errorT = 1e-7f, offset = 1e-7f;
-    uint32_t visits = 0, tests = 0, dropped = 0, iters = 0;
+    uint32_t visits = 0, tests = 0, dropped = 0, iters = 0, maxDepth = 0;
 
     AABB sceneBox = node_merged(tlas[0]);
     BoxHelper h = make_helper(org, dir, sceneBox, inv);
@@ -161,6 +161,7 @@ void intersect_one(const OrcScene* sc, F3 org, F3 dir, OrcHit& out) {
         if (top >= 15) { ++dropped; return; }
         StackEntry s = {idx & 0x7FFFu, off & 0x7FFFu, isBlas, isLeaf, tt};
         stack[++top] = s;
+        if ((uint32_t)(top + 1) > maxDepth) maxDepth = (uint32_t)(top + 1);
     };
     for (int i = 0; i < 1024; ++i) {
         ++iters;
@@ -233,6 +234,7 @@ void intersect_one(const OrcScene* sc, F3 org, F3 dir, OrcHit& out) {
     out.intoSurface = into ? 1u : 0u;
     out.ndr = ndr;
     out.nodeVisits = visits; out.triTests = tests; out.droppedPushes = dropped; out.iterations = iters;
+    out.maxDepth = maxDepth;
 }
 
 }  // namespace orc

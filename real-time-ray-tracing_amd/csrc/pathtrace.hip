@@ -445,7 +445,8 @@ inline bool one_round(uint32_t spp) { return spp >= 1 && ((int)spp + cam_sample_
 // round loop and its carried state compile away.
 template <bool kOneRound>
 __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
-    __shared__ uint2 stk[16 * 256];
+    constexpr int kCamLds = 12;  // stack entries in LDS (the rest in registers): 5 workgroups per CU
+    __shared__ uint2 stk[kCamLds * 256];
     __shared__ uint32_t sob[256];
     __shared__ float4 fold[4][64];   // this round's samples: sky colour xyz, w = 1 when it hit
     __shared__ uint32_t surf[4][64]; // pixel has a sample that hit (set by its folding thread)
@@ -490,8 +491,9 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
                 TravRay tr;
                 trav_setup(sc, org, dir, tr);
                 trav_init(st);
+                DeepStack deep;
                 for (int it = 0; it < 1024; ++it)
-                    if (trav_step(sc, tr, st, stk + tid, 256)) break;
+                    if (trav_step_t<kCamLds>(sc, tr, st, stk + tid, 256, &deep)) break;
             }
             ++rays;
             if (P.statsOut) {

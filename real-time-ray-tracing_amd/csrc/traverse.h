@@ -275,13 +275,35 @@ RT_DEV void trav_root_miss(TravState& s) {
     s.visits = 1;
 }
 
+// The deepest entries of the 16-entry stack when the LDS holds fewer (trav_step_t<kLds>): entries
+// kLds .. 15 live in registers, written and read through select chains (no indexed private array,
+// no scratch).  Only rays whose stack grows past kLds entries ever touch them.
+struct DeepStack {
+    uint2 e0, e1, e2, e3;
+};
+RT_DEV void deep_set(DeepStack& d, int k, uint2 v) {
+    d.e0 = k == 0 ? v : d.e0;
+    d.e1 = k == 1 ? v : d.e1;
+    d.e2 = k == 2 ? v : d.e2;
+    d.e3 = k == 3 ? v : d.e3;
+}
+RT_DEV unsigned long long deep_get(const DeepStack& d, int k) {
+    const uint2 v = k == 0 ? d.e0 : k == 1 ? d.e1 : k == 2 ? d.e2 : d.e3;
+    return ((unsigned long long)v.y << 32) | v.x;
+}
+
 // One loop iteration; returns true when the stack ran empty (TestForFinish, traverse.h:88-105).
 // The caller stops at 1024 iterations as well.
 //
 // Written for a short dependent chain per iteration (a lone wave's traversal latency sets the
 // tail of the queue tracer): the node visit picks the next node and the pushed sibling with
 // selects instead of the reference's four-way branch, and there is a single branch for the push.
-RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint2* stk, int stride) {
+//
+// kLds: stack entries kept in LDS (the others, up to the reference's 16, in `deep`); the camera
+// kernel keeps 12 there, so that five of its workgroups fit a CU's LDS instead of four.
+template <int kLds>
+RT_DEV bool trav_step_t(const SceneView& sc, const TravRay& r, TravState& s, uint2* stk, int stride, DeepStack* deep) {
+    static_assert(kLds >= 12 && kLds <= 16, "LDS stack depth: 12..16 entries (at most 4 in registers)");
     ++s.iters;
     bool pop;
     if (!s.cLeaf) {
@@ -298,9 +320,11 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint2
         if (push) {
             const uint32_t pIdx = goLeft ? nd.q3.y : nd.q3.x;
             const uint32_t pLeaf = goLeft ? nd.q3.w : nd.q3.z;
-            stk[(s.top + 1) * stride] = make_uint2((pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) |
-                                                       ((s.cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31),
-                                                   __float_as_uint(goLeft ? t2 : t1));
+            const uint2 entry = make_uint2((pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) |
+                                               ((s.cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31),
+                                           __float_as_uint(goLeft ? t2 : t1));
+            if (kLds == 16 || s.top + 1 < kLds) stk[(s.top + 1) * stride] = entry;
+            else deep_set(*deep, s.top + 1 - kLds, entry);
         }
         s.top += push ? 1 : 0;
         pop = !i1 && !i2;
@@ -332,7 +356,8 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint2
             if (s.top < 0) return true;
             // one 8-byte read per pop: volatile keeps the compiler from splitting it into a
             // t read inside the loop and an index read sunk after it (two dependent round trips)
-            const unsigned long long e = *(volatile LdsU64*)(&stk[s.top * stride]);
+            const unsigned long long e = (kLds == 16 || s.top < kLds) ? *(volatile LdsU64*)(&stk[s.top * stride])
+                                                                      : deep_get(*deep, s.top - kLds);
             const uint32_t a = (uint32_t)e;
             s.cT = __uint_as_float((uint32_t)(e >> 32));
             --s.top;
@@ -343,6 +368,10 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint2
         } while (s.cT > s.t);
     }
     return false;
+}
+
+RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint2* stk, int stride) {
+    return trav_step_t<16>(sc, r, s, stk, stride, nullptr);
 }
 
 // Wave-level leaf batching for the lanes of one wave that each run their own traversal: a lane

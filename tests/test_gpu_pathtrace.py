@@ -114,6 +114,29 @@ def test_pathtrace_bit_exact(rtx, oracle, tmp_path, default_scene, sky_tex, w, h
         assert (o["color"][:, 3] == 3).mean() > 0.3  # material 3 (Lambertian) on the terrain
 
 
+def test_pathtrace_1m_scene_deep_stack(rtx, oracle, tmp_path):
+    """The camera kernel keeps 12 of the 16 traversal-stack entries in LDS and the deepest four in
+    registers (traverse.h trav_step_t<12>).  The default scene's rays never hold more than 11
+    entries; the 1M-triangle scene's (BASELINE config 4, BLAS depth up to 19) reach 15, so this
+    frame runs the register entries, and its G-buffers and per-pixel ray counts stay bit-exact."""
+    w, h, frame = 1280, 720, 2
+    v, i, n = oracle.scene(4)
+    bvh = oracle.build_bvh(v, i, n, oracle.smooth_normals(v, i))
+    rays, _ = oracle.primary_rays(w, h, frame)
+    depth = oracle.intersect(bvh, rays)["maxDepth"]
+    assert (depth >= 13).sum() > 100  # deep stacks occur in this view
+    cfg = rtx.write_config(str(tmp_path / "c.toml"), w, h, chunk_dim=4)
+    rt = rtx.RayTracer(w, h, cfg).init()
+    rt.build_bvh()
+    rt.path_trace(frame, detail=True)
+    rt.sync()
+    g = gpu_gbuffers(rt, w, h)
+    rt.cleanup()
+    o = oracle.pathtrace(bvh, w, h, frame_num=frame, cam=oracle.default_camera(w, h), sky_out=oracle.sky(),
+                         tex=oracle.textures())
+    assert_gbuffers_equal(g, o)
+
+
 @pytest.mark.parametrize("dist", [1e3, 1e4, 1e5])
 def test_pathtrace_distant_camera_cull(rtx, oracle, tmp_path, default_scene, sky_tex, dist):
     """The camera kernel's scene cull (`root_surely_missed`, a slab test of the root box grown by

@@ -445,7 +445,10 @@ inline bool one_round(uint32_t spp) { return spp >= 1 && ((int)spp + cam_sample_
 // round loop and its carried state compile away.
 template <bool kOneRound>
 __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
-    constexpr int kCamLds = 12;  // stack entries in LDS (the rest in registers): 5 workgroups per CU
+    // stack entries in LDS (the rest in registers): 26 KB per workgroup, 6 workgroups per CU
+    // (measured: 16 entries 4 per CU 0.948 ms/frame, 12 entries 5 per CU 0.918, 10 entries 6 per CU
+    // 0.900; the default scene's rays hold at most 11 entries)
+    constexpr int kCamLds = 10;
     __shared__ uint2 stk[kCamLds * 256];
     __shared__ uint32_t sob[256];
     __shared__ float4 fold[4][64];   // this round's samples: sky colour xyz, w = 1 when it hit

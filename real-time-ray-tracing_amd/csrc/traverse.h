@@ -279,16 +279,18 @@ RT_DEV void trav_root_miss(TravState& s) {
 // kLds .. 15 live in registers, written and read through select chains (no indexed private array,
 // no scratch).  Only rays whose stack grows past kLds entries ever touch them.
 struct DeepStack {
-    uint2 e0, e1, e2, e3;
+    uint2 e0, e1, e2, e3, e4, e5;
 };
 RT_DEV void deep_set(DeepStack& d, int k, uint2 v) {
     d.e0 = k == 0 ? v : d.e0;
     d.e1 = k == 1 ? v : d.e1;
     d.e2 = k == 2 ? v : d.e2;
     d.e3 = k == 3 ? v : d.e3;
+    d.e4 = k == 4 ? v : d.e4;
+    d.e5 = k == 5 ? v : d.e5;
 }
 RT_DEV unsigned long long deep_get(const DeepStack& d, int k) {
-    const uint2 v = k == 0 ? d.e0 : k == 1 ? d.e1 : k == 2 ? d.e2 : d.e3;
+    const uint2 v = k == 0 ? d.e0 : k == 1 ? d.e1 : k == 2 ? d.e2 : k == 3 ? d.e3 : k == 4 ? d.e4 : d.e5;
     return ((unsigned long long)v.y << 32) | v.x;
 }
 
@@ -300,10 +302,10 @@ RT_DEV unsigned long long deep_get(const DeepStack& d, int k) {
 // selects instead of the reference's four-way branch, and there is a single branch for the push.
 //
 // kLds: stack entries kept in LDS (the others, up to the reference's 16, in `deep`); the camera
-// kernel keeps 12 there, so that five of its workgroups fit a CU's LDS instead of four.
+// kernel keeps 10 there, so that six of its workgroups fit a CU's LDS instead of four.
 template <int kLds>
 RT_DEV bool trav_step_t(const SceneView& sc, const TravRay& r, TravState& s, uint2* stk, int stride, DeepStack* deep) {
-    static_assert(kLds >= 12 && kLds <= 16, "LDS stack depth: 12..16 entries (at most 4 in registers)");
+    static_assert(kLds >= 10 && kLds <= 16, "LDS stack depth: 10..16 entries (at most 6 in registers)");
     ++s.iters;
     bool pop;
     if (!s.cLeaf) {

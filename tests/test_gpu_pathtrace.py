@@ -115,16 +115,17 @@ def test_pathtrace_bit_exact(rtx, oracle, tmp_path, default_scene, sky_tex, w, h
 
 
 def test_pathtrace_1m_scene_deep_stack(rtx, oracle, tmp_path):
-    """The camera kernel keeps 12 of the 16 traversal-stack entries in LDS and the deepest four in
-    registers (traverse.h trav_step_t<12>).  The default scene's rays never hold more than 11
-    entries; the 1M-triangle scene's (BASELINE config 4, BLAS depth up to 19) reach 15, so this
-    frame runs the register entries, and its G-buffers and per-pixel ray counts stay bit-exact."""
+    """The camera kernel keeps 10 of the 16 traversal-stack entries in LDS and the deepest six in
+    registers (traverse.h trav_step_t<10>).  The default scene's rays hold at most 11 entries; the
+    1M-triangle scene's (BASELINE config 4, BLAS depth up to 19) reach 15, so this frame runs the
+    register entries 10..14 for thousands of rays, and its G-buffers and per-pixel ray counts stay
+    bit-exact."""
     w, h, frame = 1280, 720, 2
     v, i, n = oracle.scene(4)
     bvh = oracle.build_bvh(v, i, n, oracle.smooth_normals(v, i))
     rays, _ = oracle.primary_rays(w, h, frame)
     depth = oracle.intersect(bvh, rays)["maxDepth"]
-    assert (depth >= 13).sum() > 100  # deep stacks occur in this view
+    assert (depth >= 11).sum() > 1000 and (depth >= 15).sum() > 0  # deep stacks occur in this view
     cfg = rtx.write_config(str(tmp_path / "c.toml"), w, h, chunk_dim=4)
     rt = rtx.RayTracer(w, h, cfg).init()
     rt.build_bvh()

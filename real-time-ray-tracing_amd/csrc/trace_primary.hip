@@ -4,7 +4,8 @@
 // k_trace_primary: GenerateRay (raygen.cuh:7-38, blue-noise sample frameNum*4,
 // pathtrace.cuh:116-129) + RaySceneIntersect geometry (traverse.cuh:64-222) per pixel.
 // 256-thread workgroups cover 16x16 pixels; each wave64 owns an 8x8 tile so its rays are
-// coherent.  The 16-entry traversal stack lives in LDS (32 KB per workgroup).
+// coherent.  Of the 16-entry traversal stack, 10 entries live in LDS (20 KB per workgroup) and
+// the deepest 6 in registers (traverse.h trav_step_t), so six workgroups fit a CU instead of five.
 //
 // k_smooth_normals: GenerateSmoothNormals run twice into an un-cleared buffer
 // (kernel.cu:228-257, 313-327), made deterministic: one thread per vertex gathers its
@@ -16,7 +17,8 @@
 using namespace rtd;
 
 __global__ __launch_bounds__(256) void k_trace_primary(TracePrimaryParams P) {
-    __shared__ uint2 stk[16 * 256];
+    constexpr int kLds = 10;
+    __shared__ uint2 stk[kLds * 256];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int x = blockIdx.x * 16 + (w & 1) * 8 + (lane & 7);
     const int yl = blockIdx.y * 16 + (w >> 1) * 8 + (lane >> 3);
@@ -36,7 +38,7 @@ __global__ __launch_bounds__(256) void k_trace_primary(TracePrimaryParams P) {
     sc.nodes = (const Node*)P.nodes;
     sc.tlas = (const Node*)P.tlasNodes;
     HitInfo hi;
-    intersect(sc, org, dir, stk + tid, 256, hi);
+    intersect<kLds>(sc, org, dir, stk + tid, 256, hi);
 
     const size_t p = (size_t)y * P.width + x;
     P.hitOut[p] = make_float4(hi.t, __int_as_float(hi.objectIdx), hi.u, hi.v);

@@ -425,6 +425,8 @@ RT_DEV void finalize_hit(const SceneView& sc, F3 org, F3 dir, float t, int hitId
     out.hit = hit;
 }
 
+// kLds as in trav_step_t: the stack entries kept in LDS (k_trace_primary keeps 10)
+template <int kLds = 16>
 RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint2* stk, int stride, HitInfo& out) {
     TravState s;
     if (root_surely_missed(sc, org, dir)) {
@@ -433,8 +435,9 @@ RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint2* stk, int strid
         TravRay r;
         trav_setup(sc, org, dir, r);
         trav_init(s);
+        DeepStack deep;
         for (int it = 0; it < 1024; ++it)
-            if (trav_step(sc, r, s, stk, stride)) break;
+            if (trav_step_t<kLds>(sc, r, s, stk, stride, &deep)) break;
     }
     finalize_hit(sc, org, dir, s.t, s.hitIdx, s.hitU, s.hitV, s.hitErrT, out);
     out.u = s.u;

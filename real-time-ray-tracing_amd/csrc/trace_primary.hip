@@ -16,7 +16,12 @@
 
 using namespace rtd;
 
+#ifndef RTX_PRIMARY_WPE  // ablation builds only (tools/abl_build.sh): force waves per SIMD
 __global__ __launch_bounds__(256) void k_trace_primary(TracePrimaryParams P) {
+#else
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTX_PRIMARY_WPE, RTX_PRIMARY_WPE)))
+void k_trace_primary(TracePrimaryParams P) {
+#endif
     constexpr int kLds = 10;
     __shared__ uint2 stk[kLds * 256];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;

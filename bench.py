@@ -61,6 +61,7 @@ HBM_PEAK_GBS = 8000.0   # /opt/skills/guides/MI355X_MICROARCH.md (spec peak)
 L2_PEAK_GBS = 34500.0   # MI355X_MICROARCH.md, L2 (per XCD) section: aggregate L2 bandwidth
 DELTA_MS = 16.667       # fixed AutoExposure step (SURVEY §8d determinism settings)
 PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_kernels.json")
+PMC_C2C4 = os.path.join(ROOT, "profiles", "r04_pmc_c2c4.json")  # tools/prof_r04_c2c4.sh (configs 2 and 4)
 TERRAIN_CAM = dict(pos=(8.0, 15.0, -6.0), yaw=0.0, pitch=-0.7)  # ~50 % primary hits (tests' camera)
 
 # algorithmic bytes: per node visit the 64-B node record, per triangle test the
@@ -244,6 +245,55 @@ def kernel_roofline(q, W, rows, S, kernels_ms, pmc, workload_matches):
     return out
 
 
+def pmc_c2c4(kernel, key):
+    """HBM bytes per launch and L2 hit rate of a config-2 / config-4 kernel from the committed PMC
+    passes (tools/prof_r04_c2c4.sh -> profiles/r04_pmc_c2c4.json), when its workload matches."""
+    if not os.path.exists(PMC_C2C4):
+        return {}
+    with open(PMC_C2C4) as f:
+        pm = json.load(f)
+    if pm.get("workload_key", {}).get(kernel) != key or kernel not in pm.get("kernels", {}):
+        return {}
+    e = pm["kernels"][kernel]
+    return {k: e[k] for k in ("hbm_bytes", "l2_hit_rate", "valu_busy_frac", "wait_any_frac") if k in e} | {
+        "traffic_source": os.path.relpath(PMC_C2C4, ROOT)}
+
+
+def primary_roofline(rt, W, H, ms, frames):
+    """BASELINE config 2 (1920x1080, 1 spp primary rays, k_trace_primary alone): algorithmic bytes per
+    launch from the kernel's own counters (24 B ray + 16 B hit per ray, 64 B per node visit,
+    48 B per triangle test; detail launches of the same frames 1..`frames` the timing ran, averaged),
+    over the launch's HIP-event ms, against L2 and HBM; PMC traffic from the committed passes."""
+    visits = tests = past_root = 0
+    for f in range(1, frames + 1):
+        rt.trace_primary(f, detail=True)
+        rt.sync()
+        hs = rt.download("HIT_STATS", np.uint32).reshape(-1, 4).astype(np.int64)
+        visits += int(hs[:, 0].sum())
+        tests += int(hs[:, 1].sum())
+        past_root += int((hs[:, 3] > 1).sum())
+    rays = W * H
+    v, t, pr = visits / frames, tests / frames, past_root / frames
+    alg = (24 + 16) * rays + NODE_B * v + TRI_B * t
+    a = alg / (ms * 1e-3) / 1e9
+    out = {"kernel": "k_trace_primary", "workload": "BASELINE config 2: %dx%d, 1 spp primary rays (GenerateRay + "
+                                                    "RaySceneIntersect), default scene and camera" % (W, H),
+           "kernel_ms": round(ms, 5), "rays": rays, "node_visits": round(v, 1), "tri_tests": round(t, 1),
+           "visits_per_ray": round(v / rays, 3), "algorithmic_bytes": int(alg), "achieved": round(a, 1),
+           "unit": "GB/s", "bound": "l2", "limiter": "latency", "peak": L2_PEAK_GBS, "frac": round(a / L2_PEAK_GBS, 4),
+           "frac_hbm": round(a / HBM_PEAK_GBS, 4), "mray_s": round(rays / (ms * 1e-3) / 1e6, 1),
+           "rays_traversed": round(pr, 1), "mray_s_traversed": round(pr / (ms * 1e-3) / 1e6, 1),
+           "traversed_definition": "rays whose TraverseBvh ran past the TLAS root (iterations > 1); the rest are "
+                                   "settled at the root (by the scene cull or the exact root box test)",
+           "counters": "HIT_STATS of detail launches of frames 1..%d (the timed launches' frames)" % frames,
+           "timing": "rt_time_stage(1, %d): HIP events around %d back-to-back launches, frames 1..%d" % (
+               frames, frames, frames)}
+    pm = pmc_c2c4("k_trace_primary", "%dx%dx1 primary" % (W, H))
+    out["traffic"] = pm.pop("hbm_bytes", None)
+    out.update(pm)
+    return out
+
+
 def iteration_histogram(rt, frame):
     """TraverseBvh iterations of the frame's camera rays (rt_trace_primary detail: 1 spp, frame
     index `frame`): distribution, mean, max, and how many rays the scene cull settled (1 iteration)."""
@@ -372,6 +422,7 @@ def extras_child(args):
                               "denoise_post": round(sr.time_stage(4, 20) / 20, 5),
                               "primary_rays_1spp": round(sr.time_stage(1, 20) / 20, 5)}
     out["primary_mray_s"] = round(W * H / (out["stage_ms_serial"]["primary_rays_1spp"] * 1e-3) / 1e6, 2)
+    out["primary_roofline"] = primary_roofline(sr, W, H, out["stage_ms_serial"]["primary_rays_1spp"], 20)
     sk = sr.time_path_trace_kernels(20)
     names = list(sk)
     if all(sk[k] < 0.02 for k in names[3:6]):  # the fused chain k_pt_chain ran in kernel slot 2
@@ -406,9 +457,13 @@ def extras_child(args):
     n4 = r4.info().triCount
     r4.cleanup()
     a4 = 348 * n4 / (ms4 * 1e-3) / 1e9
+    pm4 = pmc_c2c4("k_build_bvh@958720", "%d tris" % n4)
     out["lbvh_build_1m"] = {"tris": int(n4), "ms": round(ms4, 5),
-                            "roofline": {"bound": "hbm", "achieved": round(a4, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                         "frac": round(a4 / HBM_PEAK_GBS, 5), "traffic": None, "bytes_per_tri": 348}}
+                            "roofline": dict({"bound": "hbm", "achieved": round(a4, 2), "peak": HBM_PEAK_GBS,
+                                              "unit": "GB/s", "frac": round(a4 / HBM_PEAK_GBS, 5),
+                                              "traffic": pm4.pop("hbm_bytes", None), "bytes_per_tri": 348,
+                                              "algorithmic_bytes": 348 * int(n4),
+                                              "timing": "rt_time_stage(0, 30): HIP events around 30 builds"}, **pm4)}
     if args.check_file:
         fin = np.load(args.check_file)
         out["self_check"] = self_check(rtx, W, H, S, tmp, args.check_frames,

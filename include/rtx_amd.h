@@ -172,6 +172,19 @@ int rt_upload_texture(rt_context* ctx, int which, const uint16_t* texels, int wi
  * terrain.cpp:5-45), at n points (xyz triples). */
 int rt_scene_noise3d(const float* xyz, size_t n, float* out);
 
+/* The denoiser's Gaussian weights (GetGaussian3x3 / 5x5 / 7x7, gaussian.cuh:12-43; the precomputed
+ * tables, USE_PRECALCULATED_GAUSSIAN): size 3, 5 or 7, row-major size*size floats into out (count
+ * >= size*size).  The same values the device kernels use.  Host only, no device needed. */
+int rt_filter_kernel(int size, float* out, int count);
+
+/* Scan(in, out, tmp, size, blockSize, postfix), scan.cuh:258-298: prefix sum of `size` floats in
+ * DEVICE memory — blocks of block_size scanned in LDS (Blelloch tree order), the block totals
+ * scanned in one workgroup into tmp (>= size / block_size floats; unused for one block), then added.
+ * postfix 1: inclusive, 0: exclusive.  size and block_size powers of two, block_size and the block
+ * count each <= 8192 (the reference's asserts).  Enqueued on `stream` (a hipStream_t; NULL = null
+ * stream), asynchronous.  Errors: RT_ERR_ARG / RT_ERR_HIP with rt_last_error(NULL). */
+int rt_scan_device(const float* in, float* out, float* tmp, int size, int block_size, int postfix, void* stream);
+
 /* Determinism hooks the reference lacks: the frame counter is a function static
  * (kernel.cu:64) and AutoExposure reads wall-clock deltaTime (postprocessing.cu:46-51). */
 int rt_set_frame_index(rt_context* ctx, int frame_num); /* next rt_draw renders this frameNum */

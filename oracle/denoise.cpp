@@ -78,6 +78,14 @@ const double kG7[49] = {
     0.000360475, 0.00367191,  0.0147158,  0.0234191,  0.0148519,   0.0037404,   0.000370662,
     3.57221e-05, 0.000363875, 0.0014583,  0.00232075, 0.00147179,  0.000370662, 3.67315e-05};
 
+// the tables as the filters use them (each double literal rounded to float), row-major
+extern "C" int orc_filter_kernel(int size, float* out) {
+    const double* g = size == 3 ? kG3 : size == 5 ? kG5 : size == 7 ? kG7 : nullptr;
+    if (!g || !out) return -1;
+    for (int i = 0; i < size * size; ++i) out[i] = (float)g[i];
+    return 0;
+}
+
 const float kRayMaxF = 10e10f;
 
 inline float h2f(uint16_t h) { return rt_h2f(h); }

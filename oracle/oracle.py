@@ -251,6 +251,12 @@ def _bind_frame_api(L):
     L.orc_sun_dir.restype = None
     L.orc_scan.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
     L.orc_scan.restype = None
+    L.orc_scan_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
+    L.orc_scan_ex.restype = None
+    L.orc_cpu_scan.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+    L.orc_cpu_scan.restype = None
+    L.orc_filter_kernel.argtypes = [C.c_int, C.c_void_p]
+    L.orc_filter_kernel.restype = C.c_int
     L.orc_textures.argtypes = [C.c_void_p, C.c_void_p]
     L.orc_textures.restype = None
     L.orc_mip_chain.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
@@ -310,11 +316,27 @@ def sky_radiance(direction, time_of_day: float = 0.25, sun_axis_angle: float = 4
     return out
 
 
-def scan(x: np.ndarray, block: int) -> np.ndarray:
+def scan(x: np.ndarray, block: int, postfix: int = 1) -> np.ndarray:
+    """Scan (scan.cuh:258-298): Blelloch blocks in tree order, block totals scanned, added."""
     x = np.ascontiguousarray(x, np.float32)
     y = np.zeros_like(x)
-    lib().orc_scan(x.ctypes.data, y.ctypes.data, x.size, block)
+    lib().orc_scan_ex(x.ctypes.data, y.ctypes.data, x.size, block, postfix)
     return y
+
+
+def cpu_scan(x: np.ndarray, postfix: int = 1) -> np.ndarray:
+    """CpuScan (scan.cuh:235-251): the sequential float scan the reference's scan test compares with."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.zeros_like(x)
+    lib().orc_cpu_scan(x.ctypes.data, y.ctypes.data, x.size, postfix)
+    return y
+
+
+def filter_kernel(size: int) -> np.ndarray:
+    """The denoiser's Gaussian table (gaussian.cuh:12-43) as the oracle's filters use it."""
+    out = np.zeros(size * size, np.float32)
+    assert lib().orc_filter_kernel(size, out.ctypes.data) == 0
+    return out
 
 
 def textures():

@@ -184,8 +184,8 @@ static void blelloch_exclusive(float* a, int n) {
     }
 }
 
-// Scan(in, out, tmp, size, blockSize, postfix=1) (scan.cuh:258-298)
-void scan_inclusive(const float* in, float* out, int size, int blockSize) {
+// Scan(in, out, tmp, size, blockSize, postfix) (scan.cuh:258-298); postfix 0: exclusive blocks
+void scan_blocks(const float* in, float* out, int size, int blockSize, int postfix) {
     int blocks = size / blockSize;
     std::vector<float> sums(blocks), tmp(blockSize);
     for (int b = 0; b < blocks; ++b) {
@@ -204,7 +204,8 @@ void scan_inclusive(const float* in, float* out, int size, int blockSize) {
         }
         sums[b] = up[blockSize - 1];
         blelloch_exclusive(tmp.data(), blockSize);
-        for (int i = 0; i < blockSize; ++i) out[(size_t)b * blockSize + i] = tmp[i] + in[(size_t)b * blockSize + i];
+        for (int i = 0; i < blockSize; ++i)
+            out[(size_t)b * blockSize + i] = postfix ? tmp[i] + in[(size_t)b * blockSize + i] : tmp[i];
     }
     if (blocks > 1) {
         blelloch_exclusive(sums.data(), blocks);
@@ -213,11 +214,29 @@ void scan_inclusive(const float* in, float* out, int size, int blockSize) {
     }
 }
 
+void scan_inclusive(const float* in, float* out, int size, int blockSize) { scan_blocks(in, out, size, blockSize, 1); }
+
 }  // namespace orc
 
 using namespace orc;
 
 extern "C" void orc_scan(const float* in, float* out, int size, int blockSize) { scan_inclusive(in, out, size, blockSize); }
+extern "C" void orc_scan_ex(const float* in, float* out, int size, int blockSize, int postfix) {
+    scan_blocks(in, out, size, blockSize, postfix);
+}
+// CpuScan (scan.cuh:235-251): the reference's sequential float scan, its test's CPU side
+extern "C" void orc_cpu_scan(const float* in, float* out, int size, int postfix) {
+    float accu = 0.0f;
+    for (int i = 0; i < size; ++i) {
+        if (postfix) {
+            accu += in[i];
+            out[i] = accu;
+        } else {
+            out[i] = accu;
+            accu += in[i];
+        }
+    }
+}
 
 extern "C" void orc_sun_dir(float timeOfDay, float sunAxisAngle, float* out) {
     F3 d = sun_direction(timeOfDay, sunAxisAngle);

@@ -15,6 +15,7 @@
 #include <fstream>
 #include <sstream>
 
+#include "gaussian_tables.h"
 #include "rtmath.h"
 #include "toml_lite.h"
 
@@ -257,6 +258,32 @@ const char* rt_last_error(const rt_context* ctx) { return ctx ? ctx->err.c_str()
 int rt_scene_noise3d(const float* xyz, size_t n, float* out) {
     if (n > 0 && (!xyz || !out)) return RT_ERR_ARG;
     for (size_t k = 0; k < n; ++k) out[k] = rtscene::noise3d(xyz[3 * k], xyz[3 * k + 1], xyz[3 * k + 2]);
+    return RT_OK;
+}
+
+int rt_filter_kernel(int size, float* out, int count) {
+    static const float g3[9] = RT_GAUSS3_INIT, g5[25] = RT_GAUSS5_INIT, g7[49] = RT_GAUSS7_INIT;
+    const float* g = size == 3 ? g3 : size == 5 ? g5 : size == 7 ? g7 : nullptr;
+    if (!g || !out || count < size * size) return RT_ERR_ARG;
+    memcpy(out, g, sizeof(float) * size * size);
+    return RT_OK;
+}
+
+int rt_scan_device(const float* in, float* out, float* tmp, int size, int block_size, int postfix, void* stream) {
+    if (!in || !out || size <= 0) {
+        g_createError = "rt_scan_device: null buffer or empty size";
+        return RT_ERR_ARG;
+    }
+    const hipError_t e = rtk_launch_scan_ex(in, out, tmp, size, block_size, postfix ? 1 : 0, (hipStream_t)stream);
+    if (e == hipErrorInvalidValue) {
+        g_createError = "rt_scan_device: size / block_size must be powers of two with block_size and the block "
+                        "count <= 8192, and tmp non-null when there is more than one block";
+        return RT_ERR_ARG;
+    }
+    if (e != hipSuccess) {
+        g_createError = std::string("rt_scan_device: ") + hipGetErrorString(e);
+        return RT_ERR_HIP;
+    }
     return RT_OK;
 }
 

@@ -14,6 +14,7 @@
 //   noise8/16   ushort = half per 8x8 / 16x16 tile
 //   c4/c16/c64  uint2  = half4 (DownScale4 chain), histogram uint32[64], exposure float[4]
 //   scaled      uint2  = half4 at screen size, rgba uint32 = RGBA8
+#include "gaussian_tables.h"
 #include "frame_kernels.h"
 #include "pt_common.h"
 #include "rt_device.h"
@@ -51,26 +52,10 @@ constexpr bool kDnGateAll = true;
 constexpr bool kDnGateAll = false;
 #endif
 
-// gaussian.cuh:12-47 (double literals converted to float, as the reference's float arrays)
-__constant__ float cG3[9] = {(float)0.0578968, (float)0.0921378, (float)0.0584323, (float)0.0921378, (float)0.146629,
-                             (float)0.09299,   (float)0.0584322, (float)0.0929898, (float)0.0589727};
-__constant__ float cG5[25] = {
-    (float)0.00360466, (float)0.0144464, (float)0.0229902, (float)0.01458,   (float)0.0036719,
-    (float)0.0144464,  (float)0.0578968, (float)0.0921378, (float)0.0584323, (float)0.0147159,
-    (float)0.0229902,  (float)0.0921378, (float)0.146629,  (float)0.09299,   (float)0.023419,
-    (float)0.01458,    (float)0.0584322, (float)0.0929898, (float)0.0589727, (float)0.014852,
-    (float)0.00367191, (float)0.0147158, (float)0.0234191, (float)0.0148519, (float)0.0037404};
-__constant__ float cG7[49] = {
-    (float)3.47404e-05, (float)0.000353875, (float)0.00141822, (float)0.00225698, (float)0.00143134,
-    (float)0.000360475, (float)3.57221e-05, (float)0.000353875, (float)0.00360466, (float)0.0144464,
-    (float)0.0229902,   (float)0.01458,     (float)0.0036719,  (float)0.000363875, (float)0.00141822,
-    (float)0.0144464,   (float)0.0578968,   (float)0.0921378,  (float)0.0584323,  (float)0.0147159,
-    (float)0.0014583,   (float)0.00225698,  (float)0.0229902,  (float)0.0921378,  (float)0.146629,
-    (float)0.09299,     (float)0.023419,    (float)0.00232076, (float)0.00143134, (float)0.01458,
-    (float)0.0584322,   (float)0.0929898,   (float)0.0589727,  (float)0.014852,   (float)0.00147179,
-    (float)0.000360475, (float)0.00367191,  (float)0.0147158,  (float)0.0234191,  (float)0.0148519,
-    (float)0.0037404,   (float)0.000370662, (float)3.57221e-05, (float)0.000363875, (float)0.0014583,
-    (float)0.00232075,  (float)0.00147179,  (float)0.000370662, (float)3.67315e-05};
+// gaussian.cuh:12-43 (double literals converted to float, as the reference's float arrays)
+__constant__ float cG3[9] = RT_GAUSS3_INIT;
+__constant__ float cG5[25] = RT_GAUSS5_INIT;
+__constant__ float cG7[49] = RT_GAUSS7_INIT;
 
 RT_DEV float h2f(uint32_t h) { return rt_h2f((uint16_t)h); }
 RT_DEV uint32_t f2h(float f) { return rt_f2h(f); }

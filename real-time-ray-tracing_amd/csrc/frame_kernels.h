@@ -226,6 +226,9 @@ extern "C" hipError_t rtk_launch_sky(const SkyGenParams* p, hipStream_t stream);
 extern "C" hipError_t rtk_launch_mipgen(uint16_t* chain, int size, int levels, int channels, hipStream_t stream);
 extern "C" hipError_t rtk_launch_scan(const float* in, float* out, float* sums, int size, int blockSize,
                                       hipStream_t stream);
+// Scan (scan.cuh:258-298) with the reference's postfix flag and size range (rt_scan_device)
+extern "C" hipError_t rtk_launch_scan_ex(const float* in, float* out, float* sums, int size, int blockSize,
+                                         int postfix, hipStream_t stream);
 // kernels of one path-trace launch: camera, shade, trace<3>, resume<3>, trace<4>, resume<4>, resolve
 constexpr int kPtKernels = 7;
 struct PtLaunchHook {

@@ -104,19 +104,23 @@ __global__ __launch_bounds__(256) void k_sun(SkyGenParams P) {
     P.sunPdf[i] = dot(c, f3(0.3f, 0.6f, 0.1f));
 }
 
-// Blelloch scan of one block of n (power of two <= 512) values in LDS, n/2 threads.
-// out[i] = exclusive[i] + in[i]; sums[block] = the up-sweep root (block total).
+// Blelloch scan of one block of n (power of two, 2..8192) values in dynamic LDS: blockDim.x
+// threads (<= 256) take the d active pairs of each tree level in strides, so every level performs
+// the reference's additions in its order (ScanSingleBlock<n, batch>, scan.cuh:31-137, splits the
+// same levels over n/2/batch threads).  kInclusive: out[i] = exclusive[i] + in[i] (postfix 1),
+// else the exclusive scan (postfix 0); sums[block] = the up-sweep root (block total).  in == out
+// is allowed (the reference scans its block totals in place).
+template <bool kInclusive>
 __global__ __launch_bounds__(256) void k_scan_block(const float* in, float* out, float* sums, int n) {
-    __shared__ float a[512];
-    const int t = threadIdx.x;
+    extern __shared__ float a[];
+    const int t = threadIdx.x, T = blockDim.x;
     const float* src = in + (size_t)blockIdx.x * n;
-    a[t] = src[t];
-    a[t + n / 2] = src[t + n / 2];
+    for (int i = t; i < n; i += T) a[i] = src[i];
     int offset = 1;
     for (int d = n >> 1; d > 0; d >>= 1) {
         __syncthreads();
-        if (t < d) {
-            const int ai = offset * (2 * t + 1) - 1, bi = offset * (2 * t + 2) - 1;
+        for (int i = t; i < d; i += T) {
+            const int ai = offset * (2 * i + 1) - 1, bi = offset * (2 * i + 2) - 1;
             a[bi] = a[bi] + a[ai];
         }
         offset *= 2;
@@ -129,8 +133,8 @@ __global__ __launch_bounds__(256) void k_scan_block(const float* in, float* out,
     for (int d = 1; d < n; d *= 2) {
         offset >>= 1;
         __syncthreads();
-        if (t < d) {
-            const int ai = offset * (2 * t + 1) - 1, bi = offset * (2 * t + 2) - 1;
+        for (int i = t; i < d; i += T) {
+            const int ai = offset * (2 * i + 1) - 1, bi = offset * (2 * i + 2) - 1;
             const float tmp = a[ai];
             a[ai] = a[bi];
             a[bi] = a[bi] + tmp;
@@ -138,40 +142,7 @@ __global__ __launch_bounds__(256) void k_scan_block(const float* in, float* out,
     }
     __syncthreads();
     float* dst = out + (size_t)blockIdx.x * n;
-    dst[t] = a[t] + src[t];
-    dst[t + n / 2] = a[t + n / 2] + src[t + n / 2];
-}
-
-// exclusive Blelloch scan of the block totals in place (single workgroup)
-__global__ __launch_bounds__(256) void k_scan_sums(float* sums, int n) {
-    __shared__ float a[512];
-    const int t = threadIdx.x;
-    a[t] = sums[t];
-    a[t + n / 2] = sums[t + n / 2];
-    int offset = 1;
-    for (int d = n >> 1; d > 0; d >>= 1) {
-        __syncthreads();
-        if (t < d) {
-            const int ai = offset * (2 * t + 1) - 1, bi = offset * (2 * t + 2) - 1;
-            a[bi] = a[bi] + a[ai];
-        }
-        offset *= 2;
-    }
-    __syncthreads();
-    if (t == 0) a[n - 1] = 0.0f;
-    for (int d = 1; d < n; d *= 2) {
-        offset >>= 1;
-        __syncthreads();
-        if (t < d) {
-            const int ai = offset * (2 * t + 1) - 1, bi = offset * (2 * t + 2) - 1;
-            const float tmp = a[ai];
-            a[ai] = a[bi];
-            a[bi] = a[bi] + tmp;
-        }
-    }
-    __syncthreads();
-    sums[t] = a[t];
-    sums[t + n / 2] = a[t + n / 2];
+    for (int i = t; i < n; i += T) dst[i] = kInclusive ? a[i] + src[i] : a[i];
 }
 
 __global__ __launch_bounds__(256) void k_scan_add(float* out, const float* sums, int n, int total) {
@@ -179,19 +150,36 @@ __global__ __launch_bounds__(256) void k_scan_add(float* out, const float* sums,
     if (i < total) out[i] = out[i] + sums[i / n];
 }
 
-extern "C" hipError_t rtk_launch_scan(const float* in, float* out, float* sums, int size, int blockSize,
-                                      hipStream_t stream) {
-    const int blocks = size / blockSize;
-    if (blockSize < 2 || blockSize > 512 || (blockSize & (blockSize - 1)) || size % blockSize ||
-        blocks > 512 || (blocks > 1 && (blocks & (blocks - 1))))
+// Scan(in, out, tmp, size, blockSize, postfix) (scan.cuh:258-298): blocks of blockSize, the block
+// totals scanned exclusively in one workgroup, then added to every block.  Sizes as the reference
+// asserts: powers of two, blockSize and the block count each <= 8192.
+extern "C" hipError_t rtk_launch_scan_ex(const float* in, float* out, float* sums, int size, int blockSize,
+                                         int postfix, hipStream_t stream) {
+    if (blockSize < 2 || blockSize > 8192 || (blockSize & (blockSize - 1)) || size < blockSize || size % blockSize)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_scan_block, dim3(blocks), dim3(blockSize / 2), 0, stream, in, out, sums, blockSize);
+    const int blocks = size / blockSize;
+    if (blocks > 8192 || (blocks & (blocks - 1)) || (blocks > 1 && !sums)) return hipErrorInvalidValue;
+    const int thr = blockSize / 2 < 256 ? blockSize / 2 : 256;
+    const size_t lds = (size_t)blockSize * sizeof(float);
+    if (postfix)
+        hipLaunchKernelGGL(k_scan_block<true>, dim3(blocks), dim3(thr), lds, stream, in, out, blocks > 1 ? sums : nullptr,
+                           blockSize);
+    else
+        hipLaunchKernelGGL(k_scan_block<false>, dim3(blocks), dim3(thr), lds, stream, in, out,
+                           blocks > 1 ? sums : nullptr, blockSize);
     if (blocks > 1) {
-        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(blocks / 2), 0, stream, sums, blocks);
+        const int st = blocks / 2 < 256 ? blocks / 2 : 256;
+        hipLaunchKernelGGL(k_scan_block<false>, dim3(1), dim3(st), (size_t)blocks * sizeof(float), stream,
+                           (const float*)sums, sums, (float*)nullptr, blocks);
         hipLaunchKernelGGL(k_scan_add, dim3((size + 255) / 256), dim3(256), 0, stream, out, (const float*)sums,
                            blockSize, size);
     }
     return hipGetLastError();
+}
+
+extern "C" hipError_t rtk_launch_scan(const float* in, float* out, float* sums, int size, int blockSize,
+                                      hipStream_t stream) {
+    return rtk_launch_scan_ex(in, out, sums, size, blockSize, 1, stream);
 }
 
 // heap node j of the bisection over [0, right0] of `cdf` (see kSkyTreeNodes); nodes the

@@ -143,6 +143,8 @@ SIGNATURES = {
     "rt_save_image": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
     "rt_upload_texture": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]),
     "rt_scene_noise3d": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p]),
+    "rt_filter_kernel": (C.c_int, [C.c_int, C.c_void_p, C.c_int]),
+    "rt_scan_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "rt_frame_marks_begin": (C.c_int, [C.c_void_p, C.c_int, C.c_uint32]),
     "rt_frame_marks_read": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]),
 }

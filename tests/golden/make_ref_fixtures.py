@@ -9,7 +9,10 @@ present; the GPU box and the tests only read the committed outputs).
      ref_settings.json  settings_dump: the default SkyParams .. DenoisingParams member values
      sky table digest   skydata_dump: the tables in data/sky_tables.bin's layout (sha256 only: the
                         shipped file must equal it byte for byte)
-2. Records the reference's only meshProcessor scene, resources/models/test.bin: its size, sha256,
+2. Records the denoiser's precomputed Gaussian tables, gaussian.cuh:12-43 (GetGaussian3x3 / 5x5 /
+   7x7 under USE_PRECALCULATED_GAUSSIAN 1): each literal as written and as the float it becomes
+   (ref_gaussian.json).  Data read from the header's text, not source.
+3. Records the reference's only meshProcessor scene, resources/models/test.bin: its size, sha256,
    header count and first 64 records (64 B each, ref_test_bin_head.bin).  Data, not source.
 Writes ref_fixtures.json with the sha256 of every output and the commands that made them."""
 import hashlib
@@ -25,6 +28,21 @@ OUT = os.path.join(ROOT, "oracle", "_ref")
 
 def sha(b):
     return hashlib.sha256(b).hexdigest()
+
+
+def gaussian_tables(text):
+    """The three precomputed tables of gaussian.cuh (float arrays cGaussian3x3 / 5x5 / 7x7 inside the
+    USE_PRECALCULATED_GAUSSIAN branch): literal tokens and their float32 values (bit patterns)."""
+    import re
+    import struct
+    out = {}
+    for n in (3, 5, 7):
+        m = re.search(r"float\s+cGaussian%dx%d\[\]\s*=\s*\{(.*?)\}" % (n, n), text, re.S)
+        toks = [t for t in re.split(r"[\s,]+", m.group(1)) if t]
+        assert len(toks) == n * n, (n, len(toks))
+        bits = [struct.unpack("<I", struct.pack("<f", float(t)))[0] for t in toks]
+        out["%dx%d" % (n, n)] = {"literals": toks, "float32_bits": bits}
+    return out
 
 
 def main():
@@ -43,6 +61,11 @@ def main():
     sky = subprocess.run([os.path.join(OUT, "skydata_dump")], check=True, capture_output=True).stdout
     man["sky_tables"] = {"sha256": sha(sky), "bytes": len(sky), "command": "oracle/_ref/skydata_dump",
                          "source": "src/skyData.h:2-174", "compare": "real-time-ray-tracing_amd/data/sky_tables.bin"}
+    g = gaussian_tables(open(os.path.join(REF, "src", "gaussian.cuh")).read())
+    gj = (json.dumps(g, indent=1, sort_keys=True) + "\n").encode()
+    open(os.path.join(HERE, "ref_gaussian.json"), "wb").write(gj)
+    man["ref_gaussian.json"] = {"sha256": sha(gj), "command": "tests/golden/make_ref_fixtures.py gaussian_tables",
+                                "source": "src/gaussian.cuh:12-43"}
     tb = open(os.path.join(REF, "resources", "models", "test.bin"), "rb").read()
     head = tb[4:4 + 64 * 64]
     open(os.path.join(HERE, "ref_test_bin_head.bin"), "wb").write(head)

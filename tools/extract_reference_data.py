@@ -126,8 +126,9 @@ def c_array(text, name):
     return [t for t in re.split(r"[\s,]+", body) if t]
 
 
-def main():
-    os.makedirs(OUT, exist_ok=True)
+def extract(out_dir=OUT):
+    """Writes the three data files into out_dir and returns their manifest (MANIFEST.json's content)."""
+    os.makedirs(out_dir, exist_ok=True)
     manifest = {}
 
     # ---- tiles -------------------------------------------------------------
@@ -139,7 +140,7 @@ def main():
         blob += struct.pack("<I", arr.shape[0]) + arr.tobytes()
         report[k] = {"tris": int(arr.shape[0]), "nonzero_fan_start": int(sum(1 for s in starts if s)),
                      "min_|anglesum-pi|": round(margin, 6)}
-    path = os.path.join(OUT, "roundcubes_l2.bin")
+    path = os.path.join(out_dir, "roundcubes_l2.bin")
     open(path, "wb").write(bytes(blob))
     manifest["roundcubes_l2.bin"] = {"sha256": hashlib.sha256(bytes(blob)).hexdigest(),
                                      "source": "resources/models/roundcubes/2/{1..15}.obj",
@@ -153,7 +154,7 @@ def main():
     rnk = np.array([int(x) for x in c_array(sec, "h_rankingTile")], dtype=np.uint8)
     assert sob.size == 256 * 256 and scr.size == 128 * 128 * 8 and rnk.size == 128 * 128 * 8
     blob = sob.tobytes() + scr.tobytes() + rnk.tobytes()
-    path = os.path.join(OUT, "bluenoise_4spp.bin")
+    path = os.path.join(out_dir, "bluenoise_4spp.bin")
     open(path, "wb").write(blob)
     manifest["bluenoise_4spp.bin"] = {"sha256": hashlib.sha256(blob).hexdigest(),
                                       "source": "src/blueNoiseRandGenData.h (OPTIMIZED_BLUE_NOISE_SPP==4)"}
@@ -168,11 +169,16 @@ def main():
         tables.append(vals)
     blob = struct.pack("<I", len(tables)) + b"".join(struct.pack("<I", t.size) for t in tables)
     blob += b"".join(t.tobytes() for t in tables)
-    path = os.path.join(OUT, "sky_tables.bin")
+    path = os.path.join(out_dir, "sky_tables.bin")
     open(path, "wb").write(blob)
     manifest["sky_tables.bin"] = {"sha256": hashlib.sha256(blob).hexdigest(), "source": "src/skyData.h",
                                   "tables": {n: int(t.size) for n, t in zip(names, tables)}}
 
+    return manifest
+
+
+def main():
+    manifest = extract(OUT)
     json.dump(manifest, open(os.path.join(OUT, "MANIFEST.json"), "w"), indent=1, sort_keys=True)
     json.dump(manifest, sys.stdout, indent=1, sort_keys=True)
     print()

@@ -208,6 +208,9 @@ typedef struct rt_info {
     int32_t stripLocalDenoise;  /* 1: the next denoise is strip-local (the same on every rank) */
     int32_t shadeOnSide;        /* 1: pipelined frames run the shade kernel behind the camera kernel on
                                    the side stream (rt_set_post_stream), not on the context stream */
+    int32_t lastChain;          /* 1: the last rt_path_trace ran its bounce stages as the fused k_pt_chain
+                                   (serial frames while the previous serial frame's queue 3 was short),
+                                   0: as the four kernels trace<3> .. resume<4>; profiles differ */
 } rt_info;
 
 int rt_get_info(const rt_context* ctx, rt_info* out);
@@ -323,7 +326,9 @@ typedef struct rt_strip_exchange {
 #define RT_HOOK_GBUFFERS 2
 typedef int (*rt_collective_fn)(void* arg, int stage, void* stream, const rt_strip_exchange* x);
 int rt_set_collective_hook(rt_context* ctx, rt_collective_fn fn, void* arg);
-/* which stages the hook is called for: bit (1 << RT_HOOK_*); default HISTOGRAM | ROWS */
+/* which stages the hook is called for: bit (1 << RT_HOOK_*); default HISTOGRAM | ROWS.  HISTOGRAM and
+ * ROWS are mandatory whenever a strip-local denoise runs (a mask without either is refused with
+ * RT_ERR_ARG); the mask only opts into RT_HOOK_GBUFFERS. */
 int rt_set_hook_stages(rt_context* ctx, uint32_t stage_mask);
 
 /* Use caller-owned device memory (>= the buffer's size at the largest render size, i.e.

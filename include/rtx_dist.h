@@ -87,7 +87,9 @@ int rtd_exchange_rows(rtd_strips* s, void* accum, void* history, void* rgba, voi
 /* Allocate (hipMalloc) and bind (rt_bind_buffer) the full-frame buffers the exchanges move — the
  * G-buffers of all three G-buffer sets, accumulation, both history buffers, histogram, RGBA8 — and
  * install rtd_hook for RT_HOOK_GBUFFERS, RT_HOOK_HISTOGRAM and RT_HOOK_ROWS (rt_set_hook_stages).
- * ctx must be an inited context of this rank's strip (stripCount = world, stripIndex = rank). */
+ * ctx must be an inited context of this rank's strip (stripCount = world, stripIndex = rank).
+ * On failure the buffers bound before the failing step stay bound to ctx and are owned by s: the
+ * context must then not render again — destroy it (rt_destroy), then the strips (rtd_destroy). */
 int rtd_attach(rtd_strips* s, rt_context* ctx);
 /* the rt_collective_fn rtd_attach installs (arg = the rtd_strips) */
 int rtd_hook(void* arg, int stage, void* stream, const rt_strip_exchange* x);

@@ -555,6 +555,7 @@ int rt_get_info(const rt_context* ctx, rt_info* out) {
     uint32_t sa = 0, sb = 0, lo = 0, hi = (uint32_t)ctx->renderH;
     out->stripLocalDenoise = 0;
     out->shadeOnSide = ctx->postStream && ctx->shadeOnSide ? 1 : 0;
+    out->lastChain = ctx->fr.lastChain ? 1 : 0;
     if (ctx->inited && strip_local_denoise(ctx, sa, sb)) {
         gbuffer_rows((uint32_t)ctx->renderH, sa, sb, lo, hi);
         out->stripLocalDenoise = 1;

@@ -107,6 +107,7 @@ struct FrameResources {
     hipEvent_t q3Ev = nullptr;
     bool q3Pending = false;
     uint32_t lastQ3 = 0;
+    bool lastChain = false;  // the last path trace ran the fused k_pt_chain (rt_info.lastChain)
     HistCamera hist{};
     bool histValid = false;
     // denoise + post (denoising.cu, postprocessing.cu)

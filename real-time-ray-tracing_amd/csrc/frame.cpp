@@ -661,6 +661,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
         fr.q3Pending = false;
     }
     p.ws.chain = fr.ws.chain == 2 || (fr.ws.chain == 1 && !ctx->postStream && fr.lastQ3 < kChainMaxQ3);
+    fr.lastChain = p.ws.chain && !p.ws.glossy && !p.ws.microfacet;  // as rtk_launch_pt_rest decides
     if (with_detail) {  // per-pixel counters: everything in order on the context stream
         if (ctx->postStream && (rc = sync_streams(ctx)) != RT_OK) return rc;
         HIP_TRY(ctx, hipMemsetAsync(fr.rays, 0, (size_t)ctx->renderW * ctx->renderH * 4, ctx->stream));
@@ -1003,6 +1004,13 @@ int rt_set_collective_hook(rt_context* ctx, rt_collective_fn fn, void* arg) {
 
 int rt_set_hook_stages(rt_context* ctx, uint32_t stage_mask) {
     if (!ctx || (stage_mask & ~7u) != 0) return RT_ERR_ARG;
+    // HISTOGRAM and ROWS are what make a strip-local denoise equal one GPU's: a mask without them
+    // would leave each rank with its own exposure and stale peer rows, so it is refused
+    const uint32_t need = (1u << RT_HOOK_HISTOGRAM) | (1u << RT_HOOK_ROWS);
+    if ((stage_mask & need) != need) {
+        ctx->err = "rt_set_hook_stages: HISTOGRAM and ROWS are mandatory; the mask only opts into GBUFFERS";
+        return RT_ERR_ARG;
+    }
     ctx->hookStages = stage_mask;
     return RT_OK;
 }

@@ -85,7 +85,7 @@ class Info(C.Structure):
                 ("deviceId", C.c_int32), ("spp", C.c_uint32), ("gbufferSet", C.c_int32),
                 ("denoiseRowBegin", C.c_int32), ("denoiseRowEnd", C.c_int32),
                 ("gbufferRowBegin", C.c_int32), ("gbufferRowEnd", C.c_int32), ("stripLocalDenoise", C.c_int32),
-                ("shadeOnSide", C.c_int32)]
+                ("shadeOnSide", C.c_int32), ("lastChain", C.c_int32)]
 
 
 class StripExchange(C.Structure):

@@ -127,3 +127,17 @@ def test_rccl_communicator_library_exports():
     syms = sorted(set(re.findall(r"\b(rtd_[a-z_0-9]+)\s*\(", text)))
     L = C.CDLL(os.path.join(ROOT, "real-time-ray-tracing_amd", "lib", "librtx_rccl.so"))
     assert len(syms) == 4 and all(hasattr(L, s) for s in syms)
+
+
+def test_hook_stage_mask_requires_histogram_and_rows(rtx):
+    """rt_set_hook_stages: HISTOGRAM and ROWS are mandatory for a strip-local denoise; the mask only opts
+    into GBUFFERS (a mask without them would leave ranks with their own exposure and stale peer rows)."""
+    rt = rtx.RayTracer(64, 64, None)
+    L = rt.lib
+    assert L.rt_set_hook_stages(rt.h, 0) == -1
+    assert L.rt_set_hook_stages(rt.h, 1 << 2) == -1          # GBUFFERS alone
+    assert L.rt_set_hook_stages(rt.h, (1 << 0) | (1 << 2)) == -1  # no ROWS
+    assert L.rt_set_hook_stages(rt.h, 8) == -1                # unknown stage
+    assert L.rt_set_hook_stages(rt.h, 3) == 0
+    assert L.rt_set_hook_stages(rt.h, 7) == 0
+    rt.cleanup()

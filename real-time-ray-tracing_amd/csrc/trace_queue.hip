@@ -29,6 +29,16 @@ constexpr uint32_t kTrace3Short = 1u << 20;  // queue-3 length below which trace
 #define RTX_LEAF_BATCH 1
 #endif
 constexpr bool kLeafBatch = RTX_LEAF_BATCH != 0;  // ablation: -DRTX_LEAF_BATCH=0
+#ifndef RTX_TRAV_PF
+#define RTX_TRAV_PF 1
+#endif
+constexpr bool kPrefetch = RTX_TRAV_PF != 0;  // next record loaded one iteration ahead (ablation: 0)
+
+// one TraverseBvh iteration of this lane's ray (trav_step_pf, or trav_step_t without the prefetch)
+RT_DEV bool step(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk) {
+    if (kPrefetch) return trav_step_pf<16>(sc, r, s, rec, stk, kTraceBlock, nullptr);
+    return trav_step(sc, r, s, stk, kTraceBlock);
+}
 
 template <int kStep>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) {
@@ -58,6 +68,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
     uint32_t idx = 0, accV = 0, accT = 0;
     TravRay r;
     TravState s;
+    TravRec rec;  // the record the lane's next iteration processes (trav_step_pf)
     r.org = f3(0.0f);
     trav_init(s);
 #pragma unroll 1
@@ -76,6 +87,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
                     const float4 o = q.rayO[idx], d = q.rayD[idx];
                     trav_setup(sc, f3(o.x, o.y, o.z), f3(d.x, d.y, d.z), r);
                     trav_init(s);
+                    if (kPrefetch) rec = trav_first_rec(sc);
                     active = true;
                     occlusion = kStep == 4 || (__float_as_uint(d.w) & kQShadowFlag) != 0u;
                 } else if (none) {
@@ -93,10 +105,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
         if (tail || !kLeafBatch ? active : trav_lane_steps(active, s)) {
             bool done = false;
             do {  // two steps per trip: the loop's refill / exec-mask bookkeeping once per two
-                done = trav_step(sc, r, s, stk + tid, kTraceBlock) || s.iters >= 1024u ||
+                done = step(sc, r, s, rec, stk + tid) || s.iters >= 1024u ||
                        (occlusion && s.hitIdx >= 0);
                 if (!done && (tail || !kLeafBatch || trav_lane_steps(true, s)))
-                    done = trav_step(sc, r, s, stk + tid, kTraceBlock) || s.iters >= 1024u ||
+                    done = step(sc, r, s, rec, stk + tid) || s.iters >= 1024u ||
                            (occlusion && s.hitIdx >= 0);
             } while (tail && !done);
             if (done) {

@@ -376,6 +376,127 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint2
     return trav_step_t<16>(sc, r, s, stk, stride, nullptr);
 }
 
+// ---- the same iteration with its memory access one iteration ahead (trav_step_pf)
+//
+// A lone ray's iteration is a dependent chain: the node record arrives, the box tests pick the next
+// node, its address is formed and its record loaded.  In trav_step_t the loop's bookkeeping (the
+// push, counters, the leaf / pop branches' exec-mask work, the loop test) sits between the choice
+// and the next load.  trav_step_pf issues the next record's load as soon as the next node is known
+// and does that bookkeeping while the load is in flight; the record is carried to the next
+// iteration in registers (TravRec).  The iterations themselves — which node or triangle each one
+// tests, the pushes, drops, pops, counters and the 1024 cap — are trav_step_t's exactly.
+//
+// What the record holds for the node an iteration processes:
+//   internal node   its 64-B record (TLAS or BLAS)
+//   BLAS leaf       its triangle's three vertices (48 B; the fourth quad re-reads the first)
+//   TLAS leaf       the root record of that batch's BLAS: the TLAS-leaf iteration needs no data
+//                   (TraverseBvh only switches to the BLAS there), so the BLAS root's load is
+//                   issued when the TLAS leaf is chosen, one iteration earlier than trav_step_t's
+struct TravRec {
+    float4 a, b, c;
+    uint4 d;
+};
+
+RT_DEV TravRec load_rec(const SceneView& sc, bool leaf, bool blas, uint32_t idx, uint32_t off) {
+    // selects, not branches: the address is on the iteration's critical path
+    const bool tri = leaf && blas;
+    const uint32_t li = off * 1024u + idx;
+    const uint32_t ni = blas ? li : (leaf ? idx * 1024u : idx);
+    const float4* nb = (!leaf && !blas) ? (const float4*)sc.tlas : (const float4*)sc.nodes;
+    const float4* base = tri ? sc.triPos + 3u * li : nb + 4u * ni;  // pointer selects: global loads, not flat
+    TravRec rec;
+    rec.a = base[0];
+    rec.b = base[1];
+    rec.c = base[2];
+    rec.d = *(const uint4*)(base + (tri ? 0 : 3));  // no read past the triangle array's end
+    return rec;
+}
+
+// the record of the first iteration (the TLAS root, after trav_init)
+RT_DEV TravRec trav_first_rec(const SceneView& sc) { return load_rec(sc, false, false, 0u, 0u); }
+
+template <int kLds>
+RT_DEV bool trav_step_pf(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk, int stride,
+                         DeepStack* deep) {
+    static_assert(kLds >= 10 && kLds <= 16, "LDS stack depth: 10..16 entries (at most 6 in registers)");
+    ++s.iters;
+    bool pop = false, push = false, tlasLeaf = false;
+    uint32_t pIdx = 0u, pLeaf = 0u, pT = 0u;  // the pushed sibling (entry built after the load)
+    uint32_t nIdx = s.cIdx, nOff = s.cOff;
+    bool nBlas = s.cBlas, nLeaf = s.cLeaf;
+    float nT = s.cT;
+    if (!s.cLeaf) {
+        Node nd;
+        nd.q0 = rec.a; nd.q1 = rec.b; nd.q2 = rec.c; nd.q3 = rec.d;
+        ++s.visits;
+        float t1, t2;
+        bool i1, i2;
+        box_test2(r.h, nd, i1, i2, t1, t2);
+        const bool both = i1 && i2;
+        const bool goLeft = both ? (t1 < t2) : i1;
+        push = both && s.top < 15;  // a push onto a full stack is dropped
+        s.dropped += (both && !push) ? 1u : 0u;
+        pIdx = goLeft ? nd.q3.y : nd.q3.x;
+        pLeaf = goLeft ? nd.q3.w : nd.q3.z;
+        pT = __float_as_uint(goLeft ? t2 : t1);
+        pop = !i1 && !i2;
+        nIdx = goLeft ? nd.q3.x : nd.q3.y;
+        nLeaf = (goLeft ? nd.q3.z : nd.q3.w) != 0u;
+        nT = goLeft ? t1 : t2;
+    } else if (s.cBlas) {
+        const uint32_t li = s.cOff * 1024u + s.cIdx;
+        ++s.tests;
+        float tt;
+        if (watertight(r.tr, r.org, f3_of(rec.a), f3_of(rec.b), f3_of(rec.c), s.t, tt, s.u, s.v, s.errT) && tt < s.t) {
+            s.t = tt;
+            s.hitIdx = (int)li;
+            s.hitU = s.u; s.hitV = s.v; s.hitErrT = s.errT;
+        }
+        pop = true;
+    } else {  // TLAS leaf: continue at the root of that batch's BLAS, whose record is already here
+        tlasLeaf = true;
+        nLeaf = false;
+        nBlas = true;
+        nOff = s.cIdx;
+        nIdx = 0u;
+    }
+    if (pop) {  // TestForFinish (traverse.h:88-105); no push happened in this iteration
+        int top = s.top;
+        do {
+            if (top < 0) {
+                s.top = top;
+                return true;
+            }
+            const unsigned long long e = (kLds == 16 || top < kLds) ? *(volatile LdsU64*)(&stk[top * stride])
+                                                                    : deep_get(*deep, top - kLds);
+            const uint32_t a = (uint32_t)e;
+            nT = __uint_as_float((uint32_t)(e >> 32));
+            --top;
+            nIdx = a & 0x7FFFu;
+            nOff = (a >> 15) & 0x7FFFu;
+            nBlas = (a >> 30) & 1u;
+            nLeaf = (a >> 31) & 1u;
+        } while (nT > s.t);
+        s.top = top;
+    }
+    // the next iteration's record, before the bookkeeping below
+    if (!tlasLeaf) rec = load_rec(sc, nLeaf, nBlas, nIdx, nOff);
+    if (push) {
+        const uint2 entry = make_uint2((pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) | ((s.cBlas ? 1u : 0u) << 30) |
+                                           ((pLeaf ? 1u : 0u) << 31),
+                                       pT);
+        if (kLds == 16 || s.top + 1 < kLds) stk[(s.top + 1) * stride] = entry;
+        else deep_set(*deep, s.top + 1 - kLds, entry);
+        ++s.top;
+    }
+    s.cIdx = nIdx;
+    s.cOff = nOff;
+    s.cBlas = nBlas;
+    s.cLeaf = nLeaf;
+    s.cT = nT;
+    return false;
+}
+
 // Wave-level leaf batching for the lanes of one wave that each run their own traversal: a lane
 // whose next step is a BLAS leaf (a triangle test, ~1 iteration in 20) waits until enough lanes
 // are at leaves, so the triangle-test code runs for many lanes at once instead of in nearly

@@ -27,9 +27,11 @@ class FramePipeline:
         self.rt, self.device, self.pipelined = rt, device, pipelined
         self.world, self.rank = world, rank
         if pipelined:  # the trace chain outranks the denoise stream
+            import os
             lo, hi = torch.cuda.Stream.priority_range()
-            self.main = torch.cuda.Stream(device, priority=hi)
-            self.post = torch.cuda.Stream(device, priority=lo)
+            pick = {"lo": lo, "hi": hi, "0": 0}
+            self.main = torch.cuda.Stream(device, priority=pick.get(os.environ.get("RTX_MAIN_PRIO", "hi"), hi))
+            self.post = torch.cuda.Stream(device, priority=pick.get(os.environ.get("RTX_POST_PRIO", "lo"), lo))
             torch.cuda.set_stream(self.main)
         else:
             self.main, self.post = torch.cuda.current_stream(device), None

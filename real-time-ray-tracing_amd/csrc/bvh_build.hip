@@ -3,11 +3,11 @@
 // Replaces the reference's six launches (bvh.cu:7-97):
 //   UpdateSceneGeometry -> RadixSort -> BuildLBVH   (per 1024-triangle BLAS batch)
 //   UpdateTLAS -> RadixSort -> BuildLBVH             (one TLAS over the batch roots)
-// with ONE kernel: a 1024-thread workgroup (16 wave64s) builds a whole batch inside LDS
-// (gather -> batch box -> Morton -> 5x6-bit LSD radix sort -> Karras topology -> bottom-up
-// boxes), and the last workgroup to finish (agent-scope release/acquire on an arrival
-// counter, cdna_hip_programming.md Guideline 16) builds the TLAS with the same LDS
-// machinery.  Results are bit-identical to the reference semantics (oracle/bvh.cpp):
+// with ONE kernel: a workgroup builds a whole batch inside LDS (gather -> batch box -> Morton ->
+// 5x6-bit LSD radix sort -> Karras topology -> bottom-up boxes), and the last workgroup to finish
+// (agent-scope release/acquire on an arrival counter, cdna_hip_programming.md Guideline 16) builds
+// the TLAS with the same LDS machinery.  Results are bit-identical to the reference semantics
+// (oracle/bvh.cpp):
 //   * Morton codes: same fp32 ops, no contraction, saturating float->uint
 //   * sort: stable LSD radix on the low 30 bits (all codes < 2^30; padding keys
 //     0xFFFFFFFF sit at the highest positions, so stability keeps them last) == the
@@ -16,6 +16,16 @@
 //   * boxes: a pure function of the topology; evaluated by atomic bottom-up climbing in LDS
 //   * TLAS scene box: the reference's reduction skips thread slots s with s mod 64 >= 32
 //     (no +32 merge, updateGeometry.cuh:317-336), i.e. batches b with (b & 255) >= 128.
+//
+// Two workgroup shapes (kThr threads, kPer = 1024 / kThr batch elements per thread):
+//   kThr 1024  16 waves, one element per thread, leaf boxes in LDS (63 KB): two workgroups fill a
+//              CU's 32 wave slots — the default scene's 60 batches, one per CU;
+//   kThr 512   8 waves, two elements per thread, leaf boxes read back from the AABB array, 38 KB of
+//              LDS: four workgroups per CU, so 937 batches (the 958,720-triangle scene, BASELINE
+//              config 4) run in one round on 256 CUs instead of two rounds of 512.
+// The launcher takes 512 when the batches would not fit 2 per CU.
+#include <stdlib.h>
+
 #include "bvh_kernels.h"
 #include "rt_device.h"
 
@@ -23,18 +33,29 @@ using namespace rtd;
 
 namespace {
 
-constexpr int kT = 1024;  // threads per workgroup == triangles per batch (kernel.cuh:579)
+constexpr int kBatch = 1024;  // triangles per batch (kernel.cuh:579)
 
+typedef uint32_t __attribute__((may_alias)) U32Alias;
+
+template <int kThr>
 struct Lds {
-    uint32_t key[2][kT];
-    uint16_t idx[2][kT];
-    uint32_t hist[64 * 16];   // [digit][wave]
-    float leaf[kT][6];        // leaf boxes by original local index (min xyz, max xyz)
-    float merged[kT][6];      // merged box of each internal node
-    uint16_t childL[kT], childR[kT];  // bit 15 = leaf
-    uint16_t parent[kT];
-    uint32_t arrive[kT];
-    float red[16][6];
+    static constexpr bool kLeafLds = kThr == kBatch;
+    // region A: the sort's second key / index buffers and its histogram ([digit][64-element
+    // virtual wave]); after the sort, the node info of the Karras topology and the refit:
+    // per internal node [0] left child, [1] right child (bit 15 = leaf), [2] parent,
+    // [3] arrivals — one 8-byte word, so the refit reads children and parent in one ds_read_b64
+    union {
+        struct {
+            uint32_t key0[kBatch];
+            uint16_t idx0[kBatch];
+            uint16_t hist[64 * 16];
+        } srt;
+        uint16_t info[kBatch][4];
+    } a;
+    uint32_t key1[kBatch];  // sorted keys (the sort ends in buffer 1)
+    uint16_t idx1[kBatch];
+    float merged[kBatch][6];  // merged box of each internal node; rows 0..15: the box reductions
+    float leaf[kLeafLds ? kBatch : 1][6];  // leaf boxes by original local index (kThr 1024)
     uint32_t isLast;
 };
 
@@ -47,6 +68,13 @@ RT_DEV Box load_box(const float* p) {
 RT_DEV void store_box(float* p, const Box& b) {
     p[0] = b.mn.x; p[1] = b.mn.y; p[2] = b.mn.z;
     p[3] = b.mx.x; p[4] = b.mx.y; p[5] = b.mx.z;
+}
+
+// leaf box k: from LDS (kThr 1024) or from the AABB array this launch wrote (leafG)
+template <int kThr>
+RT_DEV Box leaf_box(const Lds<kThr>& s, const float* leafG, uint32_t k) {
+    if (Lds<kThr>::kLeafLds) return load_box(s.leaf[k]);
+    return load_box(leafG + 6 * (size_t)k);
 }
 
 RT_DEV uint32_t morton3(uint32_t x, uint32_t y, uint32_t z) {
@@ -64,64 +92,101 @@ RT_DEV uint32_t morton_of(F3 c, const Box& s) {
     return morton3(sat_u32(u.x * 1023.0f), sat_u32(u.y * 1023.0f), sat_u32(u.z * 1023.0f));
 }
 
-// wave64 butterfly min/max; min/max are exact, so the order cannot change the bits
+// t through a VALU move the compiler cannot see through, so an address derived from it is
+// recomputed where it is used instead of being kept (and spilled) from an earlier use
+RT_DEV int opaque_lane(int t) {
+    int r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(t));
+    return r;
+}
+
+RT_DEV float xor_lane(float v, int lane, int off) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute((lane ^ off) << 2, __float_as_int(v)));
+}
+
+// wave64 butterfly min/max; min/max are exact, so the order cannot change the bits.  The lane
+// index is opaque per call: the kernel reduces twice (batch box, TLAS box), and shared shuffle
+// addresses kept live between the two were spilled at the 64-VGPR bound.
 RT_DEV Box wave_reduce(Box b) {
+    const int lane = opaque_lane((int)__lane_id());
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-        b.mn.x = fmn(b.mn.x, __shfl_xor(b.mn.x, off));
-        b.mn.y = fmn(b.mn.y, __shfl_xor(b.mn.y, off));
-        b.mn.z = fmn(b.mn.z, __shfl_xor(b.mn.z, off));
-        b.mx.x = fmx(b.mx.x, __shfl_xor(b.mx.x, off));
-        b.mx.y = fmx(b.mx.y, __shfl_xor(b.mx.y, off));
-        b.mx.z = fmx(b.mx.z, __shfl_xor(b.mx.z, off));
+        b.mn.x = fmn(b.mn.x, xor_lane(b.mn.x, lane, off));
+        b.mn.y = fmn(b.mn.y, xor_lane(b.mn.y, lane, off));
+        b.mn.z = fmn(b.mn.z, xor_lane(b.mn.z, lane, off));
+        b.mx.x = fmx(b.mx.x, xor_lane(b.mx.x, lane, off));
+        b.mx.y = fmx(b.mx.y, xor_lane(b.mx.y, lane, off));
+        b.mx.z = fmx(b.mx.z, xor_lane(b.mx.z, lane, off));
     }
     return b;
 }
 
-// whole-workgroup box reduction (every thread returns the result)
-RT_DEV Box block_reduce(Lds& s, Box b) {
+// whole-workgroup box reduction (every thread returns the result); the per-wave partials go to
+// the sort histogram's area of region A, which the sort only clears after its first barrier (and
+// the key0 / idx0 writes after a reduction do not reach)
+template <int kThr>
+RT_DEV Box block_reduce(Lds<kThr>& s, Box b) {
+    constexpr int kW = kThr / 64;
+    static_assert(kW * 6 * 4 <= (int)sizeof(s.a.srt.hist), "reduction partials fit the histogram area");
+    float* red = (float*)s.a.srt.hist;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     b = wave_reduce(b);
-    if (lane == 0) store_box(s.red[w], b);
+    if (lane == 0) store_box(red + 6 * w, b);
     __syncthreads();
-    Box r = load_box(s.red[0]);
+    Box r = load_box(red);
 #pragma unroll
-    for (int k = 1; k < 16; ++k) {
-        Box o = load_box(s.red[k]);
+    for (int k = 1; k < kW; ++k) {
+        Box o = load_box(red + 6 * k);
         r.mn = min3(r.mn, o.mn);
         r.mx = max3(r.mx, o.mx);
     }
     return r;
 }
 
-// Stable LSD radix sort of s.key[0]/s.idx[0] (1024 entries) on bits 0..29, 6 bits per pass.
-// Within a wave, lanes with equal digits are ranked by a 6-ballot match mask; waves are
-// ranked through a [digit][wave] histogram scanned by wave 0.  Result in s.key[1]/s.idx[1].
-RT_DEV void radix_sort(Lds& s) {
+// Stable LSD radix sort of the 1024 entries key0/idx0 on bits 0..29, 6 bits per pass; result in
+// key1/idx1.  Element e sits in 64-element virtual wave e / 64: thread t of wave w holds elements
+// t + j * kThr (virtual waves w + j * kW).  Within a virtual wave, elements with equal digits are
+// ranked by a 6-ballot match mask; virtual waves are ranked through a [digit][16] histogram
+// scanned by wave 0.
+template <int kThr>
+RT_DEV void radix_sort(Lds<kThr>& s) {
+    constexpr int kW = kThr / 64, kPer = kBatch / kThr;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    int src = 0;
+    uint16_t* hist = s.a.srt.hist;
 #pragma unroll 1
     for (int pass = 0; pass < 5; ++pass) {
-        const int dst = src ^ 1;
-        const uint32_t k = s.key[src][t];
-        const uint16_t ix = s.idx[src][t];
-        const uint32_t d = (k >> (6 * pass)) & 63u;
-        s.hist[lane * 16 + w] = 0u;
-        uint64_t m = ~0ull;
+        const bool fromA = (pass & 1) == 0;  // passes 0, 2, 4 read buffer 0 (region A)
+        const uint32_t* ksrc = fromA ? s.a.srt.key0 : s.key1;
+        const uint16_t* isrc = fromA ? s.a.srt.idx0 : s.idx1;
+        uint32_t* kdst = fromA ? s.key1 : s.a.srt.key0;
+        uint16_t* idst = fromA ? s.idx1 : s.a.srt.idx0;
+        uint32_t k[kPer], d[kPer], rank[kPer];
+        uint16_t ix[kPer];
 #pragma unroll
-        for (int b = 0; b < 6; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bal = __ballot(bit);
-            m &= bit ? bal : ~bal;
+        for (int j = 0; j < kPer; ++j) {
+            k[j] = ksrc[t + j * kThr];
+            ix[j] = isrc[t + j * kThr];
+            d[j] = (k[j] >> (6 * pass)) & 63u;
+            hist[lane * 16 + w + j * kW] = 0u;  // this wave's columns, zeroed before its counts
         }
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (rank == 0) s.hist[d * 16 + w] = (uint32_t)__popcll(m);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            uint64_t m = ~0ull;
+#pragma unroll
+            for (int b = 0; b < 6; ++b) {
+                const bool bit = (d[j] >> b) & 1u;
+                const uint64_t bal = __ballot(bit);
+                m &= bit ? bal : ~bal;
+            }
+            rank[j] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (rank[j] == 0) hist[d[j] * 16 + w + j * kW] = (uint16_t)__popcll(m);
+        }
         __syncthreads();
         if (w == 0) {
             uint32_t run[16];
             uint32_t sum = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) { run[j] = sum; sum += s.hist[lane * 16 + j]; }
+            for (int j = 0; j < 16; ++j) { run[j] = sum; sum += hist[lane * 16 + j]; }
             uint32_t incl = sum;
 #pragma unroll
             for (int off = 1; off < 64; off <<= 1) {
@@ -130,14 +195,16 @@ RT_DEV void radix_sort(Lds& s) {
             }
             const uint32_t base = incl - sum;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) s.hist[lane * 16 + j] = base + run[j];
+            for (int j = 0; j < 16; ++j) hist[lane * 16 + j] = (uint16_t)(base + run[j]);
         }
         __syncthreads();
-        const uint32_t pos = s.hist[d * 16 + w] + rank;
-        s.key[dst][pos] = k;
-        s.idx[dst][pos] = ix;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const uint32_t pos = hist[d[j] * 16 + w + j * kW] + rank[j];
+            kdst[pos] = k[j];
+            idst[pos] = ix[j];
+        }
         __syncthreads();
-        src = dst;
     }
 }
 
@@ -147,11 +214,11 @@ RT_DEV int lcp(const uint32_t* key, int n, uint32_t m0, int j) {
     return x == 0u ? 32 : __builtin_clz(x);
 }
 
-// Karras 2012 topology over s.key[1][0..n) (buildBVH.cuh:60-134), children into LDS.
-RT_DEV void karras(Lds& s, int n) {
-    const int i = threadIdx.x;
-    if (i >= n - 1) return;
-    const uint32_t* key = s.key[1];
+// Karras 2012 topology over key1[0..n) (buildBVH.cuh:60-134) of internal node i, into the info
+// words; also clears node i's arrival count for the refit.
+template <int kThr>
+RT_DEV void karras_node(Lds<kThr>& s, int n, int i) {
+    const uint32_t* key = s.key1;
     const uint32_t m0 = key[i];
     const int dl = lcp(key, n, m0, i - 1);
     const int dr = lcp(key, n, m0, i + 1);
@@ -174,88 +241,159 @@ RT_DEV void karras(Lds& s, int n) {
     const int gamma = i + sp * d + (d < 0 ? d : 0);
     const int lo = i < j ? i : j, hi = i < j ? j : i;
     if (lo == gamma) {
-        s.childL[i] = (uint16_t)(0x8000u | s.idx[1][gamma]);
+        s.a.info[i][0] = (uint16_t)(0x8000u | s.idx1[gamma]);
     } else {
-        s.childL[i] = (uint16_t)gamma;
-        s.parent[gamma] = (uint16_t)i;
+        s.a.info[i][0] = (uint16_t)gamma;
+        s.a.info[gamma][2] = (uint16_t)i;
     }
     if (hi == gamma + 1) {
-        s.childR[i] = (uint16_t)(0x8000u | s.idx[1][gamma + 1]);
+        s.a.info[i][1] = (uint16_t)(0x8000u | s.idx1[gamma + 1]);
     } else {
-        s.childR[i] = (uint16_t)(gamma + 1);
-        s.parent[gamma + 1] = (uint16_t)i;
+        s.a.info[i][1] = (uint16_t)(gamma + 1);
+        s.a.info[gamma + 1][2] = (uint16_t)i;
     }
+    s.a.info[i][3] = 0u;
 }
 
-RT_DEV void store_node(Node* dst, const Box& l, const Box& r, uint16_t cl, uint16_t cr) {
+template <int kThr>
+RT_DEV void karras(Lds<kThr>& s, int n) {
+#pragma unroll 1
+    for (int i = threadIdx.x; i < n - 1; i += kThr) karras_node(s, n, i);
+}
+
+RT_DEV void store_node(Node* dst, const Box& l, const Box& r, uint32_t cl, uint32_t cr) {
     Node nd;
     nd.q0 = make_float4(l.mn.x, l.mn.y, l.mn.z, l.mx.x);
     nd.q1 = make_float4(l.mx.y, l.mx.z, r.mn.x, r.mn.y);
     nd.q2 = make_float4(r.mn.z, r.mx.x, r.mx.y, r.mx.z);
-    nd.q3 = make_uint4(cl & 0x7FFFu, cr & 0x7FFFu, cl >> 15, cr >> 15);
+    nd.q3 = make_uint4(cl & 0x7FFFu, cr & 0x7FFFu, (cl >> 15) & 1u, (cr >> 15) & 1u);
     *dst = nd;
 }
 
+template <int kThr>
+RT_DEV uint64_t info_of(const Lds<kThr>& s, int k) {
+    return *(const volatile unsigned long long*)&s.a.info[k][0];
+}
+
 // Bottom-up boxes: nodes whose children are both leaves start climbing; a parent with two
-// internal children is finished by the second arrival (LDS counter, acq_rel workgroup
-// scope); a parent with one leaf child is finished by its only internal child.
-RT_DEV void refit(Lds& s, int n, Node* nodes) {
-    const int i = threadIdx.x;
+// internal children is finished by the second arrival (LDS counter, acq_rel workgroup scope); a
+// parent with one leaf child is finished by its only internal child.
+//
+// A climbing lane carries the box it just merged to the parent: per step it reads the parent's
+// info word (children + grandparent), bumps the arrival count (two internal children only), and
+// reads the one sibling box it does not hold.  The boxes are the reference's
+// AABBCompact(left, right) / GetMerged values; only the second arrival at a parent reads the
+// first one's box from LDS (published before its count update).
+struct Climb {
+    Box l, r;
+    uint64_t inf;
+    uint32_t cl, cr;
+    int cur;
+    bool on;
+};
+
+template <int kThr>
+RT_DEV void climb_start(const Lds<kThr>& s, const float* leafG, int n, int i, Climb& c) {
+    c.on = false;
+    c.cur = i;
+    if (i >= n - 1) return;
+    c.inf = info_of(s, i);
+    c.cl = (uint32_t)c.inf & 0xFFFFu;
+    c.cr = (uint32_t)(c.inf >> 16) & 0xFFFFu;
+    if (!((c.cl & 0x8000u) && (c.cr & 0x8000u))) return;
+    c.l = leaf_box(s, leafG, c.cl & 0x7FFFu);
+    c.r = leaf_box(s, leafG, c.cr & 0x7FFFu);
+    c.on = true;
+}
+
+template <int kThr>
+RT_DEV void climb_step(Lds<kThr>& s, const float* leafG, Node* nodes, Climb& c) {
+    const Box m = box_merge(c.l, c.r);
+    store_node(nodes + c.cur, c.l, c.r, c.cl, c.cr);
+    if (c.cur == 0) {
+        c.on = false;
+        return;
+    }
+    const int p = (int)(c.inf >> 32) & 0xFFFF;
+    const uint64_t pinf = info_of(s, p);
+    const uint32_t pl = (uint32_t)pinf & 0xFFFFu, pr = (uint32_t)(pinf >> 16) & 0xFFFFu;
+    const bool curLeft = pl == (uint32_t)c.cur;  // cur is internal: its reference has no leaf bit
+    const uint32_t sib = curLeft ? pr : pl;
+    Box sb;
+    if (sib & 0x8000u) {
+        sb = leaf_box(s, leafG, sib & 0x7FFFu);
+    } else {  // two internal children: the second arrival finishes the parent
+        store_box(s.merged[c.cur], m);
+        const uint32_t old = __hip_atomic_fetch_add((U32Alias*)&s.a.info[p][2], 0x10000u, __ATOMIC_ACQ_REL,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((old >> 16) == 0u) {
+            c.on = false;
+            return;
+        }
+        sb = load_box(s.merged[sib]);
+    }
+    c.l = curLeft ? m : sb;
+    c.r = curLeft ? sb : m;
+    c.cl = pl;
+    c.cr = pr;
+    c.inf = pinf;
+    c.cur = p;
+}
+
+// The climbs of this thread's internal nodes (kPer of them, one after the other).
+template <int kThr>
+RT_DEV void refit(Lds<kThr>& s, const float* leafG, int n, Node* nodes) {
+    constexpr int kPer = kBatch / kThr;
+    const int t = threadIdx.x;
     if (n == 1) {
-        if (i == 0) {
+        if (t == 0) {
             Box zero; zero.mn = f3(0.0f); zero.mx = f3(0.0f);
-            store_node(nodes, load_box(s.leaf[0]), zero, 0x8000u, 0x8000u);
+            store_node(nodes, leaf_box(s, leafG, 0u), zero, 0x8000u, 0x8000u);
         }
         return;
     }
-    if (i >= n - 1) return;
-    if (!((s.childL[i] & 0x8000u) && (s.childR[i] & 0x8000u))) return;
-    int cur = i;
-    for (int guard = 0; guard < kT; ++guard) {  // a valid tree ends at the root in < n steps
-        const uint16_t cl = s.childL[cur], cr = s.childR[cur];
-        const Box l = (cl & 0x8000u) ? load_box(s.leaf[cl & 0x7FFFu]) : load_box(s.merged[cl]);
-        const Box r = (cr & 0x8000u) ? load_box(s.leaf[cr & 0x7FFFu]) : load_box(s.merged[cr]);
-        store_box(s.merged[cur], box_merge(l, r));
-        store_node(nodes + cur, l, r, cl, cr);
-        if (cur == 0) break;
-        const int p = s.parent[cur];
-        const bool twoInternal = !(s.childL[p] & 0x8000u) && !(s.childR[p] & 0x8000u);
-        if (twoInternal) {
-            const uint32_t old = __hip_atomic_fetch_add(&s.arrive[p], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (old == 0u) break;
-        }
-        cur = p;
+#pragma unroll 1
+    for (int j = 0; j < kPer; ++j) {
+        Climb c;
+        climb_start(s, leafG, n, t + j * kThr, c);
+        for (int guard = 0; guard < kBatch && c.on; ++guard)  // a valid tree ends at the root in < n steps
+            climb_step(s, leafG, nodes, c);
     }
 }
 
-// Sort keys already in s.key[0]/s.idx[0] and build the tree of n leaves into `nodes`.
-RT_DEV void sort_and_build(Lds& s, int n, uint32_t* mortonOut, uint32_t* reorderOut, Node* nodes) {
+// Sort the keys in key0/idx0 and build the tree of n leaves into `nodes`.
+template <int kThr>
+RT_DEV void sort_and_build(Lds<kThr>& s, const float* leafG, int n, uint32_t* mortonOut, uint32_t* reorderOut,
+                           Node* nodes) {
     __syncthreads();
     radix_sort(s);
-    const int t = threadIdx.x;
-    mortonOut[t] = s.key[1][t];
-    reorderOut[t] = s.idx[1][t];
+#pragma unroll
+    for (int j = 0; j < kBatch / kThr; ++j) {
+        const int e = threadIdx.x + j * kThr;
+        mortonOut[e] = s.key1[e];
+        reorderOut[e] = s.idx1[e];
+    }
     karras(s, n);
     __syncthreads();
 #if !(defined(RTX_BVH_ABL) && RTX_BVH_ABL == 3)
-    refit(s, n, nodes);  // (ablation 3: no refit; timing only)
+    refit(s, leafG, n, nodes);  // (ablation 3: no refit; timing only)
 #endif
 }
 
 // The TLAS of a scene of at most 64 batches, built by wave 0 of the last workgroup alone: the
-// same results as the 1024-thread path (UpdateTLAS + RadixSort + BuildLBVH over B keys) without
+// same results as the workgroup path (UpdateTLAS + RadixSort + BuildLBVH over B keys) without
 // its ~20 workgroup barriers.  The stable sort is a rank count (keys below, plus equal keys of
 // lower index: a stable sort's position); the 1024 - B padding keys (0xFFFFFFFF) keep their
 // order after the real ones, as the radix sort leaves them.  LDS written by one lane and read by
 // another is ordered by wavefront-scope fences.
-RT_DEV void tlas_wave(Lds& s, const BvhBuildParams& P, uint32_t B) {
+template <int kThr>
+RT_DEV void tlas_wave(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
     const int lane = threadIdx.x;  // 0..63
     const Node* nodes = (const Node*)P.nodes;
-    s.arrive[lane] = 0u;
     Box rb = box_empty();
     F3 rc = f3(0.0f);
     if ((uint32_t)lane < B) {
-        const Node nd = nodes[(size_t)lane * kT];
+        const Node nd = nodes[(size_t)lane * kBatch];
         Box l, r;
         l.mn = f3(nd.q0.x, nd.q0.y, nd.q0.z); l.mx = f3(nd.q0.w, nd.q1.x, nd.q1.y);
         r.mn = f3(nd.q1.z, nd.q1.w, nd.q2.x); r.mx = f3(nd.q2.y, nd.q2.z, nd.q2.w);
@@ -263,7 +401,7 @@ RT_DEV void tlas_wave(Lds& s, const BvhBuildParams& P, uint32_t B) {
         rc = (rb.mx + rb.mn) / 2.0f;
         store_box(P.tlasAabbs + 6 * (size_t)lane, rb);
     }
-    store_box(s.leaf[lane], rb);
+    if (Lds<kThr>::kLeafLds) store_box(s.leaf[lane], rb);
     // the quirk reduction keeps slots with (s & 255) < 128: every slot below 64
     const Box quirk = wave_reduce(rb);
     const uint32_t key = (uint32_t)lane < B ? morton_of(rc, quirk) : 0xFFFFFFFFu;
@@ -274,78 +412,87 @@ RT_DEV void tlas_wave(Lds& s, const BvhBuildParams& P, uint32_t B) {
         const uint32_t kj = __shfl(key, j);
         rank += (kj < key || (kj == key && j < lane)) ? 1u : 0u;
     }
-    s.key[1][rank] = key;
-    s.idx[1][rank] = (uint16_t)lane;
-    for (int t = lane; t < kT; t += 64) {
+    s.key1[rank] = key;
+    s.idx1[rank] = (uint16_t)lane;
+    for (int t = lane; t < kBatch; t += 64) {
         P.tlasMorton[t] = t < 64 ? 0u : 0xFFFFFFFFu;  // rows < 64 rewritten below
         P.tlasReorder[t] = (uint32_t)t;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    P.tlasMorton[lane] = s.key[1][lane];
-    P.tlasReorder[lane] = s.idx[1][lane];
+    P.tlasMorton[lane] = s.key1[lane];
+    P.tlasReorder[lane] = s.idx1[lane];
     karras(s, (int)B);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    refit(s, (int)B, (Node*)P.tlasNodes);
+    refit(s, P.tlasAabbs, (int)B, (Node*)P.tlasNodes);
     if (lane == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
 
-// t through a VALU move the compiler cannot see through, so an LDS slot address derived from it is
-// recomputed where it is used instead of being kept (and spilled) from an earlier use
-RT_DEV int opaque_lane(int t) {
-    int r;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(t));
-    return r;
-}
-
-__global__ __launch_bounds__(kT, 8) void k_build_bvh(BvhBuildParams P) {  // 8 waves/SIMD = 2 workgroups per CU: <= 64 VGPRs
-    __shared__ Lds s;
+// kThr 1024: 8 waves/SIMD = 2 workgroups per CU; kThr 512: 4 workgroups per CU.  Either way <= 64
+// VGPRs.
+template <int kThr>
+__global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
+    constexpr int kPer = kBatch / kThr;
+    __shared__ Lds<kThr> s;
     const int t = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const uint32_t B = P.batchCount;
-    const uint32_t start = b * kT;
-    const uint32_t cnt = (b + 1 < B) ? (uint32_t)kT : P.triCount - (B - 1) * kT;  // init.cu:129-130
+    const uint32_t start = b * kBatch;
+    const uint32_t cnt = (b + 1 < B) ? (uint32_t)kBatch : P.triCount - (B - 1) * kBatch;  // init.cu:129-130
     const uint32_t active = (((cnt - 1) >> 2) + 1) << 2;  // triangles of threads with tid*4 <= cnt-1
+    const float* leafG = P.aabbs + 6 * (size_t)start;
 
-    // ---- gather triangles, leaf boxes, centroids (updateGeometry.cuh:104-184)
-    Box bx = box_empty();
-    F3 center = f3(0.0f);
-    if ((uint32_t)t < active) {
-        const uint32_t g = start + t;
-        const uint32_t i0 = P.indices[3 * g], i1 = P.indices[3 * g + 1], i2 = P.indices[3 * g + 2];
-        const F3 v1 = f3(P.vertices[3 * i0], P.vertices[3 * i0 + 1], P.vertices[3 * i0 + 2]);
-        const F3 v2 = f3(P.vertices[3 * i1], P.vertices[3 * i1 + 1], P.vertices[3 * i1 + 2]);
-        const F3 v3 = f3(P.vertices[3 * i2], P.vertices[3 * i2 + 1], P.vertices[3 * i2 + 2]);
-        P.triPos[3 * g + 0] = make_float4(v1.x, v1.y, v1.z, 0.0f);
-        P.triPos[3 * g + 1] = make_float4(v2.x, v2.y, v2.z, 0.0f);
-        P.triPos[3 * g + 2] = make_float4(v3.x, v3.y, v3.z, 0.0f);
-        P.triNrm[3 * g + 0] = make_float4(P.normals[3 * i0], P.normals[3 * i0 + 1], P.normals[3 * i0 + 2], 0.0f);
-        P.triNrm[3 * g + 1] = make_float4(P.normals[3 * i1], P.normals[3 * i1 + 1], P.normals[3 * i1 + 2], 0.0f);
-        P.triNrm[3 * g + 2] = make_float4(P.normals[3 * i2], P.normals[3 * i2 + 1], P.normals[3 * i2 + 2], 0.0f);
-        F3 mn = min3(v1, min3(v2, v3));
-        F3 mx = max3(v1, max3(v2, v3));
-        const F3 diff = max3(mx - mn, kMachineEps * mx);
-        mx = mn + diff;
-        bx.mn = mn;
-        bx.mx = mx;
-        store_box(P.aabbs + 6 * (size_t)g, bx);
-        center = (v1 + v2 + v3) / 3.0f;
+    // ---- gather triangles, leaf boxes, centroids (updateGeometry.cuh:104-184); the centroids wait
+    // for the batch box in `merged` (free until the refit)
+    Box own = box_empty();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t e = (uint32_t)(t + j * kThr);
+        Box bx = box_empty();
+        F3 center = f3(0.0f);
+        if (e < active) {
+            const uint32_t g = start + e;
+            const uint32_t i0 = P.indices[3 * g], i1 = P.indices[3 * g + 1], i2 = P.indices[3 * g + 2];
+            const F3 v1 = f3(P.vertices[3 * i0], P.vertices[3 * i0 + 1], P.vertices[3 * i0 + 2]);
+            const F3 v2 = f3(P.vertices[3 * i1], P.vertices[3 * i1 + 1], P.vertices[3 * i1 + 2]);
+            const F3 v3 = f3(P.vertices[3 * i2], P.vertices[3 * i2 + 1], P.vertices[3 * i2 + 2]);
+            P.triPos[3 * g + 0] = make_float4(v1.x, v1.y, v1.z, 0.0f);
+            P.triPos[3 * g + 1] = make_float4(v2.x, v2.y, v2.z, 0.0f);
+            P.triPos[3 * g + 2] = make_float4(v3.x, v3.y, v3.z, 0.0f);
+            P.triNrm[3 * g + 0] = make_float4(P.normals[3 * i0], P.normals[3 * i0 + 1], P.normals[3 * i0 + 2], 0.0f);
+            P.triNrm[3 * g + 1] = make_float4(P.normals[3 * i1], P.normals[3 * i1 + 1], P.normals[3 * i1 + 2], 0.0f);
+            P.triNrm[3 * g + 2] = make_float4(P.normals[3 * i2], P.normals[3 * i2 + 1], P.normals[3 * i2 + 2], 0.0f);
+            F3 mn = min3(v1, min3(v2, v3));
+            F3 mx = max3(v1, max3(v2, v3));
+            const F3 diff = max3(mx - mn, kMachineEps * mx);
+            mx = mn + diff;
+            bx.mn = mn;
+            bx.mx = mx;
+            store_box(P.aabbs + 6 * (size_t)g, bx);
+            center = (v1 + v2 + v3) / 3.0f;
+        }
+        if (Lds<kThr>::kLeafLds) store_box(s.leaf[e], bx);
+        s.merged[e][0] = center.x;
+        s.merged[e][1] = center.y;
+        s.merged[e][2] = center.z;
+        own.mn = min3(own.mn, bx.mn);  // exact min / max: the grouping cannot change the bits
+        own.mx = max3(own.mx, bx.mx);
     }
-    store_box(s.leaf[t], bx);
 
     // ---- batch box (updateGeometry.cuh:186-248) and Morton codes (:250-261)
-    const Box scene = block_reduce(s, bx);
-    s.key[0][t] = ((uint32_t)t < active) ? morton_of(center, scene) : 0xFFFFFFFFu;
-    s.idx[0][t] = (uint16_t)t;
+    const Box scene = block_reduce(s, own);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t e = (uint32_t)(t + j * kThr);
+        const F3 center = f3(s.merged[e][0], s.merged[e][1], s.merged[e][2]);
+        s.a.srt.key0[e] = (e < active) ? morton_of(center, scene) : 0xFFFFFFFFu;
+        s.a.srt.idx0[e] = (uint16_t)e;
+    }
     if (t == 0) store_box(P.batchSceneAabbs + 6 * (size_t)b, scene);
 
     Node* const nodes = (Node*)P.nodes;
-    // the refit's arrival counters, zeroed here (the sort's barriers order it before the refit)
-    // rather than at entry: the slot address would otherwise stay live across the gather, and at
-    // the 64-VGPR bound it was spilled to scratch
-    s.arrive[opaque_lane(t)] = 0u;
-    sort_and_build(s, (int)cnt, P.morton + start, P.reorder + start, nodes + start);
+    sort_and_build(s, leafG, (int)cnt, P.morton + start, P.reorder + start, nodes + start);
 
     // ---- arrival: the last workgroup builds the TLAS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -373,30 +520,57 @@ __global__ __launch_bounds__(kT, 8) void k_build_bvh(BvhBuildParams P) {  // 8 w
 #endif
 
     // ---- TLAS (UpdateTLAS, updateGeometry.cuh:264-364; then sort + Karras over B keys)
-    s.arrive[opaque_lane(t)] = 0u;
-    Box rb = box_empty();
-    F3 rc = f3(0.0f);
-    if ((uint32_t)t < B) {
-        const Node nd = nodes[(size_t)t * kT];
-        Box l, r;
-        l.mn = f3(nd.q0.x, nd.q0.y, nd.q0.z); l.mx = f3(nd.q0.w, nd.q1.x, nd.q1.y);
-        r.mn = f3(nd.q1.z, nd.q1.w, nd.q2.x); r.mx = f3(nd.q2.y, nd.q2.z, nd.q2.w);
-        rb = box_merge(l, r);
-        rc = (rb.mx + rb.mn) / 2.0f;
-        store_box(P.tlasAabbs + 6 * (size_t)t, rb);
+    Box rq = box_empty();  // this thread's contribution to the quirk reduction
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t e = (uint32_t)(t + j * kThr);
+        Box rb = box_empty();
+        if (e < B) {
+            const Node nd = nodes[(size_t)e * kBatch];
+            Box l, r;
+            l.mn = f3(nd.q0.x, nd.q0.y, nd.q0.z); l.mx = f3(nd.q0.w, nd.q1.x, nd.q1.y);
+            r.mn = f3(nd.q1.z, nd.q1.w, nd.q2.x); r.mx = f3(nd.q2.y, nd.q2.z, nd.q2.w);
+            rb = box_merge(l, r);
+            store_box(P.tlasAabbs + 6 * (size_t)e, rb);
+            if ((e & 255u) < 128u) {
+                rq.mn = min3(rq.mn, rb.mn);
+                rq.mx = max3(rq.mx, rb.mx);
+            }
+        }
+        if (Lds<kThr>::kLeafLds) store_box(s.leaf[e], rb);
     }
-    store_box(s.leaf[t], rb);
-    const Box contrib = ((uint32_t)t < B && (t & 255) < 128) ? rb : box_empty();
-    const Box quirk = block_reduce(s, contrib);
-    s.key[0][t] = ((uint32_t)t < B) ? morton_of(rc, quirk) : 0xFFFFFFFFu;
-    s.idx[0][t] = (uint16_t)t;
+    const Box quirk = block_reduce(s, rq);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t e = (uint32_t)(t + j * kThr);
+        uint32_t key = 0xFFFFFFFFu;
+        if (e < B) {  // the leaf centre from the box just stored (not held across the reduction)
+            const Box lb = leaf_box(s, P.tlasAabbs, e);
+            key = morton_of((lb.mx + lb.mn) / 2.0f, quirk);
+        }
+        s.a.srt.key0[e] = key;
+        s.a.srt.idx0[e] = (uint16_t)e;
+    }
     if (t == 0) store_box(P.tlasSceneAabb, quirk);
-    sort_and_build(s, (int)B, P.tlasMorton, P.tlasReorder, (Node*)P.tlasNodes);
+    sort_and_build(s, (const float*)P.tlasAabbs, (int)B, P.tlasMorton, P.tlasReorder, (Node*)P.tlasNodes);
     __syncthreads();
     if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Batches that fit two 1024-thread workgroups per CU take that shape; more take the 512-thread one,
+// four per CU ([render] bvhThreads, or RTX_BVH_THREADS=512|1024, forces one: tests and A/B).
 extern "C" hipError_t rtk_launch_build_bvh(const BvhBuildParams* p, hipStream_t stream) {
-    hipLaunchKernelGGL(k_build_bvh, dim3(p->batchCount), dim3(kT), 0, stream, *p);
+    static int forced = [] {
+        const char* a = getenv("RTX_BVH_THREADS");
+        return a ? atoi(a) : 0;
+    }();
+    int dev = 0, cus = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    const int want = p->threads ? (int)p->threads : forced;
+    const bool narrow = want == 512 || (want != 1024 && (int)p->batchCount > 2 * cus);
+    if (narrow) hipLaunchKernelGGL(k_build_bvh<512>, dim3(p->batchCount), dim3(512), 0, stream, *p);
+    else hipLaunchKernelGGL(k_build_bvh<1024>, dim3(p->batchCount), dim3(1024), 0, stream, *p);
     return hipGetLastError();
 }

@@ -23,6 +23,7 @@ struct BvhBuildParams {
     uint32_t* tlasReorder;     // [1024]
     void* tlasNodes;           // [B]
     uint32_t* counter;         // arrival counter, zero between launches
+    uint32_t threads;          // workgroup shape: 0 = by batch count, 512 or 1024 ([render] bvhThreads)
 };
 
 struct TraceCamera {

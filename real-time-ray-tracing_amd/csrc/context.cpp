@@ -322,6 +322,7 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
     ctx->chunkDim = rttoml::find_or_int(doc, "scene", "chunkDim", 1);
     ctx->meshFile = rttoml::find_or_string(doc, "scene", "meshFile", "");
     ctx->spp = rttoml::find_or_int(doc, "render", "spp", 1);
+    ctx->bvhThreads = rttoml::find_or_int(doc, "render", "bvhThreads", 0);  // LBVH workgroup shape (A/B, tests)
     ctx->device = rttoml::find_or_int(doc, "render", "device", -1);
     ctx->stripY0 = rttoml::find_or_int(doc, "render", "stripY0", 0);
     ctx->stripRows = rttoml::find_or_int(doc, "render", "stripRows", -1);
@@ -329,8 +330,9 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
     ctx->stripIndex = rttoml::find_or_int(doc, "render", "stripIndex", 0);
     ctx->materialOverride = rttoml::find_or_int(doc, "render", "materialOverride", -1);
     if (ctx->screenW <= 0 || ctx->screenH <= 0 || ctx->screenW > 16384 || ctx->screenH > 16384 || ctx->spp < 1 ||
-        ctx->spp > 64 || ctx->chunkDim < 1 || ctx->chunkDim > 8) {
-        g_createError = "invalid resolution / spp / chunkDim";
+        ctx->spp > 64 || ctx->chunkDim < 1 || ctx->chunkDim > 8 ||
+        (ctx->bvhThreads != 0 && ctx->bvhThreads != 512 && ctx->bvhThreads != 1024)) {
+        g_createError = "invalid resolution / spp / chunkDim / bvhThreads";
         delete ctx;
         return RT_ERR_ARG;
     }
@@ -615,6 +617,7 @@ int rt_build_bvh(rt_context* ctx) {
     p.tlasReorder = ctx->dTlasReorder;
     p.tlasNodes = ctx->dTlasNodes;
     p.counter = ctx->dCounter;
+    p.threads = (uint32_t)ctx->bvhThreads;
     HIP_TRY(ctx, rtk_launch_build_bvh(&p, stream));
     if (ctx->postStream) {
         HIP_TRY(ctx, hipEventRecord(ctx->buildDone[ctx->bvhSet], stream));

@@ -38,7 +38,10 @@ struct BvhBufs {
     uint32_t* counter = nullptr;
 };
 
-constexpr int kGbSets = 3;  // G-buffer / camera-output sets in flight with frame pipelining
+#ifndef RTX_GB_SETS  // A/B builds only (tools/abl_build.sh): 2..4; rtx_dist.h hosts assume 3
+#define RTX_GB_SETS 3
+#endif
+constexpr int kGbSets = RTX_GB_SETS;  // G-buffer / camera-output sets in flight with frame pipelining
 
 struct FrameResources {
     bool ready = false;
@@ -166,6 +169,7 @@ struct rt_context {
     int chunkDim = 1;
     std::string meshFile;  // [scene] meshFile: meshProcessor .bin instead of the procedural scene
     int spp = 1;
+    int bvhThreads = 0;  // LBVH workgroup shape: 0 = by batch count, 512 or 1024 ([render] bvhThreads)
     int stripY0 = 0, stripRows = -1;  // [render] stripY0/stripRows: screen-strip split
     int stripCount = 1, stripIndex = 0;  // [render] stripCount/stripIndex: interleaved row blocks (row_of)
     int device = -1;

@@ -443,8 +443,16 @@ inline bool one_round(uint32_t spp) { return spp >= 1 && ((int)spp + cam_sample_
 //
 // kOneRound: every sample wave runs one round (spp <= 4 except 3: the launcher checks), so the
 // round loop and its carried state compile away.
+#ifndef RTX_CAM_PF  // the camera rays' iterations as trav_step_pf (record one iteration ahead); A/B flag
+#define RTX_CAM_PF 0
+#endif
+#ifdef RTX_CAM_WPE  // ablation builds only: forced waves per SIMD
+#define RTX_CAM_ATTR __attribute__((amdgpu_waves_per_eu(RTX_CAM_WPE, RTX_CAM_WPE)))
+#else
+#define RTX_CAM_ATTR
+#endif
 template <bool kOneRound>
-__global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
+__global__ __launch_bounds__(256) RTX_CAM_ATTR void k_pt_camera(PathTraceParams P) {
     // stack entries in LDS (the rest in registers): 26 KB per workgroup, 6 workgroups per CU
     // (measured: 16 entries 4 per CU 0.948 ms/frame, 12 entries 5 per CU 0.918, 10 entries 6 per CU
     // 0.900; the default scene's rays hold at most 11 entries)
@@ -495,8 +503,14 @@ __global__ __launch_bounds__(256) void k_pt_camera(PathTraceParams P) {
                 trav_setup(sc, org, dir, tr);
                 trav_init(st);
                 DeepStack deep;
-                for (int it = 0; it < 1024; ++it)
-                    if (trav_step_t<kCamLds>(sc, tr, st, stk + tid, 256, &deep)) break;
+                if (RTX_CAM_PF) {
+                    TravRec trec = trav_first_rec(sc);
+                    for (int it = 0; it < 1024; ++it)
+                        if (trav_step_pf<kCamLds>(sc, tr, st, trec, stk + tid, 256, &deep)) break;
+                } else {
+                    for (int it = 0; it < 1024; ++it)
+                        if (trav_step_t<kCamLds>(sc, tr, st, stk + tid, 256, &deep)) break;
+                }
             }
             ++rays;
             if (P.statsOut) {
@@ -867,6 +881,14 @@ constexpr bool kChainStaticFirst = RTX_CHAIN_STATIC != 0;  // ablation: static f
 // Per sample the code is the one the separate kernels run (resume_entry, trav_step), so the
 // G-buffers are identical.  The hit records a wave reads in phase 2 are ones its own lanes wrote
 // (a workgroup-scope fence orders them), so no record crosses workgroups inside the launch.
+#ifndef RTX_CHAIN_PF  // the chain's traversals as trav_step_pf (record one iteration ahead); A/B flag
+#define RTX_CHAIN_PF 0
+#endif
+RT_DEV bool chain_step(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk) {
+    if (RTX_CHAIN_PF) return trav_step_pf<16>(sc, r, s, rec, stk, 256, nullptr);
+    return trav_step(sc, r, s, stk, 256);
+}
+
 __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
     __shared__ uint2 stk[16 * 256];
     __shared__ uint32_t sob[256];
@@ -896,6 +918,7 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
         uint32_t idx = 0;
         TravRay r;
         TravState s;
+        TravRec rec;  // RTX_CHAIN_PF: the record of the lane's next iteration
         r.org = f3(0.0f);
         trav_init(s);
 #pragma unroll 1
@@ -920,6 +943,7 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
                         const float4 o = q.rayO[idx], d = q.rayD[idx];
                         trav_setup(sc, f3(o.x, o.y, o.z), f3(d.x, d.y, d.z), r);
                         trav_init(s);
+                        if (RTX_CHAIN_PF) rec = trav_first_rec(sc);
                         active = true;
                         occlusion = (__float_as_uint(d.w) & kQShadowFlag) != 0u;
                     } else if (none) {
@@ -935,7 +959,7 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
             if (tail ? active : trav_lane_steps(active, s)) {
                 bool done = false;
                 do {
-                    done = trav_step(sc, r, s, stk + tid, 256) || s.iters >= 1024u || (occlusion && s.hitIdx >= 0);
+                    done = chain_step(sc, r, s, rec, stk + tid) || s.iters >= 1024u || (occlusion && s.hitIdx >= 0);
                 } while (tail && !done);
                 if (done) {
                     P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);
@@ -977,6 +1001,8 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
                     trav_setup(sc, f3(o.x, o.y, o.z), f3(d.x, d.y, d.z), r4);
                 }
                 trav_init(s4);
+                TravRec rec4;
+                if (RTX_CHAIN_PF) rec4 = trav_first_rec(sc);
                 const bool mine = act;
 #if defined(RTX_CHAIN_ABL) && RTX_CHAIN_ABL == 2
                 act = false;  // timing ablation: I4 rays not traced
@@ -984,12 +1010,12 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
                 if (nq4 < 16u) {  // few rays: plain per-lane loop (no ballots, no leaf batching)
 #pragma unroll 1
                     while (act)
-                        if (trav_step(sc, r4, s4, stk + tid, 256) || s4.iters >= 1024u || s4.hitIdx >= 0) act = false;
+                        if (chain_step(sc, r4, s4, rec4, stk + tid) || s4.iters >= 1024u || s4.hitIdx >= 0) act = false;
                 } else {
 #pragma unroll 1
                     while (__ballot(act) != 0ull) {
                         if (trav_lane_steps(act, s4)) {
-                            if (trav_step(sc, r4, s4, stk + tid, 256) || s4.iters >= 1024u || s4.hitIdx >= 0)
+                            if (chain_step(sc, r4, s4, rec4, stk + tid) || s4.iters >= 1024u || s4.hitIdx >= 0)
                                 act = false;
                         }
                     }

@@ -16,6 +16,10 @@
 
 using namespace rtd;
 
+#ifndef RTX_PRIM_PF  // 1: trav_run_pf (record one iteration ahead, while-while); 2: trav_step_pf; 0: neither
+#define RTX_PRIM_PF 1
+#endif
+
 #ifndef RTX_PRIMARY_WPE  // ablation builds only (tools/abl_build.sh): force waves per SIMD
 __global__ __launch_bounds__(256) void k_trace_primary(TracePrimaryParams P) {
 #else
@@ -43,7 +47,7 @@ void k_trace_primary(TracePrimaryParams P) {
     sc.nodes = (const Node*)P.nodes;
     sc.tlas = (const Node*)P.tlasNodes;
     HitInfo hi;
-    intersect<kLds>(sc, org, dir, stk + tid, 256, hi);
+    intersect<kLds, RTX_PRIM_PF>(sc, org, dir, stk + tid, 256, hi);
 
     const size_t p = (size_t)y * P.width + x;
     P.hitOut[p] = make_float4(hi.t, __int_as_float(hi.objectIdx), hi.u, hi.v);

@@ -33,6 +33,10 @@ constexpr bool kLeafBatch = RTX_LEAF_BATCH != 0;  // ablation: -DRTX_LEAF_BATCH=
 #define RTX_TRAV_PF 1
 #endif
 constexpr bool kPrefetch = RTX_TRAV_PF != 0;  // next record loaded one iteration ahead (ablation: 0)
+#ifndef RTX_TAIL_RUN
+#define RTX_TAIL_RUN 1
+#endif
+constexpr bool kTailRun = RTX_TAIL_RUN != 0;  // tail rays finished by trav_run_pf (ablation: 0)
 
 // one TraverseBvh iteration of this lane's ray (trav_step_pf, or trav_step_t without the prefetch)
 RT_DEV bool step(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk) {
@@ -104,13 +108,18 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
         const bool tail = f.resLo == f.resHi && f.drained == (1u << kParts) - 1u;
         if (tail || !kLeafBatch ? active : trav_lane_steps(active, s)) {
             bool done = false;
-            do {  // two steps per trip: the loop's refill / exec-mask bookkeeping once per two
-                done = step(sc, r, s, rec, stk + tid) || s.iters >= 1024u ||
-                       (occlusion && s.hitIdx >= 0);
-                if (!done && (tail || !kLeafBatch || trav_lane_steps(true, s)))
+            if (kPrefetch && kTailRun && tail) {  // the rest of the ray in one call (while-while)
+                trav_run_pf<16>(sc, r, s, rec, stk + tid, kTraceBlock, nullptr, occlusion);
+                done = true;
+            } else {
+                do {  // two steps per trip: the loop's refill / exec-mask bookkeeping once per two
                     done = step(sc, r, s, rec, stk + tid) || s.iters >= 1024u ||
                            (occlusion && s.hitIdx >= 0);
-            } while (tail && !done);
+                    if (!done && (tail || !kLeafBatch || trav_lane_steps(true, s)))
+                        done = step(sc, r, s, rec, stk + tid) || s.iters >= 1024u ||
+                               (occlusion && s.hitIdx >= 0);
+                } while (tail && !done);
+            }
             if (done) {
                 P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);
                 P.ws.hitErr[idx] = s.hitErrT;

@@ -546,8 +546,112 @@ RT_DEV void finalize_hit(const SceneView& sc, F3 org, F3 dir, float t, int hitId
     out.hit = hit;
 }
 
-// kLds as in trav_step_t: the stack entries kept in LDS (k_trace_primary keeps 10)
-template <int kLds = 16>
+// A whole traversal, from the lane's current state to its end, as nested loops (while-while,
+// Aila & Laine 2009): an inner loop over internal nodes — box test, the next record's load, the
+// push — and between its runs the leaf steps (the triangle test, or the TLAS leaf's switch to its
+// BLAS) and the pops.  A lone ray's internal-node iterations then skip the leaf and pop branches'
+// exec-mask work.  Each ray's iterations, pushes, drops, pops and counters are trav_step_pf's, and
+// it stops where `trav_step_pf(...) || s.iters >= 1024 || (occlusion && s.hitIdx >= 0)` would
+// (an occlusion ray stops right after its hitting test: the pop that would follow changes nothing
+// the caller reads).  rec holds the record of the lane's current node on entry.
+template <int kLds>
+RT_DEV void trav_run_pf(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk, int stride,
+                        DeepStack* deep, bool occlusion) {
+    static_assert(kLds >= 10 && kLds <= 16, "LDS stack depth: 10..16 entries (at most 6 in registers)");
+#pragma unroll 1
+    while (true) {
+        bool pop = false;
+#pragma unroll 1
+        while (!s.cLeaf) {  // internal nodes
+            Node nd;
+            nd.q0 = rec.a; nd.q1 = rec.b; nd.q2 = rec.c; nd.q3 = rec.d;
+            ++s.iters;
+            ++s.visits;
+            float t1, t2;
+            bool i1, i2;
+            box_test2(r.h, nd, i1, i2, t1, t2);
+            if (!i1 && !i2) {
+                pop = true;
+                break;
+            }
+            const bool both = i1 && i2;
+            const bool goLeft = both ? (t1 < t2) : i1;
+            const bool push = both && s.top < 15;  // a push onto a full stack is dropped
+            s.dropped += (both && !push) ? 1u : 0u;
+            const uint32_t nIdx = goLeft ? nd.q3.x : nd.q3.y;
+            const bool nLeaf = (goLeft ? nd.q3.z : nd.q3.w) != 0u;
+            const float nT = goLeft ? t1 : t2;
+            rec = load_rec(sc, nLeaf, s.cBlas, nIdx, s.cOff);  // the next record, before the push
+            if (push) {
+                const uint32_t pIdx = goLeft ? nd.q3.y : nd.q3.x;
+                const uint32_t pLeaf = goLeft ? nd.q3.w : nd.q3.z;
+                const uint2 entry = make_uint2((pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) |
+                                                   ((s.cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31),
+                                               __float_as_uint(goLeft ? t2 : t1));
+                if (kLds == 16 || s.top + 1 < kLds) stk[(s.top + 1) * stride] = entry;
+                else deep_set(*deep, s.top + 1 - kLds, entry);
+                ++s.top;
+            }
+            s.cIdx = nIdx;
+            s.cLeaf = nLeaf;
+            s.cT = nT;
+            if (s.iters >= 1024u) return;
+        }
+        if (!pop) {
+            ++s.iters;
+            if (!s.cBlas) {  // TLAS leaf: continue at the root of that batch's BLAS, whose record is here
+                s.cLeaf = false;
+                s.cBlas = true;
+                s.cOff = s.cIdx;
+                s.cIdx = 0u;
+                if (s.iters >= 1024u) return;
+                continue;
+            }
+            const uint32_t li = s.cOff * 1024u + s.cIdx;
+            ++s.tests;
+            float tt;
+            if (watertight(r.tr, r.org, f3_of(rec.a), f3_of(rec.b), f3_of(rec.c), s.t, tt, s.u, s.v, s.errT) &&
+                tt < s.t) {
+                s.t = tt;
+                s.hitIdx = (int)li;
+                s.hitU = s.u; s.hitV = s.v; s.hitErrT = s.errT;
+            }
+            if (occlusion && s.hitIdx >= 0) return;
+        }
+        // TestForFinish (traverse.h:88-105)
+        int top = s.top;
+        uint32_t nIdx = 0u, nOff = 0u;
+        bool nBlas = false, nLeaf = false;
+        float nT = 0.0f;
+        do {
+            if (top < 0) {
+                s.top = top;
+                return;
+            }
+            const unsigned long long e = (kLds == 16 || top < kLds) ? *(volatile LdsU64*)(&stk[top * stride])
+                                                                    : deep_get(*deep, top - kLds);
+            const uint32_t a = (uint32_t)e;
+            nT = __uint_as_float((uint32_t)(e >> 32));
+            --top;
+            nIdx = a & 0x7FFFu;
+            nOff = (a >> 15) & 0x7FFFu;
+            nBlas = (a >> 30) & 1u;
+            nLeaf = (a >> 31) & 1u;
+        } while (nT > s.t);
+        s.top = top;
+        rec = load_rec(sc, nLeaf, nBlas, nIdx, nOff);
+        s.cIdx = nIdx;
+        s.cOff = nOff;
+        s.cBlas = nBlas;
+        s.cLeaf = nLeaf;
+        s.cT = nT;
+        if (s.iters >= 1024u) return;
+    }
+}
+
+// kLds as in trav_step_t: the stack entries kept in LDS (k_trace_primary keeps 10); kPf: the
+// iterations of trav_step_pf (record loaded one iteration ahead) run by trav_run_pf
+template <int kLds = 16, int kPf = 0>  // kPf 0: trav_step_t, 1: trav_run_pf, 2: trav_step_pf (A/B)
 RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint2* stk, int stride, HitInfo& out) {
     TravState s;
     if (root_surely_missed(sc, org, dir)) {
@@ -557,8 +661,17 @@ RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint2* stk, int strid
         trav_setup(sc, org, dir, r);
         trav_init(s);
         DeepStack deep;
-        for (int it = 0; it < 1024; ++it)
-            if (trav_step_t<kLds>(sc, r, s, stk, stride, &deep)) break;
+        if (kPf == 1) {
+            TravRec rec = trav_first_rec(sc);
+            trav_run_pf<kLds>(sc, r, s, rec, stk, stride, &deep, false);
+        } else if (kPf == 2) {
+            TravRec rec = trav_first_rec(sc);
+            for (int it = 0; it < 1024; ++it)
+                if (trav_step_pf<kLds>(sc, r, s, rec, stk, stride, &deep)) break;
+        } else {
+            for (int it = 0; it < 1024; ++it)
+                if (trav_step_t<kLds>(sc, r, s, stk, stride, &deep)) break;
+        }
     }
     finalize_hit(sc, org, dir, s.t, s.hitIdx, s.hitU, s.hitV, s.hitErrT, out);
     out.u = s.u;

@@ -141,3 +141,12 @@ def test_hook_stage_mask_requires_histogram_and_rows(rtx):
     assert L.rt_set_hook_stages(rt.h, 3) == 0
     assert L.rt_set_hook_stages(rt.h, 7) == 0
     rt.cleanup()
+
+
+def test_bvh_threads_config_is_checked(rtx, tmp_path):
+    """[render] bvhThreads picks the LBVH workgroup shape: 0 (by batch count), 512 or 1024."""
+    for v in (0, 512, 1024):
+        rtx.RayTracer(64, 64, rtx.write_config(str(tmp_path / ("t%d.toml" % v)), 64, 64,
+                                               extra="bvhThreads = %d\n" % v)).cleanup()
+    with pytest.raises(rtx.RtError):
+        rtx.RayTracer(64, 64, rtx.write_config(str(tmp_path / "bad.toml"), 64, 64, extra="bvhThreads = 256\n"))

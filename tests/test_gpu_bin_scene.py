@@ -10,8 +10,9 @@ from scene_bin import bin_bvh, probe_triangles, terrain_patch, write_bin
 pytestmark = pytest.mark.gpu
 
 
-def make(rtx, tmp_path, path, w=64, h=48, spp=1):
-    cfg = rtx.write_config(str(tmp_path / "b.toml"), w, h, spp=spp, mesh_file=path)
+def make(rtx, tmp_path, path, w=64, h=48, spp=1, threads=0):
+    cfg = rtx.write_config(str(tmp_path / "b.toml"), w, h, spp=spp, mesh_file=path,
+                           extra="bvhThreads = %d\n" % threads)
     rt = rtx.RayTracer(w, h, cfg).init()
     rt.set_delta_time(16.667)
     return rt
@@ -82,7 +83,8 @@ def test_bin_terrain_frame(rtx, oracle, tmp_path, ntri):
     rt.cleanup()
 
 
-def test_one_triangle_last_batch(rtx, oracle, tmp_path):
+@pytest.mark.parametrize("threads", [0, 512])
+def test_one_triangle_last_batch(rtx, oracle, tmp_path, threads):
     """N = 1,025: the last BLAS batch holds 1 real triangle and 3 padding ones (triCountArray = 1,
     init.cu:104-130), the triCount == 1 branch of BuildLBVH (buildBVH.cuh:31-38).  The reference
     writes that node to bvhNodes[0] BEFORE the per-batch offset, racing batch 0's own root and
@@ -92,7 +94,7 @@ def test_one_triangle_last_batch(rtx, oracle, tmp_path):
     tris = terrain_patch(23, 23)[:1025]
     path = write_bin(str(tmp_path / "n1025.bin"), tris)
     w, h = 96, 64
-    rt = make(rtx, tmp_path, path, w, h)
+    rt = make(rtx, tmp_path, path, w, h, threads=threads)
     info = rt.info()
     assert (info.triCount, info.triCountPadded, info.batchCount) == (1025, 1028, 2)
     b, _, _, n = bin_bvh(oracle, path)

@@ -1,13 +1,17 @@
 """GPU LBVH build (one fused launch) vs the CPU oracle: bit-exact Morton codes, reorder
-indices, node topology and boxes, TLAS — default scene and the ~1M-triangle variant."""
+indices, node topology and boxes, TLAS — default scene and the ~1M-triangle variant, in both
+workgroup shapes of the build kernel ([render] bvhThreads: 1024 threads with leaf boxes in LDS,
+512 threads with two elements each and leaf boxes read back from the AABB array; 0 picks by the
+batch count: 1024 for the default scene's 60 batches, 512 for the 1M scene's 937)."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 
-def build_gpu(rtx, tmp_path, chunk_dim, w=64, h=64):
-    cfg = rtx.write_config(str(tmp_path / ("c%d.toml" % chunk_dim)), w, h, chunk_dim=chunk_dim)
+def build_gpu(rtx, tmp_path, chunk_dim, w=64, h=64, threads=0):
+    cfg = rtx.write_config(str(tmp_path / ("c%d_%d.toml" % (chunk_dim, threads))), w, h, chunk_dim=chunk_dim,
+                           extra="bvhThreads = %d\n" % threads)
     rt = rtx.RayTracer(w, h, cfg).init()
     rt.build_bvh()
     rt.sync()
@@ -18,10 +22,10 @@ def as_nodes(rtx, raw):
     return raw.view(rtx.NODE_DTYPE)
 
 
-@pytest.mark.parametrize("chunk_dim", [1, 4])
-def test_bvh_bit_exact(rtx, oracle, tmp_path, chunk_dim):
+@pytest.mark.parametrize("chunk_dim,threads", [(1, 0), (4, 0), (1, 512), (4, 1024), (2, 512)])
+def test_bvh_bit_exact(rtx, oracle, tmp_path, chunk_dim, threads):
     v, i, n = oracle.scene(chunk_dim)
-    rt = build_gpu(rtx, tmp_path, chunk_dim)
+    rt = build_gpu(rtx, tmp_path, chunk_dim, threads=threads)
     info = rt.info()
     assert info.triCount == n and info.triCountPadded == i.shape[0]
     gv = rt.download("VERTICES", np.float32).reshape(-1, 3)
@@ -55,8 +59,9 @@ def test_bvh_bit_exact(rtx, oracle, tmp_path, chunk_dim):
     rt.cleanup()
 
 
-def test_bvh_rebuild_is_idempotent(rtx, tmp_path):
-    rt = build_gpu(rtx, tmp_path, 1)
+@pytest.mark.parametrize("threads", [1024, 512])
+def test_bvh_rebuild_is_idempotent(rtx, tmp_path, threads):
+    rt = build_gpu(rtx, tmp_path, 1, threads=threads)
     first = rt.download("NODES").copy()
     tlas = rt.download("TLAS_NODES").copy()
     for _ in range(5):

@@ -446,6 +446,9 @@ inline bool one_round(uint32_t spp) { return spp >= 1 && ((int)spp + cam_sample_
 #ifndef RTX_CAM_PF  // the camera rays' iterations as trav_step_pf (record one iteration ahead); A/B flag
 #define RTX_CAM_PF 0
 #endif
+#ifndef RTX_CAM_RUN  // the camera rays' traversal as trav_run_pf<.., false> (while-while); A/B flag
+#define RTX_CAM_RUN 0
+#endif
 #ifdef RTX_CAM_WPE  // ablation builds only: forced waves per SIMD
 #define RTX_CAM_ATTR __attribute__((amdgpu_waves_per_eu(RTX_CAM_WPE, RTX_CAM_WPE)))
 #else
@@ -503,7 +506,10 @@ __global__ __launch_bounds__(256) RTX_CAM_ATTR void k_pt_camera(PathTraceParams 
                 trav_setup(sc, org, dir, tr);
                 trav_init(st);
                 DeepStack deep;
-                if (RTX_CAM_PF) {
+                if (RTX_CAM_RUN) {  // while-while loops (trav_run_pf), records loaded where used
+                    TravRec trec;
+                    trav_run_pf<kCamLds, false>(sc, tr, st, trec, stk + tid, 256, &deep, false);
+                } else if (RTX_CAM_PF) {
                     TravRec trec = trav_first_rec(sc);
                     for (int it = 0; it < 1024; ++it)
                         if (trav_step_pf<kCamLds>(sc, tr, st, trec, stk + tid, 256, &deep)) break;

@@ -33,10 +33,10 @@ constexpr bool kLeafBatch = RTX_LEAF_BATCH != 0;  // ablation: -DRTX_LEAF_BATCH=
 #define RTX_TRAV_PF 1
 #endif
 constexpr bool kPrefetch = RTX_TRAV_PF != 0;  // next record loaded one iteration ahead (ablation: 0)
-#ifndef RTX_TAIL_RUN
-#define RTX_TAIL_RUN 1
+#ifndef RTX_TAIL_RUN  // A/B only: tail rays finished by trav_run_pf (while-while) — measured slower,
+#define RTX_TAIL_RUN 0  // lone ray 0.423 -> 0.495 us/iteration, frame 0.898 -> 0.944 ms
 #endif
-constexpr bool kTailRun = RTX_TAIL_RUN != 0;  // tail rays finished by trav_run_pf (ablation: 0)
+constexpr bool kTailRun = RTX_TAIL_RUN != 0;
 
 // one TraverseBvh iteration of this lane's ray (trav_step_pf, or trav_step_t without the prefetch)
 RT_DEV bool step(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk) {

@@ -554,7 +554,10 @@ RT_DEV void finalize_hit(const SceneView& sc, F3 org, F3 dir, float t, int hitId
 // it stops where `trav_step_pf(...) || s.iters >= 1024 || (occlusion && s.hitIdx >= 0)` would
 // (an occlusion ray stops right after its hitting test: the pop that would follow changes nothing
 // the caller reads).  rec holds the record of the lane's current node on entry.
-template <int kLds>
+//
+// kPf false: the same loops with each record loaded where it is used (no record carried across
+// iterations: fewer registers live through the loop, for kernels whose occupancy they set).
+template <int kLds, bool kPf = true>
 RT_DEV void trav_run_pf(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk, int stride,
                         DeepStack* deep, bool occlusion) {
     static_assert(kLds >= 10 && kLds <= 16, "LDS stack depth: 10..16 entries (at most 6 in registers)");
@@ -563,6 +566,7 @@ RT_DEV void trav_run_pf(const SceneView& sc, const TravRay& r, TravState& s, Tra
         bool pop = false;
 #pragma unroll 1
         while (!s.cLeaf) {  // internal nodes
+            if (!kPf) rec = load_rec(sc, false, s.cBlas, s.cIdx, s.cOff);
             Node nd;
             nd.q0 = rec.a; nd.q1 = rec.b; nd.q2 = rec.c; nd.q3 = rec.d;
             ++s.iters;
@@ -581,7 +585,7 @@ RT_DEV void trav_run_pf(const SceneView& sc, const TravRay& r, TravState& s, Tra
             const uint32_t nIdx = goLeft ? nd.q3.x : nd.q3.y;
             const bool nLeaf = (goLeft ? nd.q3.z : nd.q3.w) != 0u;
             const float nT = goLeft ? t1 : t2;
-            rec = load_rec(sc, nLeaf, s.cBlas, nIdx, s.cOff);  // the next record, before the push
+            if (kPf) rec = load_rec(sc, nLeaf, s.cBlas, nIdx, s.cOff);  // the next record, before the push
             if (push) {
                 const uint32_t pIdx = goLeft ? nd.q3.y : nd.q3.x;
                 const uint32_t pLeaf = goLeft ? nd.q3.w : nd.q3.z;
@@ -608,6 +612,7 @@ RT_DEV void trav_run_pf(const SceneView& sc, const TravRay& r, TravState& s, Tra
                 continue;
             }
             const uint32_t li = s.cOff * 1024u + s.cIdx;
+            if (!kPf) rec = load_rec(sc, true, true, s.cIdx, s.cOff);
             ++s.tests;
             float tt;
             if (watertight(r.tr, r.org, f3_of(rec.a), f3_of(rec.b), f3_of(rec.c), s.t, tt, s.u, s.v, s.errT) &&
@@ -639,7 +644,7 @@ RT_DEV void trav_run_pf(const SceneView& sc, const TravRay& r, TravState& s, Tra
             nLeaf = (a >> 31) & 1u;
         } while (nT > s.t);
         s.top = top;
-        rec = load_rec(sc, nLeaf, nBlas, nIdx, nOff);
+        if (kPf) rec = load_rec(sc, nLeaf, nBlas, nIdx, nOff);
         s.cIdx = nIdx;
         s.cOff = nOff;
         s.cBlas = nBlas;

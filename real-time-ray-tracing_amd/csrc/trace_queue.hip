@@ -39,7 +39,11 @@ constexpr bool kPrefetch = RTX_TRAV_PF != 0;  // next record loaded one iteratio
 constexpr bool kTailRun = RTX_TAIL_RUN != 0;
 
 // one TraverseBvh iteration of this lane's ray (trav_step_pf, or trav_step_t without the prefetch)
+#ifndef RTX_STEP2
+#define RTX_STEP2 0
+#endif
 RT_DEV bool step(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk) {
+    if (kPrefetch && RTX_STEP2) return trav_step_pf2<16>(sc, r, s, rec, stk, kTraceBlock, nullptr);
     if (kPrefetch) return trav_step_pf<16>(sc, r, s, rec, stk, kTraceBlock, nullptr);
     return trav_step(sc, r, s, stk, kTraceBlock);
 }

@@ -415,10 +415,17 @@ RT_DEV TravRec load_rec(const SceneView& sc, bool leaf, bool blas, uint32_t idx,
 // the record of the first iteration (the TLAS root, after trav_init)
 RT_DEV TravRec trav_first_rec(const SceneView& sc) { return load_rec(sc, false, false, 0u, 0u); }
 
+// measurement hook of tools/lat_probe.hip (iteration start, record arrival); empty in the product
+#ifndef RTX_TRAV_HOOK
+#define RTX_TRAV_HOOK(k, s, rec)
+#endif
+
 template <int kLds>
 RT_DEV bool trav_step_pf(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk, int stride,
                          DeepStack* deep) {
     static_assert(kLds >= 10 && kLds <= 16, "LDS stack depth: 10..16 entries (at most 6 in registers)");
+    RTX_TRAV_HOOK(0, s, rec);
+    RTX_TRAV_HOOK(1, s, rec);
     ++s.iters;
     bool pop = false, push = false, tlasLeaf = false;
     uint32_t pIdx = 0u, pLeaf = 0u, pT = 0u;  // the pushed sibling (entry built after the load)
@@ -544,6 +551,98 @@ RT_DEV void finalize_hit(const SceneView& sc, F3 org, F3 dir, float t, int hitId
     out.ndr = ndr;
     out.into = into;
     out.hit = hit;
+}
+
+// trav_step_pf with one divergent region.  The internal-node case — nine iterations in ten — runs
+// straight through: the box tests run for every iteration (on a leaf's record their results are
+// unused), the next node and the push are selects, and only a leaf iteration or a pop enters the
+// branch.  A TLAS leaf's BLAS root is loaded again at its own iteration (a cache hit) rather than
+// carried, so the record load is unconditional.  Same iterations, pushes, drops, pops and counters
+// as trav_step_pf.
+template <int kLds>
+RT_DEV bool trav_step_pf2(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk, int stride,
+                          DeepStack* deep) {
+    static_assert(kLds >= 10 && kLds <= 16, "LDS stack depth: 10..16 entries (at most 6 in registers)");
+    ++s.iters;
+    Node nd;
+    nd.q0 = rec.a; nd.q1 = rec.b; nd.q2 = rec.c; nd.q3 = rec.d;
+    float t1, t2;
+    bool i1, i2;
+    box_test2(r.h, nd, i1, i2, t1, t2);
+    const bool node = !s.cLeaf;
+    const bool both = i1 && i2;
+    const bool goLeft = both ? (t1 < t2) : i1;
+    const bool push = node && both && s.top < 15;  // a push onto a full stack is dropped
+    s.visits += node ? 1u : 0u;
+    s.dropped += (node && both && !push) ? 1u : 0u;
+    const uint32_t pIdx = goLeft ? nd.q3.y : nd.q3.x;
+    const uint32_t pLeaf = goLeft ? nd.q3.w : nd.q3.z;
+    const uint32_t pT = __float_as_uint(goLeft ? t2 : t1);
+    uint32_t nIdx = goLeft ? nd.q3.x : nd.q3.y;
+    bool nLeaf = (goLeft ? nd.q3.z : nd.q3.w) != 0u;
+    float nT = goLeft ? t1 : t2;
+    uint32_t nOff = s.cOff;
+    bool nBlas = s.cBlas;
+    if (!node || (!i1 && !i2)) {  // a leaf iteration, or a node whose children both missed
+        bool pop = node;
+        if (!node) {
+            if (s.cBlas) {
+                const uint32_t li = s.cOff * 1024u + s.cIdx;
+                ++s.tests;
+                float tt;
+                if (watertight(r.tr, r.org, f3_of(rec.a), f3_of(rec.b), f3_of(rec.c), s.t, tt, s.u, s.v, s.errT) &&
+                    tt < s.t) {
+                    s.t = tt;
+                    s.hitIdx = (int)li;
+                    s.hitU = s.u; s.hitV = s.v; s.hitErrT = s.errT;
+                }
+                pop = true;
+            } else {  // TLAS leaf: continue at the root of that batch's BLAS
+                nLeaf = false;
+                nBlas = true;
+                nOff = s.cIdx;
+                nIdx = 0u;
+                nT = s.cT;
+            }
+        }
+        if (pop) {  // TestForFinish (traverse.h:88-105)
+            int top = s.top;
+            do {
+                if (top < 0) {
+                    s.top = top;
+                    return true;
+                }
+                const unsigned long long e = (kLds == 16 || top < kLds) ? *(volatile LdsU64*)(&stk[top * stride])
+                                                                        : deep_get(*deep, top - kLds);
+                const uint32_t a = (uint32_t)e;
+                nT = __uint_as_float((uint32_t)(e >> 32));
+                --top;
+                nIdx = a & 0x7FFFu;
+                nOff = (a >> 15) & 0x7FFFu;
+                nBlas = (a >> 30) & 1u;
+                nLeaf = (a >> 31) & 1u;
+            } while (nT > s.t);
+            s.top = top;
+        }
+    }
+    // the pushed entry is formed before the load, so the current record's registers are free for
+    // the next one (otherwise the compiler loads into other registers and waits to copy them back)
+    uint32_t eA = (pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) | ((s.cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31);
+    uint32_t eT = pT;
+    asm volatile("" : "+v"(eA), "+v"(eT)::"memory");
+    rec = load_rec(sc, nLeaf, nBlas, nIdx, nOff);
+    if (push) {
+        const uint2 entry = make_uint2(eA, eT);
+        if (kLds == 16 || s.top + 1 < kLds) stk[(s.top + 1) * stride] = entry;
+        else deep_set(*deep, s.top + 1 - kLds, entry);
+        ++s.top;
+    }
+    s.cIdx = nIdx;
+    s.cOff = nOff;
+    s.cBlas = nBlas;
+    s.cLeaf = nLeaf;
+    s.cT = nT;
+    return false;
 }
 
 // A whole traversal, from the lane's current state to its end, as nested loops (while-while,
@@ -673,6 +772,10 @@ RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint2* stk, int strid
             TravRec rec = trav_first_rec(sc);
             for (int it = 0; it < 1024; ++it)
                 if (trav_step_pf<kLds>(sc, r, s, rec, stk, stride, &deep)) break;
+        } else if (kPf == 3) {
+            TravRec rec = trav_first_rec(sc);
+            for (int it = 0; it < 1024; ++it)
+                if (trav_step_pf2<kLds>(sc, r, s, rec, stk, stride, &deep)) break;
         } else {
             for (int it = 0; it < 1024; ++it)
                 if (trav_step_t<kLds>(sc, r, s, stk, stride, &deep)) break;

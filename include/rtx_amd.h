@@ -421,7 +421,10 @@ enum rt_array_name {
     RT_ARR_TEX_ALBEDO_AO = 37,   /* ushort4, 11-level mip chain of 1024^2 (levels concatenated, 1024 -> 1) */
     RT_ARR_TEX_NORMAL_ROUGHNESS = 38, /* ushort4, same layout */
     RT_ARR_TEX_HEIGHT = 39,      /* ushort, same layout (zero unless uploaded) */
-    RT_ARR_HDR = 40              /* float4[W*H] pre-tone-map HDR of the last rt_draw / rt_denoise_post with_hdr */
+    RT_ARR_HDR = 40,             /* float4[W*H] pre-tone-map HDR of the last rt_draw / rt_denoise_post with_hdr */
+    RT_ARR_BVH_ARENA = 41        /* the traversal's record arena as the device holds it (64-B records: B*1024 BLAS
+                                    nodes, B TLAS nodes, triCountPadded triangle records); the
+                                    NODES / TLAS_NODES / TRI_POS arrays are views of it in the reference layout */
 };
 int rt_download(const rt_context* ctx, int what, void* dst, size_t bytes);
 

@@ -261,12 +261,25 @@ RT_DEV void karras(Lds<kThr>& s, int n) {
     for (int i = threadIdx.x; i < n - 1; i += kThr) karras_node(s, n, i);
 }
 
-RT_DEV void store_node(Node* dst, const Box& l, const Box& r, uint32_t cl, uint32_t cr) {
+// Traversal words of one tree's child references (traverse.h, the record arena): an internal
+// child c is the node at nodeBase + c, a leaf c the record at leafBase + c * leafMul (a BLAS: the
+// triangle record; the TLAS: batch c's BLAS root), each with its (leaf, BLAS) kind bits.
+struct WordCtx {
+    uint32_t nodeKind, nodeBase, leafKind, leafBase, leafMul;
+};
+RT_DEV uint32_t child_word(const WordCtx& w, uint32_t c) {
+    const uint32_t i = c & 0x7FFFu;
+    return (c & 0x8000u) ? (w.leafKind | (w.leafBase + i * w.leafMul)) : (w.nodeKind | (w.nodeBase + i));
+}
+
+// the reference's BVHNode boxes in q0..q2; q3: the children's traversal words and the reference's
+// child references (left | right << 16, bit 15 of each = leaf), for rt_download's reference layout
+RT_DEV void store_node(Node* dst, const Box& l, const Box& r, uint32_t cl, uint32_t cr, const WordCtx& w) {
     Node nd;
     nd.q0 = make_float4(l.mn.x, l.mn.y, l.mn.z, l.mx.x);
     nd.q1 = make_float4(l.mx.y, l.mx.z, r.mn.x, r.mn.y);
     nd.q2 = make_float4(r.mn.z, r.mx.x, r.mx.y, r.mx.z);
-    nd.q3 = make_uint4(cl & 0x7FFFu, cr & 0x7FFFu, (cl >> 15) & 1u, (cr >> 15) & 1u);
+    nd.q3 = make_uint4(child_word(w, cl), child_word(w, cr), (cl & 0xFFFFu) | ((cr & 0xFFFFu) << 16), 0u);
     *dst = nd;
 }
 
@@ -307,9 +320,9 @@ RT_DEV void climb_start(const Lds<kThr>& s, const float* leafG, int n, int i, Cl
 }
 
 template <int kThr>
-RT_DEV void climb_step(Lds<kThr>& s, const float* leafG, Node* nodes, Climb& c) {
+RT_DEV void climb_step(Lds<kThr>& s, const float* leafG, Node* nodes, const WordCtx& w, Climb& c) {
     const Box m = box_merge(c.l, c.r);
-    store_node(nodes + c.cur, c.l, c.r, c.cl, c.cr);
+    store_node(nodes + c.cur, c.l, c.r, c.cl, c.cr, w);
     if (c.cur == 0) {
         c.on = false;
         return;
@@ -342,13 +355,13 @@ RT_DEV void climb_step(Lds<kThr>& s, const float* leafG, Node* nodes, Climb& c) 
 
 // The climbs of this thread's internal nodes (kPer of them, one after the other).
 template <int kThr>
-RT_DEV void refit(Lds<kThr>& s, const float* leafG, int n, Node* nodes) {
+RT_DEV void refit(Lds<kThr>& s, const float* leafG, int n, Node* nodes, const WordCtx& w) {
     constexpr int kPer = kBatch / kThr;
     const int t = threadIdx.x;
     if (n == 1) {
         if (t == 0) {
             Box zero; zero.mn = f3(0.0f); zero.mx = f3(0.0f);
-            store_node(nodes, leaf_box(s, leafG, 0u), zero, 0x8000u, 0x8000u);
+            store_node(nodes, leaf_box(s, leafG, 0u), zero, 0x8000u, 0x8000u, w);
         }
         return;
     }
@@ -357,14 +370,14 @@ RT_DEV void refit(Lds<kThr>& s, const float* leafG, int n, Node* nodes) {
         Climb c;
         climb_start(s, leafG, n, t + j * kThr, c);
         for (int guard = 0; guard < kBatch && c.on; ++guard)  // a valid tree ends at the root in < n steps
-            climb_step(s, leafG, nodes, c);
+            climb_step(s, leafG, nodes, w, c);
     }
 }
 
 // Sort the keys in key0/idx0 and build the tree of n leaves into `nodes`.
 template <int kThr>
 RT_DEV void sort_and_build(Lds<kThr>& s, const float* leafG, int n, uint32_t* mortonOut, uint32_t* reorderOut,
-                           Node* nodes) {
+                           Node* nodes, const WordCtx& w) {
     __syncthreads();
     radix_sort(s);
 #pragma unroll
@@ -376,9 +389,12 @@ RT_DEV void sort_and_build(Lds<kThr>& s, const float* leafG, int n, uint32_t* mo
     karras(s, n);
     __syncthreads();
 #if !(defined(RTX_BVH_ABL) && RTX_BVH_ABL == 3)
-    refit(s, leafG, n, nodes);  // (ablation 3: no refit; timing only)
+    refit(s, leafG, n, nodes, w);  // (ablation 3: no refit; timing only)
 #endif
 }
+
+// the TLAS's child words: internal nodes after the B*1024 BLAS slots, leaves at their BLAS roots
+RT_DEV WordCtx tlas_words(uint32_t B) { return WordCtx{0u, B * (uint32_t)kBatch, kLeafBit, 0u, (uint32_t)kBatch}; }
 
 // The TLAS of a scene of at most 64 batches, built by wave 0 of the last workgroup alone: the
 // same results as the workgroup path (UpdateTLAS + RadixSort + BuildLBVH over B keys) without
@@ -423,7 +439,7 @@ RT_DEV void tlas_wave(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
     P.tlasReorder[lane] = s.idx1[lane];
     karras(s, (int)B);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    refit(s, P.tlasAabbs, (int)B, (Node*)P.tlasNodes);
+    refit(s, P.tlasAabbs, (int)B, (Node*)P.tlasNodes, tlas_words(B));
     if (lane == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -457,9 +473,9 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
             const F3 v1 = f3(P.vertices[3 * i0], P.vertices[3 * i0 + 1], P.vertices[3 * i0 + 2]);
             const F3 v2 = f3(P.vertices[3 * i1], P.vertices[3 * i1 + 1], P.vertices[3 * i1 + 2]);
             const F3 v3 = f3(P.vertices[3 * i2], P.vertices[3 * i2 + 1], P.vertices[3 * i2 + 2]);
-            P.triPos[3 * g + 0] = make_float4(v1.x, v1.y, v1.z, 0.0f);
-            P.triPos[3 * g + 1] = make_float4(v2.x, v2.y, v2.z, 0.0f);
-            P.triPos[3 * g + 2] = make_float4(v3.x, v3.y, v3.z, 0.0f);
+            P.triPos[4 * g + 0] = make_float4(v1.x, v1.y, v1.z, 0.0f);  // the triangle's arena record
+            P.triPos[4 * g + 1] = make_float4(v2.x, v2.y, v2.z, 0.0f);
+            P.triPos[4 * g + 2] = make_float4(v3.x, v3.y, v3.z, 0.0f);
             P.triNrm[3 * g + 0] = make_float4(P.normals[3 * i0], P.normals[3 * i0 + 1], P.normals[3 * i0 + 2], 0.0f);
             P.triNrm[3 * g + 1] = make_float4(P.normals[3 * i1], P.normals[3 * i1 + 1], P.normals[3 * i1 + 2], 0.0f);
             P.triNrm[3 * g + 2] = make_float4(P.normals[3 * i2], P.normals[3 * i2 + 1], P.normals[3 * i2 + 2], 0.0f);
@@ -492,7 +508,8 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
     if (t == 0) store_box(P.batchSceneAabbs + 6 * (size_t)b, scene);
 
     Node* const nodes = (Node*)P.nodes;
-    sort_and_build(s, leafG, (int)cnt, P.morton + start, P.reorder + start, nodes + start);
+    const WordCtx blasWords{kBlasBit, start, kLeafBit | kBlasBit, B * (uint32_t)kBatch + B + start, 1u};
+    sort_and_build(s, leafG, (int)cnt, P.morton + start, P.reorder + start, nodes + start, blasWords);
 
     // ---- arrival: the last workgroup builds the TLAS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -552,7 +569,8 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
         s.a.srt.idx0[e] = (uint16_t)e;
     }
     if (t == 0) store_box(P.tlasSceneAabb, quirk);
-    sort_and_build(s, (const float*)P.tlasAabbs, (int)B, P.tlasMorton, P.tlasReorder, (Node*)P.tlasNodes);
+    sort_and_build(s, (const float*)P.tlasAabbs, (int)B, P.tlasMorton, P.tlasReorder, (Node*)P.tlasNodes,
+                   tlas_words(B));
     __syncthreads();
     if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

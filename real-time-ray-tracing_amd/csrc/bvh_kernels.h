@@ -10,18 +10,19 @@ struct BvhBuildParams {
     uint32_t triCount;
     uint32_t triCountPadded;
     uint32_t batchCount;
-    float4* triPos;            // [triCountPadded][3] (xyz, 0)
+    float4* triPos;            // the arena's triangle records [triCountPadded][4]: v1, v2, v3 (w 0), one quad unused
     float4* triNrm;            // [triCountPadded][3] (xyz, 0)
     float* aabbs;              // [triCountPadded][6]
     float* batchSceneAabbs;    // [B][6]
     uint32_t* morton;          // [B*1024] sorted keys
     uint32_t* reorder;         // [B*1024]
-    void* nodes;               // [triCountPadded] 64-B nodes
+    void* nodes;               // the record arena (traverse.h): [B*1024] BLAS nodes, then the TLAS nodes, then
+                               // the triangle records (triPos = nodes + 64 * (B*1024 + B) bytes)
     float* tlasAabbs;          // [B][6]
     float* tlasSceneAabb;      // [6]
     uint32_t* tlasMorton;      // [1024]
     uint32_t* tlasReorder;     // [1024]
-    void* tlasNodes;           // [B]
+    void* tlasNodes;           // [B] = nodes + 64 * B*1024 bytes
     uint32_t* counter;         // arrival counter, zero between launches
     uint32_t threads;          // workgroup shape: 0 = by batch count, 512 or 1024 ([render] bvhThreads)
 };
@@ -87,10 +88,10 @@ struct TracePrimaryParams {
     uint32_t nStrips, strip;
     int frameNum;
     const uint8_t* bluenoise;   // sobol | scrambling | ranking
-    const float4* triPos;
+    const float4* triPos;       // the arena's triangle records
     const float4* triNrm;
-    const void* nodes;
-    const void* tlasNodes;
+    const void* nodes;          // the record arena
+    const void* tlasNodes;      // its TLAS nodes
     float4* hitOut;             // [W*H] (t, objectIdx bits, u, v)
     float4* normalOut;          // [W*H] optional (geometric normal, hit)
     float4* fakeNormalOut;      // [W*H] optional

@@ -415,18 +415,19 @@ int rt_init(rt_context* ctx) {
     ALLOC(ctx->dVerts, (size_t)ctx->nv * 12);
     ALLOC(ctx->dNormals, (size_t)ctx->nv * 12);
     ALLOC(ctx->dIdx, (size_t)NP * 12);
-    ALLOC(ctx->dTriPos, (size_t)NP * 48);
+    // the record arena (traverse.h): BLAS nodes, TLAS nodes, triangle records, 64 B each
+    ALLOC(ctx->dNodes, arena_bytes(ctx->B, NP));
+    ctx->dTlasNodes = (char*)ctx->dNodes + (size_t)ctx->B * 1024 * 64;
+    ctx->dTriPos = (float4*)((char*)ctx->dNodes + ((size_t)ctx->B * 1024 + ctx->B) * 64);
     ALLOC(ctx->dTriNrm, (size_t)NP * 48);
     ALLOC(ctx->dAabbs, (size_t)NP * 24);
     ALLOC(ctx->dBatchScene, (size_t)ctx->B * 24);
     ALLOC(ctx->dMorton, (size_t)ctx->B * 4096);
     ALLOC(ctx->dReorder, (size_t)ctx->B * 4096);
-    ALLOC(ctx->dNodes, (size_t)ctx->B * 1024 * 64);
     ALLOC(ctx->dTlasAabbs, (size_t)ctx->B * 24);
     ALLOC(ctx->dTlasScene, 24);
     ALLOC(ctx->dTlasMorton, 4096);
     ALLOC(ctx->dTlasReorder, 4096);
-    ALLOC(ctx->dTlasNodes, (size_t)ctx->B * 64);
     ALLOC(ctx->dCounter, 64);
     ctx->bvh[0] = BvhBufs{ctx->dTriPos, ctx->dTriNrm, ctx->dAabbs, ctx->dBatchScene, ctx->dMorton, ctx->dReorder,
                           ctx->dNodes, ctx->dTlasAabbs, ctx->dTlasScene, ctx->dTlasMorton, ctx->dTlasReorder,
@@ -441,8 +442,7 @@ int rt_init(rt_context* ctx) {
     HIP_TRY(ctx, hipMemcpy(ctx->dVerts, ctx->mesh.vertices.data(), (size_t)ctx->nv * 12, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemcpy(ctx->dIdx, ctx->mesh.indices.data(), (size_t)NP * 12, hipMemcpyHostToDevice));
     HIP_TRY(ctx, hipMemset(ctx->dCounter, 0, 64));
-    HIP_TRY(ctx, hipMemset(ctx->dNodes, 0, (size_t)ctx->B * 1024 * 64));
-    HIP_TRY(ctx, hipMemset(ctx->dTlasNodes, 0, (size_t)ctx->B * 64));
+    HIP_TRY(ctx, hipMemset(ctx->dNodes, 0, arena_bytes(ctx->B, NP)));
 
     std::string bn;
     if (!read_file(dataDir + "/bluenoise_4spp.bin", bn) || bn.size() != 327680) {
@@ -804,6 +804,7 @@ size_t rt_array_bytes(const rt_context* ctx, int what) {
         case RT_ARR_TLAS_MORTON: return 4096;
         case RT_ARR_TLAS_REORDER: return 4096;
         case RT_ARR_TLAS_NODES: return B * 64;
+        case RT_ARR_BVH_ARENA: return arena_bytes(B, NP);
         case RT_ARR_TLAS_SCENE_AABB: return 24;
         case RT_ARR_BATCH_SCENE_AABBS: return B * 24;
         case RT_ARR_HITS: return P * 16;
@@ -851,6 +852,7 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
         case RT_ARR_MORTON: src = ctx->dMorton; break;
         case RT_ARR_REORDER: src = ctx->dReorder; break;
         case RT_ARR_NODES: src = ctx->dNodes; break;
+        case RT_ARR_BVH_ARENA: src = ctx->dNodes; break;
         case RT_ARR_TLAS_AABBS: src = ctx->dTlasAabbs; break;
         case RT_ARR_TLAS_MORTON: src = ctx->dTlasMorton; break;
         case RT_ARR_TLAS_REORDER: src = ctx->dTlasReorder; break;
@@ -896,7 +898,24 @@ int rt_download(const rt_context* cctx, int what, void* dst, size_t bytes) {
     const size_t need = rt_array_bytes(ctx, what);
     if (bytes < need) { ctx->err = "destination too small"; return RT_ERR_ARG; }
     if (int rc = sync_streams(ctx)) return rc;
+    if (what == RT_ARR_TRI_POS) {  // the arena's 64-B triangle records -> the reference's [N][3] float4
+        HIP_TRY(ctx, hipMemcpy2D(dst, 48, src, 64, 48, ctx->mesh.triCountPadded, hipMemcpyDeviceToHost));
+        return RT_OK;
+    }
     HIP_TRY(ctx, hipMemcpy(dst, src, need, hipMemcpyDeviceToHost));
+    if (what == RT_ARR_NODES || what == RT_ARR_TLAS_NODES) {
+        // the reference's q3 (idxLeft, idxRight, isLeftLeaf, isRightLeaf) from the child references
+        // the build keeps in q3.z (traverse.h, the record arena); a slot never written stays zero
+        uint32_t* q = (uint32_t*)dst;
+        for (size_t k = 0; k < need / 64; ++k) {
+            uint32_t* q3 = q + 16 * k + 12;
+            const uint32_t cl = q3[2] & 0xFFFFu, cr = q3[2] >> 16;
+            q3[0] = cl & 0x7FFFu;
+            q3[1] = cr & 0x7FFFu;
+            q3[2] = (cl >> 15) & 1u;
+            q3[3] = (cr >> 15) & 1u;
+        }
+    }
     return RT_OK;
 }
 

@@ -22,6 +22,10 @@ struct HostCamera {  // Camera::update outputs (kernel.cuh:103-121)
 // Device buffers of RayTracer::draw after the BVH (kernel.cu:259-398)
 // Build outputs and scratch of one LBVH (bvh_build.hip).  With frame pipelining there are two,
 // so frame f+1's build and camera rays run beside frame f's trace kernels.
+// Bytes of an LBVH set's record arena (traverse.h): B*1024 BLAS nodes, B TLAS nodes and NP
+// triangle records of 64 B.  BvhBufs::nodes is the arena; tlasNodes and triPos point into it.
+inline size_t arena_bytes(size_t B, size_t NP) { return (B * 1024 + B + NP) * 64; }
+
 struct BvhBufs {
     float4* triPos = nullptr;
     float4* triNrm = nullptr;

@@ -1035,18 +1035,21 @@ int ensure_bvh_pair(rt_context* ctx) {
     {
         const size_t NP = ctx->mesh.triCountPadded, B = ctx->B;
         BvhBufs& b = ctx->bvh[1];
-        ALLOC(b.triPos, NP * 48);
+        if (!b.nodes) {  // the record arena (traverse.h), as in rt_init
+            ALLOC(b.nodes, arena_bytes(B, NP));
+            HIP_TRY(ctx, hipMemset(b.nodes, 0, arena_bytes(B, NP)));
+            b.tlasNodes = (char*)b.nodes + B * 1024 * 64;
+            b.triPos = (float4*)((char*)b.nodes + (B * 1024 + B) * 64);
+        }
         ALLOC(b.triNrm, NP * 48);
         ALLOC(b.aabbs, NP * 24);
         ALLOC(b.batchScene, B * 24);
         ALLOC(b.morton, B * 4096);
         ALLOC(b.reorder, B * 4096);
-        ALLOC(b.nodes, B * 1024 * 64);
         ALLOC(b.tlasAabbs, B * 24);
         ALLOC(b.tlasScene, 24);
         ALLOC(b.tlasMorton, 4096);
         ALLOC(b.tlasReorder, 4096);
-        ALLOC(b.tlasNodes, B * 64);
         if (!b.counter) {
             ALLOC(b.counter, 64);
             HIP_TRY(ctx, hipMemset(b.counter, 0, 64));

@@ -132,10 +132,10 @@ struct PathTraceParams {
     int materialOverride;       // < 0: reference material table (material 3 everywhere)
     uint32_t triCount;
     const uint8_t* bluenoise;
-    const float4* triPos;
+    const float4* triPos;       // the record arena's triangle records (traverse.h)
     const float4* triNrm;
-    const void* nodes;
-    const void* tlasNodes;
+    const void* nodes;          // the record arena
+    const void* tlasNodes;      // its TLAS nodes
     const uint2* texAlbedo;     // ushort4 texels, kTexLevels levels concatenated
     const uint2* texNormal;
     const float4* skyBuffer;

@@ -370,14 +370,7 @@ RT_DEV void enqueue(const PtQueue& q, uint32_t slot, const PathVars& v, uint32_t
     q.st2[slot] = make_float4(v.beta0.x, v.beta0.y, v.beta0.z, 0.0f);
 }
 
-RT_DEV SceneView scene_of(const PathTraceParams& P) {
-    SceneView sc;
-    sc.triPos = P.triPos;
-    sc.triNrm = P.triNrm;
-    sc.nodes = (const Node*)P.nodes;
-    sc.tlas = (const Node*)P.tlasNodes;
-    return sc;
-}
+RT_DEV SceneView scene_of(const PathTraceParams& P) { return scene_view(P.nodes, P.tlasNodes, P.triPos, P.triNrm); }
 
 // workgroup sum of traced rays into the frame counter (one atomic per workgroup)
 // w: the calling wave's index in the workgroup (wave-uniform); the lane comes from v_mbcnt, so a
@@ -443,19 +436,13 @@ inline bool one_round(uint32_t spp) { return spp >= 1 && ((int)spp + cam_sample_
 //
 // kOneRound: every sample wave runs one round (spp <= 4 except 3: the launcher checks), so the
 // round loop and its carried state compile away.
-#ifndef RTX_CAM_PF  // the camera rays' iterations as trav_step_pf (record one iteration ahead); A/B flag
-#define RTX_CAM_PF 0
-#endif
-#ifndef RTX_CAM_RUN  // the camera rays' traversal as trav_run_pf<.., false> (while-while); A/B flag
-#define RTX_CAM_RUN 0
-#endif
 #ifdef RTX_CAM_WPE  // ablation builds only: forced waves per SIMD
 #define RTX_CAM_ATTR __attribute__((amdgpu_waves_per_eu(RTX_CAM_WPE, RTX_CAM_WPE)))
 #else
 #define RTX_CAM_ATTR
 #endif
 template <bool kOneRound>
-__global__ __launch_bounds__(256) RTX_CAM_ATTR void k_pt_camera(PathTraceParams P) {
+__global__ __launch_bounds__(256, 6) RTX_CAM_ATTR void k_pt_camera(PathTraceParams P) {
     // stack entries in LDS (the rest in registers): 26 KB per workgroup, 6 workgroups per CU
     // (measured: 16 entries 4 per CU 0.948 ms/frame, 12 entries 5 per CU 0.918, 10 entries 6 per CU
     // 0.900; the default scene's rays hold at most 11 entries)
@@ -499,24 +486,16 @@ __global__ __launch_bounds__(256) RTX_CAM_ATTR void k_pt_camera(PathTraceParams 
                                   dir, uv);
             TravState st;
             if (root_surely_missed(sc, org, dir)) {  // most sky rays: settled without the ray-box helper
-                trav_root_miss(st);
+                trav_root_miss(st, sc.root);
                 ++camCull;
             } else {
                 TravRay tr;
                 trav_setup(sc, org, dir, tr);
-                trav_init(st);
+                trav_init(st, sc.root);
                 DeepStack deep;
-                if (RTX_CAM_RUN) {  // while-while loops (trav_run_pf), records loaded where used
-                    TravRec trec;
-                    trav_run_pf<kCamLds, false>(sc, tr, st, trec, stk + tid, 256, &deep, false);
-                } else if (RTX_CAM_PF) {
-                    TravRec trec = trav_first_rec(sc);
-                    for (int it = 0; it < 1024; ++it)
-                        if (trav_step_pf<kCamLds>(sc, tr, st, trec, stk + tid, 256, &deep)) break;
-                } else {
-                    for (int it = 0; it < 1024; ++it)
-                        if (trav_step_t<kCamLds>(sc, tr, st, stk + tid, 256, &deep)) break;
-                }
+                TravRec trec;  // each iteration loads its own record (kCarry false: occupancy)
+                for (int it = 0; it < 1024; ++it)
+                    if (trav_step<kCamLds, false>(sc, tr, st, trec, stk + tid, 256, &deep)) break;
             }
             ++rays;
             if (P.statsOut) {
@@ -615,7 +594,7 @@ __global__ __launch_bounds__(256) RTX_CAM_ATTR void k_pt_camera(PathTraceParams 
 // is not carried across rounds (229 instead of 256 VGPRs; one GPU 0.970 -> 0.945 ms/frame).
 template <bool kGlossy, bool kMF, bool kOneRound>
 __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
-    __shared__ uint2 stk[kGlossy ? 16 * 256 : 1];
+    __shared__ uint2 stk[kGlossy ? 17 * 256 : 1];  // 16 entries + trav_step's dead slot
     __shared__ uint32_t sob[256];
     __shared__ float4 foldL[4][64];  // this round's samples: finished colour xyz, w = 1 when deferred
     __shared__ float4 foldA[4][64];  // their albedo
@@ -887,16 +866,12 @@ constexpr bool kChainStaticFirst = RTX_CHAIN_STATIC != 0;  // ablation: static f
 // Per sample the code is the one the separate kernels run (resume_entry, trav_step), so the
 // G-buffers are identical.  The hit records a wave reads in phase 2 are ones its own lanes wrote
 // (a workgroup-scope fence orders them), so no record crosses workgroups inside the launch.
-#ifndef RTX_CHAIN_PF  // the chain's traversals as trav_step_pf (record one iteration ahead); A/B flag
-#define RTX_CHAIN_PF 0
-#endif
 RT_DEV bool chain_step(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk) {
-    if (RTX_CHAIN_PF) return trav_step_pf<16>(sc, r, s, rec, stk, 256, nullptr);
-    return trav_step(sc, r, s, stk, 256);
+    return trav_step<16, false>(sc, r, s, rec, stk, 256, nullptr);  // no carried record: 168 VGPRs, no scratch
 }
 
 __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
-    __shared__ uint2 stk[16 * 256];
+    __shared__ uint2 stk[17 * 256];  // 16 entries + trav_step's dead slot
     __shared__ uint32_t sob[256];
     __shared__ uint2 ranges[4][kChainRanges];
     __shared__ uint32_t q4list[4][64];
@@ -924,9 +899,9 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
         uint32_t idx = 0;
         TravRay r;
         TravState s;
-        TravRec rec;  // RTX_CHAIN_PF: the record of the lane's next iteration
+        TravRec rec;  // scratch of chain_step (each iteration loads its own record)
         r.org = f3(0.0f);
-        trav_init(s);
+        trav_init(s, sc.root);
 #pragma unroll 1
         while (true) {
             const unsigned long long need = __ballot(!active && !exhausted);
@@ -948,8 +923,7 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
                         idx = f.resLo + rank;
                         const float4 o = q.rayO[idx], d = q.rayD[idx];
                         trav_setup(sc, f3(o.x, o.y, o.z), f3(d.x, d.y, d.z), r);
-                        trav_init(s);
-                        if (RTX_CHAIN_PF) rec = trav_first_rec(sc);
+                        trav_init(s, sc.root);
                         active = true;
                         occlusion = (__float_as_uint(d.w) & kQShadowFlag) != 0u;
                     } else if (none) {
@@ -1006,9 +980,8 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
                     const float4 o = P.ws.q4.rayO[slot], d = P.ws.q4.rayD[slot];  // slot 0 for idle lanes
                     trav_setup(sc, f3(o.x, o.y, o.z), f3(d.x, d.y, d.z), r4);
                 }
-                trav_init(s4);
+                trav_init(s4, sc.root);
                 TravRec rec4;
-                if (RTX_CHAIN_PF) rec4 = trav_first_rec(sc);
                 const bool mine = act;
 #if defined(RTX_CHAIN_ABL) && RTX_CHAIN_ABL == 2
                 act = false;  // timing ablation: I4 rays not traced

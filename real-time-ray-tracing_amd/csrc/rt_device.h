@@ -81,11 +81,14 @@ RT_DEV uint32_t sat_u32(float x) {
 }
 RT_DEV float err_gamma(int n) { return (n * kMachineEps) / (1.0f - n * kMachineEps); }
 
-// canonical 64-byte BVH node: 4 x 16 B
+// 64-byte BVH node: 4 x 16 B
 //   q0 = lmin.x lmin.y lmin.z lmax.x
 //   q1 = lmax.y lmax.z rmin.x rmin.y
 //   q2 = rmin.z rmax.x rmax.y rmax.z
-//   q3 = idxLeft idxRight isLeftLeaf isRightLeaf
+//   q3 = left word, right word, left | right << 16 (the reference's child references), 0
+// (the reference's q3 is idxLeft idxRight isLeftLeaf isRightLeaf; rt_download restores it).  A
+// word is a record-arena index with the child's kind on top (traverse.h, the record arena).
+constexpr uint32_t kLeafBit = 0x80000000u, kBlasBit = 0x40000000u, kIdxMask = 0x3FFFFFFFu;
 struct alignas(16) Node {
     float4 q0, q1, q2;
     uint4 q3;

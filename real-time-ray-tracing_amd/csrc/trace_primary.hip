@@ -5,9 +5,8 @@
 // pathtrace.cuh:116-129) + RaySceneIntersect geometry (traverse.cuh:64-222) per pixel.
 // 256-thread workgroups cover 16x16 pixels; each wave64 owns an 8x8 tile so its rays are
 // coherent.  Of the 16-entry traversal stack, 10 entries live in LDS (20 KB per workgroup) and
-// the deepest 6 in registers (traverse.h trav_step_t).  The iterations are trav_step_pf's: each
-// node's record is loaded as soon as the previous iteration has chosen it (90 VGPRs, five
-// workgroups per CU: 0.160 -> 0.139 ms per 1080p launch).
+// the deepest 6 in registers (traverse.h trav_step<10>); each node's record is loaded by the
+// iteration that chooses it.
 //
 // k_smooth_normals: GenerateSmoothNormals run twice into an un-cleared buffer
 // (kernel.cu:228-257, 313-327), made deterministic: one thread per vertex gathers its
@@ -17,10 +16,6 @@
 #include "traverse.h"
 
 using namespace rtd;
-
-#ifndef RTX_PRIM_PF  // 2: trav_step_pf (record one iteration ahead); 1: trav_run_pf; 0: trav_step_t
-#define RTX_PRIM_PF 2  // measured 0.139 / 0.233 / 0.160 ms per 1080p launch
-#endif
 
 #ifndef RTX_PRIMARY_WPE  // ablation builds only (tools/abl_build.sh): force waves per SIMD
 __global__ __launch_bounds__(256) void k_trace_primary(TracePrimaryParams P) {
@@ -43,13 +38,9 @@ void k_trace_primary(TracePrimaryParams P) {
     F2 sampleUv;
     generate_ray(P.cam, x, y, pix, ap, org, dir, centerDir, sampleUv);
 
-    SceneView sc;
-    sc.triPos = P.triPos;
-    sc.triNrm = P.triNrm;
-    sc.nodes = (const Node*)P.nodes;
-    sc.tlas = (const Node*)P.tlasNodes;
+    const SceneView sc = scene_view(P.nodes, P.tlasNodes, P.triPos, P.triNrm);
     HitInfo hi;
-    intersect<kLds, RTX_PRIM_PF>(sc, org, dir, stk + tid, 256, hi);
+    intersect<kLds>(sc, org, dir, stk + tid, 256, hi);
 
     const size_t p = (size_t)y * P.width + x;
     P.hitOut[p] = make_float4(hi.t, __int_as_float(hi.objectIdx), hi.u, hi.v);

@@ -29,38 +29,15 @@ constexpr uint32_t kTrace3Short = 1u << 20;  // queue-3 length below which trace
 #define RTX_LEAF_BATCH 1
 #endif
 constexpr bool kLeafBatch = RTX_LEAF_BATCH != 0;  // ablation: -DRTX_LEAF_BATCH=0
-#ifndef RTX_TRAV_PF
-#define RTX_TRAV_PF 1
-#endif
-constexpr bool kPrefetch = RTX_TRAV_PF != 0;  // next record loaded one iteration ahead (ablation: 0)
-#ifndef RTX_TAIL_RUN  // A/B only: tail rays finished by trav_run_pf (while-while) — measured slower,
-#define RTX_TAIL_RUN 0  // lone ray 0.423 -> 0.495 us/iteration, frame 0.898 -> 0.944 ms
-#endif
-constexpr bool kTailRun = RTX_TAIL_RUN != 0;
-
-// one TraverseBvh iteration of this lane's ray (trav_step_pf, or trav_step_t without the prefetch)
-#ifndef RTX_STEP2
-#define RTX_STEP2 0
-#endif
-RT_DEV bool step(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk) {
-    if (kPrefetch && RTX_STEP2) return trav_step_pf2<16>(sc, r, s, rec, stk, kTraceBlock, nullptr);
-    if (kPrefetch) return trav_step_pf<16>(sc, r, s, rec, stk, kTraceBlock, nullptr);
-    return trav_step(sc, r, s, stk, kTraceBlock);
-}
-
 template <int kStep>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) {
-    __shared__ uint2 stk[16 * kTraceBlock];
+    __shared__ uint2 stk[17 * kTraceBlock];  // 16 entries + the dead slot trav_step stores above the top
     const int tid = threadIdx.x;
     const int lane = (int)__lane_id();
     const PtQueue& q = kStep == 3 ? P.ws.q3 : P.ws.q4;
     const uint32_t n = P.ws.counters[kStep == 3 ? kCntQ3 : kCntQ4];
     uint32_t* fetchCounters = P.ws.fetch + (kStep == 3 ? 0 : kParts * 16);
-    SceneView sc;
-    sc.triPos = P.triPos;
-    sc.triNrm = P.triNrm;
-    sc.nodes = (const Node*)P.nodes;
-    sc.tlas = (const Node*)P.tlasNodes;
+    const SceneView sc = scene_view(P.nodes, P.tlasNodes, P.triPos, P.triNrm);
 
     // a short queue 3 runs on the first trace3ShortBlocks workgroups only (frame.cpp); the others
     // leave before taking any work, and the static first batches are cut over the ones that stay
@@ -76,9 +53,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
     uint32_t idx = 0, accV = 0, accT = 0;
     TravRay r;
     TravState s;
-    TravRec rec;  // the record the lane's next iteration processes (trav_step_pf)
+    TravRec rec;  // the record the lane's next iteration processes
     r.org = f3(0.0f);
-    trav_init(s);
+    trav_init(s, sc.root);
 #pragma unroll 1
     while (true) {
         const unsigned long long need = __ballot(!active && !exhausted);
@@ -94,8 +71,8 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
                     idx = f.resLo + rank;
                     const float4 o = q.rayO[idx], d = q.rayD[idx];
                     trav_setup(sc, f3(o.x, o.y, o.z), f3(d.x, d.y, d.z), r);
-                    trav_init(s);
-                    if (kPrefetch) rec = trav_first_rec(sc);
+                    trav_init(s, sc.root);
+                    rec = trav_first_rec(sc);
                     active = true;
                     occlusion = kStep == 4 || (__float_as_uint(d.w) & kQShadowFlag) != 0u;
                 } else if (none) {
@@ -111,19 +88,14 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
         // kernel's tail).  Each ray's steps are unchanged.
         const bool tail = f.resLo == f.resHi && f.drained == (1u << kParts) - 1u;
         if (tail || !kLeafBatch ? active : trav_lane_steps(active, s)) {
-            bool done = false;
-            if (kPrefetch && kTailRun && tail) {  // the rest of the ray in one call (while-while)
-                trav_run_pf<16>(sc, r, s, rec, stk + tid, kTraceBlock, nullptr, occlusion);
-                done = true;
-            } else {
-                do {  // two steps per trip: the loop's refill / exec-mask bookkeeping once per two
-                    done = step(sc, r, s, rec, stk + tid) || s.iters >= 1024u ||
+            bool done;
+            do {  // two steps per trip: the loop's refill / exec-mask bookkeeping once per two
+                done = trav_step<16>(sc, r, s, rec, stk + tid, kTraceBlock, nullptr) || s.iters >= 1024u ||
+                       (occlusion && s.hitIdx >= 0);
+                if (!done && (tail || !kLeafBatch || trav_lane_steps(true, s)))
+                    done = trav_step<16>(sc, r, s, rec, stk + tid, kTraceBlock, nullptr) || s.iters >= 1024u ||
                            (occlusion && s.hitIdx >= 0);
-                    if (!done && (tail || !kLeafBatch || trav_lane_steps(true, s)))
-                        done = step(sc, r, s, rec, stk + tid) || s.iters >= 1024u ||
-                               (occlusion && s.hitIdx >= 0);
-                } while (tail && !done);
-            }
+            } while (tail && !done);
             if (done) {
                 P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);
                 P.ws.hitErr[idx] = s.hitErrT;

@@ -10,8 +10,8 @@
 //
 // GPU mapping: the per-ray box helper is re-expressed per world axis (near/far plane
 // selection by direction sign) so the inner loop indexes nothing dynamically; the stack
-// lives in LDS as [entry][thread] columns (conflict-free ds_read/write_b32); nodes are the
-// canonical 64-B records (4 x dwordx4), triangles 3 x float4.
+// lives in LDS as [entry][thread] columns (conflict-free ds_read/write_b64); every record the
+// traversal reads — BLAS node, TLAS node, triangle — is a 64-B slot of one record arena (below).
 #pragma once
 #include "rt_device.h"
 
@@ -168,12 +168,46 @@ RT_DEV bool watertight(const TriRay& r, F3 org, F3 v1, F3 v2, F3 v3, float tCur,
     return true;
 }
 
+// ---- the record arena
+//
+// One allocation of 64-B records per LBVH set, written by k_build_bvh:
+//
+//   [0, B*1024)              BLAS nodes, batch b's at b*1024 (the reference's per-batch arrays)
+//   [B*1024, B*1024 + B)     TLAS nodes
+//   [B*1024 + B, .. + NP)    triangle records: the three vertices (w = 0), a fourth quad unused
+//
+// A node's boxes sit where the reference's BVHNode keeps them (q0..q2); its fourth quad holds the
+// two children as ready traversal words (q3.x, q3.y) and the reference's child references (q3.z:
+// left | right << 16, leaf = bit 15 of each), from which rt_download rebuilds the reference layout.
+// A traversal word is the arena index of the record the next iteration reads, with the
+// reference's (isLeaf, isBlas) pair on top:
+//
+//   bit 31 leaf, bit 30 BLAS   00 TLAS node   01 BLAS node   10 TLAS leaf   11 BLAS leaf (triangle)
+//
+// A TLAS leaf's word indexes its batch's BLAS root (the iteration at a TLAS leaf only switches
+// to that BLAS, traverse.h:140-145), a BLAS leaf's the triangle record.  So forming the next
+// node, the pushed entry and the record address takes no index arithmetic: a stack entry is
+// (word, t) and a record is arena + 64 * (word & kIdxMask), whatever its kind.
+// (kLeafBit, kBlasBit, kIdxMask: rt_device.h)
+
 struct SceneView {
-    const float4* triPos;   // [N][3]
+    const float4* arena;    // 64-B records (4 float4 each)
+    const float4* tris;     // the arena's triangle records (triangle i at tris + 4 * i)
     const float4* triNrm;   // [N][3]
-    const Node* nodes;      // BLAS, 1024 per batch
-    const Node* tlas;       // TLAS
+    uint32_t root;          // arena index of the TLAS root (B*1024)
+    uint32_t triBase;       // arena index of triangle 0 (B*1024 + B)
 };
+
+// nodes = the arena (its BLAS nodes), tlas = its TLAS nodes, tris = its triangle records
+RT_DEV SceneView scene_view(const void* nodes, const void* tlas, const float4* tris, const float4* triNrm) {
+    SceneView sc;
+    sc.arena = (const float4*)nodes;
+    sc.tris = tris;
+    sc.triNrm = triNrm;
+    sc.root = (uint32_t)(((const float4*)tlas - sc.arena) / 4);
+    sc.triBase = (uint32_t)((tris - sc.arena) / 4);
+    return sc;
+}
 
 struct HitInfo {
     float t;
@@ -187,6 +221,16 @@ struct HitInfo {
     uint32_t visits, tests, dropped, iters;
 };
 
+RT_DEV Node node_at(const SceneView& sc, uint32_t idx) {
+    const float4* p = sc.arena + 4u * idx;
+    Node n;
+    n.q0 = p[0];
+    n.q1 = p[1];
+    n.q2 = p[2];
+    n.q3 = *(const uint4*)(p + 3);
+    return n;
+}
+
 RT_DEV Box node_merged(const Node& n) {
     Box b;
     b.mx = f3(fmx(n.q0.w, n.q2.y), fmx(n.q1.x, n.q2.z), fmx(n.q1.y, n.q2.w));
@@ -196,35 +240,31 @@ RT_DEV Box node_merged(const Node& n) {
 
 RT_DEV F3 f3_of(float4 a) { return f3(a.x, a.y, a.z); }
 
-// stack entry: uint2 {idx (15) | blasOffset (15) << 15 | isBlas << 30 | isLeaf << 31, bits of float t};
-// stk points at this thread's column: entry k lives at [k * stride], so a push is one
-// ds_write_b64 and a pop one ds_read_b64 (the pop loop's dependent LDS round trip).
-//
-// The traversal is split into setup / one loop iteration / hit finalisation so that the
-// inline callers (primary rays, intersect()) and the persistent queue tracer (trace_queue.hip)
-// run the same per-iteration code: one call of trav_step == one iteration of TraverseBvh's
-// loop (traverse.h:120-160), which keeps the 1024-iteration cap exact per ray.
+// The traversal is split into setup / one loop iteration / hit finalisation so that the inline
+// callers (camera and primary rays, intersect()) and the persistent queue tracer (trace_queue.hip)
+// run the same per-iteration code: one call of trav_step == one iteration of TraverseBvh's loop
+// (traverse.h:120-160), which keeps the 1024-iteration cap exact per ray.
 struct TravRay {
     F3 org;
     RayBox h;
     TriRay tr;
 };
 
+// stack entry: uint2 {traversal word, bits of float t}; stk points at this thread's column: entry
+// k lives at [k * stride], so a push is one ds_write_b64 and a pop one ds_read_b64.
 struct TravState {
     float t;
     int hitIdx;
     float hitU, hitV, hitErrT;   // of the closest hit
     float u, v, errT;            // of the last successful triangle test (HitInfo.u/.v)
     int top;
-    uint32_t cIdx, cOff;
-    bool cBlas, cLeaf;
-    float cT;
+    uint32_t cur;                // traversal word of the record this iteration processes
     uint32_t visits, tests, dropped, iters;
 };
 
 RT_DEV void trav_setup(const SceneView& sc, F3 org, F3 dir, TravRay& r) {
     const F3 inv = f3(safe_divide(1.0f, dir.x), safe_divide(1.0f, dir.y), safe_divide(1.0f, dir.z));
-    const Box sceneBox = node_merged(sc.tlas[0]);
+    const Box sceneBox = node_merged(node_at(sc, sc.root));
     r.org = org;
     r.h = make_raybox(org, dir, sceneBox, inv);
     r.tr = make_triray(dir);
@@ -240,7 +280,7 @@ RT_DEV void trav_setup(const SceneView& sc, F3 org, F3 dir, TravRay& r) {
 // merged box) are missed by the exact test, and the ray's result is that first iteration's:
 // a miss after one iteration and one node visit.  Any NaN leaves the ray to the full traversal.
 RT_DEV bool root_surely_missed(const SceneView& sc, F3 org, F3 dir) {
-    const Box b = node_merged(sc.tlas[0]);
+    const Box b = node_merged(node_at(sc, sc.root));
     const float m = 0.01f * fmx(fmx(b.mx.x - b.mn.x, b.mx.y - b.mn.y), b.mx.z - b.mn.z) + 0.01f;
     // the hardware reciprocal (1 ulp): its error is as far below the margin as the helper's
     // rounding; a zero component gives an infinity, and a 0 * inf NaN goes to the full traversal
@@ -254,30 +294,26 @@ RT_DEV bool root_surely_missed(const SceneView& sc, F3 org, F3 dir) {
     return finite && !(tn <= tf && tf > 0.0f);
 }
 
-// the state TraverseBvh ends in for a ray root_surely_missed settles (one root visit, no hit)
-RT_DEV void trav_root_miss(TravState& s);
-
-RT_DEV void trav_init(TravState& s) {
+RT_DEV void trav_init(TravState& s, uint32_t root) {
     s.t = kRayMax;
     s.hitIdx = -1;
     s.hitU = 0.0f; s.hitV = 0.0f; s.hitErrT = 1e-7f;
     s.u = 0.0f; s.v = 0.0f; s.errT = 1e-7f;
     s.top = -1;
-    s.cIdx = 0; s.cOff = 0;
-    s.cBlas = false; s.cLeaf = false;
-    s.cT = -kFltMax;
+    s.cur = root;
     s.visits = 0; s.tests = 0; s.dropped = 0; s.iters = 0;
 }
 
-RT_DEV void trav_root_miss(TravState& s) {
-    trav_init(s);
+// the state TraverseBvh ends in for a ray root_surely_missed settles (one root visit, no hit)
+RT_DEV void trav_root_miss(TravState& s, uint32_t root) {
+    trav_init(s, root);
     s.iters = 1;
     s.visits = 1;
 }
 
-// The deepest entries of the 16-entry stack when the LDS holds fewer (trav_step_t<kLds>): entries
-// kLds .. 15 live in registers, written and read through select chains (no indexed private array,
-// no scratch).  Only rays whose stack grows past kLds entries ever touch them.
+// The deepest entries of the 16-entry stack when the LDS holds fewer (trav_step<kLds < 16>):
+// entries kLds .. 15 live in registers, written and read through select chains (no indexed private
+// array, no scratch).  Only rays whose stack grows past kLds entries ever touch them.
 struct DeepStack {
     uint2 e0, e1, e2, e3, e4, e5;
 };
@@ -294,214 +330,122 @@ RT_DEV unsigned long long deep_get(const DeepStack& d, int k) {
     return ((unsigned long long)v.y << 32) | v.x;
 }
 
-// One loop iteration; returns true when the stack ran empty (TestForFinish, traverse.h:88-105).
-// The caller stops at 1024 iterations as well.
-//
-// Written for a short dependent chain per iteration (a lone wave's traversal latency sets the
-// tail of the queue tracer): the node visit picks the next node and the pushed sibling with
-// selects instead of the reference's four-way branch, and there is a single branch for the push.
-//
-// kLds: stack entries kept in LDS (the others, up to the reference's 16, in `deep`); the camera
-// kernel keeps 10 there, so that six of its workgroups fit a CU's LDS instead of four.
-template <int kLds>
-RT_DEV bool trav_step_t(const SceneView& sc, const TravRay& r, TravState& s, uint2* stk, int stride, DeepStack* deep) {
-    static_assert(kLds >= 10 && kLds <= 16, "LDS stack depth: 10..16 entries (at most 6 in registers)");
-    ++s.iters;
-    bool pop;
-    if (!s.cLeaf) {
-        const Node nd = s.cBlas ? sc.nodes[s.cOff * 1024u + s.cIdx] : sc.tlas[s.cIdx];
-        ++s.visits;
-        float t1, t2;
-        bool i1, i2;
-        box_test2(r.h, nd, i1, i2, t1, t2);
-        // one child hit: go there; both: nearer first (tie -> right), push the other
-        const bool both = i1 && i2;
-        const bool goLeft = both ? (t1 < t2) : i1;
-        const bool push = both && s.top < 15;  // a push onto a full stack is dropped
-        s.dropped += (both && !push) ? 1u : 0u;
-        if (push) {
-            const uint32_t pIdx = goLeft ? nd.q3.y : nd.q3.x;
-            const uint32_t pLeaf = goLeft ? nd.q3.w : nd.q3.z;
-            const uint2 entry = make_uint2((pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) |
-                                               ((s.cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31),
-                                           __float_as_uint(goLeft ? t2 : t1));
-            if (kLds == 16 || s.top + 1 < kLds) stk[(s.top + 1) * stride] = entry;
-            else deep_set(*deep, s.top + 1 - kLds, entry);
-        }
-        s.top += push ? 1 : 0;
-        pop = !i1 && !i2;
-        if (!pop) {
-            s.cIdx = goLeft ? nd.q3.x : nd.q3.y;
-            s.cLeaf = (goLeft ? nd.q3.z : nd.q3.w) != 0u;
-            s.cT = goLeft ? t1 : t2;
-        }
-    } else if (s.cBlas) {
-        const uint32_t li = s.cOff * 1024u + s.cIdx;
-        const float4 p0 = sc.triPos[3 * li], p1 = sc.triPos[3 * li + 1], p2 = sc.triPos[3 * li + 2];
-        ++s.tests;
-        float tt;
-        if (watertight(r.tr, r.org, f3_of(p0), f3_of(p1), f3_of(p2), s.t, tt, s.u, s.v, s.errT) && tt < s.t) {
-            s.t = tt;
-            s.hitIdx = (int)li;
-            s.hitU = s.u; s.hitV = s.v; s.hitErrT = s.errT;
-        }
-        pop = true;
-    } else {  // TLAS leaf: continue at the root of that batch's BLAS
-        s.cLeaf = false;
-        s.cBlas = true;
-        s.cOff = s.cIdx;
-        s.cIdx = 0;
-        pop = false;
-    }
-    if (pop) {  // TestForFinish (traverse.h:88-105)
-        do {
-            if (s.top < 0) return true;
-            // one 8-byte read per pop: volatile keeps the compiler from splitting it into a
-            // t read inside the loop and an index read sunk after it (two dependent round trips)
-            const unsigned long long e = (kLds == 16 || s.top < kLds) ? *(volatile LdsU64*)(&stk[s.top * stride])
-                                                                      : deep_get(*deep, s.top - kLds);
-            const uint32_t a = (uint32_t)e;
-            s.cT = __uint_as_float((uint32_t)(e >> 32));
-            --s.top;
-            s.cIdx = a & 0x7FFFu;
-            s.cOff = (a >> 15) & 0x7FFFu;
-            s.cBlas = (a >> 30) & 1u;
-            s.cLeaf = (a >> 31) & 1u;
-        } while (s.cT > s.t);
-    }
-    return false;
-}
-
-RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, uint2* stk, int stride) {
-    return trav_step_t<16>(sc, r, s, stk, stride, nullptr);
-}
-
-// ---- the same iteration with its memory access one iteration ahead (trav_step_pf)
-//
-// A lone ray's iteration is a dependent chain: the node record arrives, the box tests pick the next
-// node, its address is formed and its record loaded.  In trav_step_t the loop's bookkeeping (the
-// push, counters, the leaf / pop branches' exec-mask work, the loop test) sits between the choice
-// and the next load.  trav_step_pf issues the next record's load as soon as the next node is known
-// and does that bookkeeping while the load is in flight; the record is carried to the next
-// iteration in registers (TravRec).  The iterations themselves — which node or triangle each one
-// tests, the pushes, drops, pops, counters and the 1024 cap — are trav_step_t's exactly.
-//
-// What the record holds for the node an iteration processes:
-//   internal node   its 64-B record (TLAS or BLAS)
-//   BLAS leaf       its triangle's three vertices (48 B; the fourth quad re-reads the first)
-//   TLAS leaf       the root record of that batch's BLAS: the TLAS-leaf iteration needs no data
-//                   (TraverseBvh only switches to the BLAS there), so the BLAS root's load is
-//                   issued when the TLAS leaf is chosen, one iteration earlier than trav_step_t's
+// The record an iteration processes, loaded by the iteration before it (or by trav_first_rec):
+// internal node (TLAS or BLAS) its 64-B record, BLAS leaf its triangle record, TLAS leaf the root
+// record of that batch's BLAS (that iteration reads nothing; the next one reads this again).
 struct TravRec {
     float4 a, b, c;
     uint4 d;
 };
 
-RT_DEV TravRec load_rec(const SceneView& sc, bool leaf, bool blas, uint32_t idx, uint32_t off) {
-    // selects, not branches: the address is on the iteration's critical path
-    const bool tri = leaf && blas;
-    const uint32_t li = off * 1024u + idx;
-    const uint32_t ni = blas ? li : (leaf ? idx * 1024u : idx);
-    const float4* nb = (!leaf && !blas) ? (const float4*)sc.tlas : (const float4*)sc.nodes;
-    const float4* base = tri ? sc.triPos + 3u * li : nb + 4u * ni;  // pointer selects: global loads, not flat
+RT_DEV TravRec trav_load(const SceneView& sc, uint32_t word) {
+    const float4* p = sc.arena + 4u * (word & kIdxMask);
     TravRec rec;
-    rec.a = base[0];
-    rec.b = base[1];
-    rec.c = base[2];
-    rec.d = *(const uint4*)(base + (tri ? 0 : 3));  // no read past the triangle array's end
+    rec.a = p[0];
+    rec.b = p[1];
+    rec.c = p[2];
+    rec.d = *(const uint4*)(p + 3);
     return rec;
 }
 
-// the record of the first iteration (the TLAS root, after trav_init)
-RT_DEV TravRec trav_first_rec(const SceneView& sc) { return load_rec(sc, false, false, 0u, 0u); }
+RT_DEV TravRec trav_first_rec(const SceneView& sc) { return trav_load(sc, sc.root); }
 
-// measurement hook of tools/lat_probe.hip (iteration start, record arrival); empty in the product
+// measurement hook of tools/probe/lat_probe.hip (iteration start, record arrival); empty in the product
 #ifndef RTX_TRAV_HOOK
 #define RTX_TRAV_HOOK(k, s, rec)
 #endif
 
-template <int kLds>
-RT_DEV bool trav_step_pf(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk, int stride,
-                         DeepStack* deep) {
+// One TraverseBvh iteration (traverse.h:120-160); returns true when the stack ran empty
+// (TestForFinish, traverse.h:88-105).  The caller stops at 1024 iterations as well.  On entry rec
+// holds the record of s.cur; on return, that of the new s.cur.
+//
+// A lone ray's iteration is a dependent chain of instructions (tools/probe/lat_probe.hip: its
+// record load is covered, the ~100 instructions are not), so the iteration runs as straight-line
+// code wherever the reference's branches allow it:
+//   - the box tests run on every iteration's record (a leaf's results are masked off);
+//   - the stack top is read at the start whether or not the iteration pops;
+//   - the would-be pushed entry is stored one slot above the top unconditionally (the stack
+//     column has kLds + 1 slots; a slot above the top is dead), when kLds is 16;
+//   - the next record is loaded unconditionally (a TLAS leaf's iteration re-reads its BLAS root);
+//     issuing it before the triangle test instead (in place, the vertices copied out) measured
+//     slower: 0.369 -> 0.405 us per lone-ray iteration, trace<3> 266 -> 270 us;
+// branches remain for the triangle test and for pops past entries farther than the closest hit.
+// The iterations — which node or triangle each one tests, pushes, drops (a push onto a full
+// stack), pops, counters — are TraverseBvh's.
+//
+// kLds: stack entries kept in LDS (the others, up to the reference's 16, in `deep`); the camera
+// and primary-ray kernels keep 10 there, so that six of their workgroups fit a CU's LDS.
+// kCarry false: the iteration loads its own record at its start instead (rec is scratch, nothing
+// is carried from one iteration to the next: 14 fewer registers live across the loop, for kernels
+// whose occupancy the registers set — the camera rays, the fused chain).
+template <int kLds, bool kCarry = true>
+RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk, int stride,
+                      DeepStack* deep) {
     static_assert(kLds >= 10 && kLds <= 16, "LDS stack depth: 10..16 entries (at most 6 in registers)");
+    if (!kCarry) rec = trav_load(sc, s.cur);
     RTX_TRAV_HOOK(0, s, rec);
     RTX_TRAV_HOOK(1, s, rec);
     ++s.iters;
-    bool pop = false, push = false, tlasLeaf = false;
-    uint32_t pIdx = 0u, pLeaf = 0u, pT = 0u;  // the pushed sibling (entry built after the load)
-    uint32_t nIdx = s.cIdx, nOff = s.cOff;
-    bool nBlas = s.cBlas, nLeaf = s.cLeaf;
-    float nT = s.cT;
-    if (!s.cLeaf) {
-        Node nd;
-        nd.q0 = rec.a; nd.q1 = rec.b; nd.q2 = rec.c; nd.q3 = rec.d;
-        ++s.visits;
-        float t1, t2;
-        bool i1, i2;
-        box_test2(r.h, nd, i1, i2, t1, t2);
-        const bool both = i1 && i2;
-        const bool goLeft = both ? (t1 < t2) : i1;
-        push = both && s.top < 15;  // a push onto a full stack is dropped
-        s.dropped += (both && !push) ? 1u : 0u;
-        pIdx = goLeft ? nd.q3.y : nd.q3.x;
-        pLeaf = goLeft ? nd.q3.w : nd.q3.z;
-        pT = __float_as_uint(goLeft ? t2 : t1);
-        pop = !i1 && !i2;
-        nIdx = goLeft ? nd.q3.x : nd.q3.y;
-        nLeaf = (goLeft ? nd.q3.z : nd.q3.w) != 0u;
-        nT = goLeft ? t1 : t2;
-    } else if (s.cBlas) {
-        const uint32_t li = s.cOff * 1024u + s.cIdx;
+    const uint32_t cur = s.cur;
+    const bool isNode = !(cur & kLeafBit);
+    const bool isTri = cur >= (kLeafBit | kBlasBit);
+    const int tp = s.top;
+    // the stack top, read whether or not this iteration pops (kLds 16; with a register part the
+    // pops read where they happen: fewer registers live through the box tests)
+    const unsigned long long e = kLds == 16 ? *(volatile LdsU64*)(&stk[(tp < 0 ? 0 : tp) * stride]) : 0ull;
+    Node nd;
+    nd.q0 = rec.a; nd.q1 = rec.b; nd.q2 = rec.c; nd.q3 = rec.d;
+    float t1, t2;
+    bool i1, i2;
+    box_test2(r.h, nd, i1, i2, t1, t2);
+    i1 = i1 && isNode;
+    i2 = i2 && isNode;
+    // one child hit: go there; both: nearer first (tie -> right), push the other
+    const bool both = i1 && i2;
+    const bool goLeft = i1 && (!i2 || t1 < t2);
+    const bool push = both && tp < 15;  // a push onto a full stack is dropped
+    s.dropped += (both && !push) ? 1u : 0u;
+    s.visits += isNode ? 1u : 0u;
+    const uint2 pushed = make_uint2(goLeft ? rec.d.y : rec.d.x, __float_as_uint(goLeft ? t2 : t1));
+    if (kLds == 16) {
+        stk[(tp + 1) * stride] = pushed;
+    } else if (push) {
+        if (tp + 1 < kLds) stk[(tp + 1) * stride] = pushed;
+        else deep_set(*deep, tp + 1 - kLds, pushed);
+    }
+    uint32_t next = isNode ? (goLeft ? rec.d.x : rec.d.y) : ((cur & kIdxMask) | kBlasBit);  // TLAS leaf: its BLAS
+    const bool pop = isTri || (isNode && !i1 && !i2);
+    bool done = kLds == 16 && pop && tp < 0;
+    int top = (pop && kLds == 16) ? tp - 1 : ((push && !pop) ? tp + 1 : tp);
+    next = (pop && kLds == 16) ? (uint32_t)e : next;
+    // kLds 16: the popped entry is e, and the loop pops on past entries farther than the closest
+    // hit; otherwise the loop makes every pop (a +inf start enters it)
+    float et = pop ? (kLds == 16 ? __uint_as_float((uint32_t)(e >> 32)) : __builtin_inff()) : -kFltMax;
+    if (isTri) {  // after the box tests' values are spent: fewer registers live through it
         ++s.tests;
         float tt;
         if (watertight(r.tr, r.org, f3_of(rec.a), f3_of(rec.b), f3_of(rec.c), s.t, tt, s.u, s.v, s.errT) && tt < s.t) {
             s.t = tt;
-            s.hitIdx = (int)li;
+            s.hitIdx = (int)((cur & kIdxMask) - sc.triBase);
             s.hitU = s.u; s.hitV = s.v; s.hitErrT = s.errT;
         }
-        pop = true;
-    } else {  // TLAS leaf: continue at the root of that batch's BLAS, whose record is already here
-        tlasLeaf = true;
-        nLeaf = false;
-        nBlas = true;
-        nOff = s.cIdx;
-        nIdx = 0u;
     }
-    if (pop) {  // TestForFinish (traverse.h:88-105); no push happened in this iteration
-        int top = s.top;
-        do {
-            if (top < 0) {
-                s.top = top;
-                return true;
-            }
-            const unsigned long long e = (kLds == 16 || top < kLds) ? *(volatile LdsU64*)(&stk[top * stride])
-                                                                    : deep_get(*deep, top - kLds);
-            const uint32_t a = (uint32_t)e;
-            nT = __uint_as_float((uint32_t)(e >> 32));
-            --top;
-            nIdx = a & 0x7FFFu;
-            nOff = (a >> 15) & 0x7FFFu;
-            nBlas = (a >> 30) & 1u;
-            nLeaf = (a >> 31) & 1u;
-        } while (nT > s.t);
-        s.top = top;
+    while (!done && et > s.t) {  // pop (past entries farther than the closest hit)
+        if (top < 0) {
+            done = true;
+            break;
+        }
+        const unsigned long long f = (kLds == 16 || top < kLds) ? *(volatile LdsU64*)(&stk[top * stride])
+                                                                : deep_get(*deep, top - kLds);
+        next = (uint32_t)f;
+        et = __uint_as_float((uint32_t)(f >> 32));
+        --top;
     }
-    // the next iteration's record, before the bookkeeping below
-    if (!tlasLeaf) rec = load_rec(sc, nLeaf, nBlas, nIdx, nOff);
-    if (push) {
-        const uint2 entry = make_uint2((pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) | ((s.cBlas ? 1u : 0u) << 30) |
-                                           ((pLeaf ? 1u : 0u) << 31),
-                                       pT);
-        if (kLds == 16 || s.top + 1 < kLds) stk[(s.top + 1) * stride] = entry;
-        else deep_set(*deep, s.top + 1 - kLds, entry);
-        ++s.top;
-    }
-    s.cIdx = nIdx;
-    s.cOff = nOff;
-    s.cBlas = nBlas;
-    s.cLeaf = nLeaf;
-    s.cT = nT;
-    return false;
+    next = done ? cur : next;  // a finished ray loads a record that exists
+    if (kCarry) rec = trav_load(sc, next);
+    s.top = top;
+    s.cur = next;
+    return done;
 }
 
 // Wave-level leaf batching for the lanes of one wave that each run their own traversal: a lane
@@ -510,7 +454,7 @@ RT_DEV bool trav_step_pf(const SceneView& sc, const TravRay& r, TravState& s, Tr
 // every trip of the loop.  Each ray's own sequence of steps is unchanged (a waiting lane only
 // pauses), hence its hits, counters and 1024-step cap.  Returns whether this lane steps now.
 RT_DEV bool trav_lane_steps(bool active, const TravState& s) {
-    const bool atLeaf = active && s.cLeaf && s.cBlas;
+    const bool atLeaf = active && s.cur >= (kLeafBit | kBlasBit);
     const unsigned long long lm = __ballot(atLeaf), am = __ballot(active);
     const int nl = __popcll(lm), na = __popcll(am);
     const bool doLeaf = nl >= 16 || nl * 4 >= na;
@@ -523,7 +467,8 @@ RT_DEV void finalize_hit(const SceneView& sc, F3 org, F3 dir, float t, int hitId
     F3 nrm = f3(0.0f), pos = f3(kRayMax), fake = f3(0.0f);
     float offset = 1e-7f;
     if (hitIdx >= 0) {
-        const F3 v1 = f3_of(sc.triPos[3 * hitIdx]), v2 = f3_of(sc.triPos[3 * hitIdx + 1]), v3 = f3_of(sc.triPos[3 * hitIdx + 2]);
+        const float4* tp = sc.tris + 4 * hitIdx;
+        const F3 v1 = f3_of(tp[0]), v2 = f3_of(tp[1]), v3 = f3_of(tp[2]);
         nrm = normalize(cross(v2 - v1, v3 - v1));
         const float w = -dot(nrm, v1);
         const F3 p = org + dir * t;
@@ -553,233 +498,21 @@ RT_DEV void finalize_hit(const SceneView& sc, F3 org, F3 dir, float t, int hitId
     out.hit = hit;
 }
 
-// trav_step_pf with one divergent region.  The internal-node case — nine iterations in ten — runs
-// straight through: the box tests run for every iteration (on a leaf's record their results are
-// unused), the next node and the push are selects, and only a leaf iteration or a pop enters the
-// branch.  A TLAS leaf's BLAS root is loaded again at its own iteration (a cache hit) rather than
-// carried, so the record load is unconditional.  Same iterations, pushes, drops, pops and counters
-// as trav_step_pf.
-template <int kLds>
-RT_DEV bool trav_step_pf2(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk, int stride,
-                          DeepStack* deep) {
-    static_assert(kLds >= 10 && kLds <= 16, "LDS stack depth: 10..16 entries (at most 6 in registers)");
-    ++s.iters;
-    Node nd;
-    nd.q0 = rec.a; nd.q1 = rec.b; nd.q2 = rec.c; nd.q3 = rec.d;
-    float t1, t2;
-    bool i1, i2;
-    box_test2(r.h, nd, i1, i2, t1, t2);
-    const bool node = !s.cLeaf;
-    const bool both = i1 && i2;
-    const bool goLeft = both ? (t1 < t2) : i1;
-    const bool push = node && both && s.top < 15;  // a push onto a full stack is dropped
-    s.visits += node ? 1u : 0u;
-    s.dropped += (node && both && !push) ? 1u : 0u;
-    const uint32_t pIdx = goLeft ? nd.q3.y : nd.q3.x;
-    const uint32_t pLeaf = goLeft ? nd.q3.w : nd.q3.z;
-    const uint32_t pT = __float_as_uint(goLeft ? t2 : t1);
-    uint32_t nIdx = goLeft ? nd.q3.x : nd.q3.y;
-    bool nLeaf = (goLeft ? nd.q3.z : nd.q3.w) != 0u;
-    float nT = goLeft ? t1 : t2;
-    uint32_t nOff = s.cOff;
-    bool nBlas = s.cBlas;
-    if (!node || (!i1 && !i2)) {  // a leaf iteration, or a node whose children both missed
-        bool pop = node;
-        if (!node) {
-            if (s.cBlas) {
-                const uint32_t li = s.cOff * 1024u + s.cIdx;
-                ++s.tests;
-                float tt;
-                if (watertight(r.tr, r.org, f3_of(rec.a), f3_of(rec.b), f3_of(rec.c), s.t, tt, s.u, s.v, s.errT) &&
-                    tt < s.t) {
-                    s.t = tt;
-                    s.hitIdx = (int)li;
-                    s.hitU = s.u; s.hitV = s.v; s.hitErrT = s.errT;
-                }
-                pop = true;
-            } else {  // TLAS leaf: continue at the root of that batch's BLAS
-                nLeaf = false;
-                nBlas = true;
-                nOff = s.cIdx;
-                nIdx = 0u;
-                nT = s.cT;
-            }
-        }
-        if (pop) {  // TestForFinish (traverse.h:88-105)
-            int top = s.top;
-            do {
-                if (top < 0) {
-                    s.top = top;
-                    return true;
-                }
-                const unsigned long long e = (kLds == 16 || top < kLds) ? *(volatile LdsU64*)(&stk[top * stride])
-                                                                        : deep_get(*deep, top - kLds);
-                const uint32_t a = (uint32_t)e;
-                nT = __uint_as_float((uint32_t)(e >> 32));
-                --top;
-                nIdx = a & 0x7FFFu;
-                nOff = (a >> 15) & 0x7FFFu;
-                nBlas = (a >> 30) & 1u;
-                nLeaf = (a >> 31) & 1u;
-            } while (nT > s.t);
-            s.top = top;
-        }
-    }
-    // the pushed entry is formed before the load, so the current record's registers are free for
-    // the next one (otherwise the compiler loads into other registers and waits to copy them back)
-    uint32_t eA = (pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) | ((s.cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31);
-    uint32_t eT = pT;
-    asm volatile("" : "+v"(eA), "+v"(eT)::"memory");
-    rec = load_rec(sc, nLeaf, nBlas, nIdx, nOff);
-    if (push) {
-        const uint2 entry = make_uint2(eA, eT);
-        if (kLds == 16 || s.top + 1 < kLds) stk[(s.top + 1) * stride] = entry;
-        else deep_set(*deep, s.top + 1 - kLds, entry);
-        ++s.top;
-    }
-    s.cIdx = nIdx;
-    s.cOff = nOff;
-    s.cBlas = nBlas;
-    s.cLeaf = nLeaf;
-    s.cT = nT;
-    return false;
-}
-
-// A whole traversal, from the lane's current state to its end, as nested loops (while-while,
-// Aila & Laine 2009): an inner loop over internal nodes — box test, the next record's load, the
-// push — and between its runs the leaf steps (the triangle test, or the TLAS leaf's switch to its
-// BLAS) and the pops.  A lone ray's internal-node iterations then skip the leaf and pop branches'
-// exec-mask work.  Each ray's iterations, pushes, drops, pops and counters are trav_step_pf's, and
-// it stops where `trav_step_pf(...) || s.iters >= 1024 || (occlusion && s.hitIdx >= 0)` would
-// (an occlusion ray stops right after its hitting test: the pop that would follow changes nothing
-// the caller reads).  rec holds the record of the lane's current node on entry.
-//
-// kPf false: the same loops with each record loaded where it is used (no record carried across
-// iterations: fewer registers live through the loop, for kernels whose occupancy they set).
-template <int kLds, bool kPf = true>
-RT_DEV void trav_run_pf(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk, int stride,
-                        DeepStack* deep, bool occlusion) {
-    static_assert(kLds >= 10 && kLds <= 16, "LDS stack depth: 10..16 entries (at most 6 in registers)");
-#pragma unroll 1
-    while (true) {
-        bool pop = false;
-#pragma unroll 1
-        while (!s.cLeaf) {  // internal nodes
-            if (!kPf) rec = load_rec(sc, false, s.cBlas, s.cIdx, s.cOff);
-            Node nd;
-            nd.q0 = rec.a; nd.q1 = rec.b; nd.q2 = rec.c; nd.q3 = rec.d;
-            ++s.iters;
-            ++s.visits;
-            float t1, t2;
-            bool i1, i2;
-            box_test2(r.h, nd, i1, i2, t1, t2);
-            if (!i1 && !i2) {
-                pop = true;
-                break;
-            }
-            const bool both = i1 && i2;
-            const bool goLeft = both ? (t1 < t2) : i1;
-            const bool push = both && s.top < 15;  // a push onto a full stack is dropped
-            s.dropped += (both && !push) ? 1u : 0u;
-            const uint32_t nIdx = goLeft ? nd.q3.x : nd.q3.y;
-            const bool nLeaf = (goLeft ? nd.q3.z : nd.q3.w) != 0u;
-            const float nT = goLeft ? t1 : t2;
-            if (kPf) rec = load_rec(sc, nLeaf, s.cBlas, nIdx, s.cOff);  // the next record, before the push
-            if (push) {
-                const uint32_t pIdx = goLeft ? nd.q3.y : nd.q3.x;
-                const uint32_t pLeaf = goLeft ? nd.q3.w : nd.q3.z;
-                const uint2 entry = make_uint2((pIdx & 0x7FFFu) | ((s.cOff & 0x7FFFu) << 15) |
-                                                   ((s.cBlas ? 1u : 0u) << 30) | ((pLeaf ? 1u : 0u) << 31),
-                                               __float_as_uint(goLeft ? t2 : t1));
-                if (kLds == 16 || s.top + 1 < kLds) stk[(s.top + 1) * stride] = entry;
-                else deep_set(*deep, s.top + 1 - kLds, entry);
-                ++s.top;
-            }
-            s.cIdx = nIdx;
-            s.cLeaf = nLeaf;
-            s.cT = nT;
-            if (s.iters >= 1024u) return;
-        }
-        if (!pop) {
-            ++s.iters;
-            if (!s.cBlas) {  // TLAS leaf: continue at the root of that batch's BLAS, whose record is here
-                s.cLeaf = false;
-                s.cBlas = true;
-                s.cOff = s.cIdx;
-                s.cIdx = 0u;
-                if (s.iters >= 1024u) return;
-                continue;
-            }
-            const uint32_t li = s.cOff * 1024u + s.cIdx;
-            if (!kPf) rec = load_rec(sc, true, true, s.cIdx, s.cOff);
-            ++s.tests;
-            float tt;
-            if (watertight(r.tr, r.org, f3_of(rec.a), f3_of(rec.b), f3_of(rec.c), s.t, tt, s.u, s.v, s.errT) &&
-                tt < s.t) {
-                s.t = tt;
-                s.hitIdx = (int)li;
-                s.hitU = s.u; s.hitV = s.v; s.hitErrT = s.errT;
-            }
-            if (occlusion && s.hitIdx >= 0) return;
-        }
-        // TestForFinish (traverse.h:88-105)
-        int top = s.top;
-        uint32_t nIdx = 0u, nOff = 0u;
-        bool nBlas = false, nLeaf = false;
-        float nT = 0.0f;
-        do {
-            if (top < 0) {
-                s.top = top;
-                return;
-            }
-            const unsigned long long e = (kLds == 16 || top < kLds) ? *(volatile LdsU64*)(&stk[top * stride])
-                                                                    : deep_get(*deep, top - kLds);
-            const uint32_t a = (uint32_t)e;
-            nT = __uint_as_float((uint32_t)(e >> 32));
-            --top;
-            nIdx = a & 0x7FFFu;
-            nOff = (a >> 15) & 0x7FFFu;
-            nBlas = (a >> 30) & 1u;
-            nLeaf = (a >> 31) & 1u;
-        } while (nT > s.t);
-        s.top = top;
-        if (kPf) rec = load_rec(sc, nLeaf, nBlas, nIdx, nOff);
-        s.cIdx = nIdx;
-        s.cOff = nOff;
-        s.cBlas = nBlas;
-        s.cLeaf = nLeaf;
-        s.cT = nT;
-        if (s.iters >= 1024u) return;
-    }
-}
-
-// kLds as in trav_step_t: the stack entries kept in LDS (k_trace_primary keeps 10); kPf: the
-// iterations of trav_step_pf (record loaded one iteration ahead) run by trav_run_pf
-template <int kLds = 16, int kPf = 0>  // kPf 0: trav_step_t, 1: trav_run_pf, 2: trav_step_pf (A/B)
+// One ray's closest hit (RaySceneIntersect): scene cull, then trav_step to the end.  stk: this
+// thread's stack column (kLds + 1 slots when kLds is 16).
+template <int kLds = 16>
 RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint2* stk, int stride, HitInfo& out) {
     TravState s;
     if (root_surely_missed(sc, org, dir)) {
-        trav_root_miss(s);
+        trav_root_miss(s, sc.root);
     } else {
         TravRay r;
         trav_setup(sc, org, dir, r);
-        trav_init(s);
+        trav_init(s, sc.root);
         DeepStack deep;
-        if (kPf == 1) {
-            TravRec rec = trav_first_rec(sc);
-            trav_run_pf<kLds>(sc, r, s, rec, stk, stride, &deep, false);
-        } else if (kPf == 2) {
-            TravRec rec = trav_first_rec(sc);
-            for (int it = 0; it < 1024; ++it)
-                if (trav_step_pf<kLds>(sc, r, s, rec, stk, stride, &deep)) break;
-        } else if (kPf == 3) {
-            TravRec rec = trav_first_rec(sc);
-            for (int it = 0; it < 1024; ++it)
-                if (trav_step_pf2<kLds>(sc, r, s, rec, stk, stride, &deep)) break;
-        } else {
-            for (int it = 0; it < 1024; ++it)
-                if (trav_step_t<kLds>(sc, r, s, stk, stride, &deep)) break;
-        }
+        TravRec rec = trav_first_rec(sc);
+        for (int it = 0; it < 1024; ++it)
+            if (trav_step<kLds>(sc, r, s, rec, stk, stride, &deep)) break;
     }
     finalize_hit(sc, org, dir, s.t, s.hitIdx, s.hitU, s.hitV, s.hitErrT, out);
     out.u = s.u;

@@ -26,7 +26,8 @@ ARR = dict(VERTICES=0, INDICES=1, NORMALS=2, TRI_POS=3, AABBS=4, MORTON=5, REORD
            HIT_NORMALS=15, HIT_FAKE_NORMALS=16, HIT_STATS=17, TRI_NRM=18, RAYS=19, SKY_PDF=20, SKY_CDF=21,
            SUN_PDF=22, SUN_CDF=23, SUN_DIR=24, HISTOGRAM=25, EXPOSURE=26, COLOR4=27, COLOR16=28, COLOR64=29,
            RGBA8=30, PT_STATS=31, PT_QUEUE=32, PT_Q3_ORIGINS=33, PT_Q3_DIRS=34,
-           PT_Q4_ORIGINS=35, PT_Q4_DIRS=36, TEX_ALBEDO_AO=37, TEX_NORMAL_ROUGHNESS=38, TEX_HEIGHT=39, HDR=40)
+           PT_Q4_ORIGINS=35, PT_Q4_DIRS=36, TEX_ALBEDO_AO=37, TEX_NORMAL_ROUGHNESS=38, TEX_HEIGHT=39, HDR=40,
+           BVH_ARENA=41)
 TEX = dict(SOIL_ALBEDO_AO=0, SOIL_NORMAL_ROUGHNESS=1, SOIL_HEIGHT=2)  # MipmapTextureName (texture.h:5-12)
 # rt_buffer_name (Buffer2DName, kernel.cuh:286-315)
 BUF = dict(RENDER_COLOR=0, ACCUMULATION=1, HISTORY_COLOR=2, SCALED_COLOR=3, NORMAL=10, DEPTH=11, HISTORY_DEPTH=12,

@@ -413,7 +413,10 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, TravR
         if (tp + 1 < kLds) stk[(tp + 1) * stride] = pushed;
         else deep_set(*deep, tp + 1 - kLds, pushed);
     }
-    uint32_t next = isNode ? (goLeft ? rec.d.x : rec.d.y) : ((cur & kIdxMask) | kBlasBit);  // TLAS leaf: its BLAS
+    // the next node: the chosen child, or at a TLAS leaf (10 -> 01) its BLAS root; as mask
+    // arithmetic on the leaf bit (a ternary on isNode became a branch)
+    const uint32_t nodeNext = goLeft ? rec.d.x : rec.d.y;
+    uint32_t next = nodeNext ^ ((nodeNext ^ cur ^ (kLeafBit | kBlasBit)) & (uint32_t)((int)cur >> 31));
     const bool pop = isTri || (isNode && !i1 && !i2);
     bool done = kLds == 16 && pop && tp < 0;
     int top = (pop && kLds == 16) ? tp - 1 : ((push && !pop) ? tp + 1 : tp);

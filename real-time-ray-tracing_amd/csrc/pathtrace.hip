@@ -485,7 +485,11 @@ __global__ __launch_bounds__(256, 6) RTX_CAM_ATTR void k_pt_camera(PathTracePara
             generate_ray_jittered(P.cam, x, y, F2{rnd(c, 0, 0), rnd(c, 0, 1)}, F2{rnd(c, 0, 2), rnd(c, 0, 3)}, org,
                                   dir, uv);
             TravState st;
+#if defined(RTX_CAM_ABL) && RTX_CAM_ABL == 1  // timing ablation only: no traversal (every ray culled)
+            if (true) {
+#else
             if (root_surely_missed(sc, org, dir)) {  // most sky rays: settled without the ray-box helper
+#endif
                 trav_root_miss(st, sc.root);
                 ++camCull;
             } else {
@@ -521,7 +525,11 @@ __global__ __launch_bounds__(256, 6) RTX_CAM_ATTR void k_pt_camera(PathTracePara
                 v.rs.albedo = f3(1.0f);
                 v.beta0 = f3(1.0f);
                 v.beta1 = f3(1.0f);
+#if defined(RTX_CAM_ABL) && RTX_CAM_ABL == 2  // timing ablation only: no sky colour
+                const F3 Ls = dir;
+#else
                 const F3 Ls = finish(c, v);
+#endif
                 out = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
             }
         }
@@ -795,7 +803,11 @@ RT_DEV void store_path_L(const PathCtx& c, const PathVars& v, uint32_t p, uint32
 
 // Resumes the samples of queue kStep (3 or 4) once k_trace_queue has written their hits.
 template <int kStep, bool kMF>
+#ifndef RTX_CTX_PRIO  // A/B: wave priority (s_setprio) of the context stream's tracers and resume kernels
+#define RTX_CTX_PRIO 0
+#endif
 __global__ __launch_bounds__(256, kMF ? 2 : 3) void k_pt_resume(PathTraceParams P) {
+    if (RTX_CTX_PRIO > 0) __builtin_amdgcn_s_setprio(RTX_CTX_PRIO);
     __shared__ uint32_t sob[256];
     __shared__ unsigned long long wgRays[4];
     // step 4 ends the path before any diffuse interaction: no light sampling there

@@ -1091,7 +1091,11 @@ __global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const u
         }
     } im{sS, X0, Y0, Ws, Hs};
     uint2 cur = im.at(x, y);
+#if defined(RTX_SP_ABL) && RTX_SP_ABL == 4  // timing ablation only: no sharpen
+    if (false) {
+#else
     if (P.sharpen) {
+#endif
         F3 c[3][3];
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -1115,15 +1119,22 @@ __global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const u
         o = o / (f3(1.0f) + f3(4.0f) * w);
         cur = pack_color(o, 0x3C00u);
     }
+#if !(defined(RTX_SP_ABL) && RTX_SP_ABL == 2)  // timing ablation only: no tone map
     if (P.tonemap) {
         const F3 c = tonemap_color(rgb_of(cur) * P.exposure[0], P.toneMappingType, P.maxWhite, P.gamma);
         cur = pack_color(c, 0x3C00u);
     }
+#endif
     P.scaledB[p] = cur;
     // CopyToOutput (kernel.cu:26-59): blue-noise dither (bn/256; the -1/512 is integer 0)
     const int s = P.frameNum;
+#if defined(RTX_SP_ABL) && RTX_SP_ABL == 3  // timing ablation only: no dither
+    F3 c = rgb_of(cur);
+    (void)s;
+#else
     F3 c = rgb_of(cur) + f3(bluenoise(P.bluenoise, x, y, s, 0) / 256, bluenoise(P.bluenoise, x, y, s, 1) / 256,
                             bluenoise(P.bluenoise, x, y, s, 2) / 256);
+#endif
     const float hi = 1.0f - 1.1920928955078125e-07f;
     c = clamp3(c, f3(0.0f), f3(hi));
     P.rgba[(size_t)y * P.rgbaPitch + x] = (uint32_t)(uint8_t)(c.x * 256) | ((uint32_t)(uint8_t)(c.y * 256) << 8) |
@@ -1170,7 +1181,10 @@ void tile_range(const DenoisePostParams* P, int halo, int& t0, int& t1) {
 // phase 0: TemporalSpatialDenoising + DownScale4 + Histogram2 (the histogram is this strip's share
 // when strip-local); phase 1: AutoExposure onwards.  A multi-GPU host sums the histograms between
 // the phases.
+static hipError_t denoise_phase3(DenoisePostParams* P, hipStream_t s);
+
 extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int phase) {
+    if (phase == 3) return denoise_phase3(P, s);
     const int W = (int)P->W, H = (int)P->H, Ws = (int)P->Ws, Hs = (int)P->Hs;
     const size_t Pn = (size_t)W * H;
     const dim3 b256(256);
@@ -1322,6 +1336,33 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         }
         cur = dst;
     }
+    P->svgfOut = cur;
+    P->histDepthDone = histDepthDone ? 1 : 0;
+    if (phase == 2) return hipSuccess;
+    return rtk_denoise_phase(P, s, 3);
+}
+
+// phase 3: TemporalFilter2 onwards, up to the histogram (the tail of phase 0)
+static hipError_t denoise_phase3(DenoisePostParams* P, hipStream_t s) {
+    const int W = (int)P->W, H = (int)P->H;
+    const size_t Pn = (size_t)W * H;
+    const dim3 b256(256);
+    const int W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16b = (W4 + 3) / 4, H16b = (H4 + 3) / 4, W64 = (W16b + 3) / 4,
+              H64 = (H16b + 3) / 4;
+    hipError_t e;
+    auto tiles = [&](int halo, DenoisePostParams& Q, dim3& g) {
+        int t0, t1;
+        tile_range(P, halo, t0, t1);
+        Q = *P;
+        Q.ty0 = t0;
+        Q.ty1 = t1;
+        g = dim3((W + 15) / 16, (unsigned)(t1 > t0 ? t1 - t0 : 0));
+        return t1 > t0;
+    };
+    DenoisePostParams Q;
+    dim3 g;
+    uint2* cur = P->svgfOut;
+    const bool histDepthDone = P->histDepthDone != 0;
     if (P->temporal2) {
         if (P->frameNum != 1) {
             if (tiles(1, Q, g)) {

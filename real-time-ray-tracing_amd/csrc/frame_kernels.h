@@ -213,10 +213,14 @@ struct DenoisePostParams {
     uint32_t* chainCounter;     // k_downscale_chain's workgroup counter (zero between launches)
     int exposureDone;           // set by phase 0 when k_downscale_chain ran AutoExposure
     int histDepthInTemporal;    // k_temporal also copies depth into the history depth (per launch)
+    uint2* svgfOut;             // phase 2 -> 3: the colour buffer TemporalSpatialDenoising ended in
+    int histDepthDone;          // phase 2 -> 3: k_temporal already wrote the history depth
 };
 
 extern "C" hipError_t rtk_denoise_post(DenoisePostParams* p, hipStream_t stream);
-// phase 0: denoise .. DownScale4 + Histogram2; phase 1: AutoExposure .. RGBA8 (finalColor of phase 0 in)
+// phase 0: denoise .. DownScale4 + Histogram2; phase 1: AutoExposure .. RGBA8 (finalColor of phase 0 in).
+// Phase 0 = phase 2 (TemporalSpatialDenoising: TemporalFilter .. the a-trous passes) then phase 3
+// (TemporalFilter2 .. Histogram2).
 extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* p, hipStream_t stream, int phase);
 // the render-size float4 HDR copy (rt_draw's hdr_out) of a denoised colour buffer
 extern "C" hipError_t rtk_hdr_out(const uint2* color, float4* hdr, size_t n, hipStream_t stream);

@@ -374,12 +374,25 @@ RT_DEV void refit(Lds<kThr>& s, const float* leafG, int n, Node* nodes, const Wo
     }
 }
 
+// Timing-only builds (-DRTX_BVH_STAMPS, tools/lbvh_stamps.py): s_memtime at the phase boundaries of
+// each workgroup (slots 1..6) and s_memrealtime at its start and end (0, 7), kept by thread 0 and
+// written over the last 8 Morton keys of its batch at the end
+#ifdef RTX_BVH_STAMPS
+#define BVH_STAMP(k) do { if (threadIdx.x == 0) g_stamp[k] = (uint32_t)__builtin_readcyclecounter(); } while (0)
+#define BVH_RSTAMP(k) do { if (threadIdx.x == 0) g_stamp[k] = (uint32_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+__shared__ uint32_t g_stamp[8];
+#else
+#define BVH_STAMP(k) do { } while (0)
+#define BVH_RSTAMP(k) do { } while (0)
+#endif
+
 // Sort the keys in key0/idx0 and build the tree of n leaves into `nodes`.
 template <int kThr>
 RT_DEV void sort_and_build(Lds<kThr>& s, const float* leafG, int n, uint32_t* mortonOut, uint32_t* reorderOut,
                            Node* nodes, const WordCtx& w) {
     __syncthreads();
     radix_sort(s);
+    BVH_STAMP(3);
 #pragma unroll
     for (int j = 0; j < kBatch / kThr; ++j) {
         const int e = threadIdx.x + j * kThr;
@@ -388,6 +401,7 @@ RT_DEV void sort_and_build(Lds<kThr>& s, const float* leafG, int n, uint32_t* mo
     }
     karras(s, n);
     __syncthreads();
+    BVH_STAMP(4);
 #if !(defined(RTX_BVH_ABL) && RTX_BVH_ABL == 3)
     refit(s, leafG, n, nodes, w);  // (ablation 3: no refit; timing only)
 #endif
@@ -454,6 +468,8 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
     const int t = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const uint32_t B = P.batchCount;
+    BVH_RSTAMP(0);
+    BVH_STAMP(1);
     const uint32_t start = b * kBatch;
     const uint32_t cnt = (b + 1 < B) ? (uint32_t)kBatch : P.triCount - (B - 1) * kBatch;  // init.cu:129-130
     const uint32_t active = (((cnt - 1) >> 2) + 1) << 2;  // triangles of threads with tid*4 <= cnt-1
@@ -509,7 +525,10 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
 
     Node* const nodes = (Node*)P.nodes;
     const WordCtx blasWords{kBlasBit, start, kLeafBit | kBlasBit, B * (uint32_t)kBatch + B + start, 1u};
+    BVH_STAMP(2);
     sort_and_build(s, leafG, (int)cnt, P.morton + start, P.reorder + start, nodes + start, blasWords);
+    __syncthreads();
+    BVH_STAMP(5);
 
     // ---- arrival: the last workgroup builds the TLAS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -526,9 +545,19 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
         s.isLast = last;
     }
     __syncthreads();
+#ifdef RTX_BVH_STAMPS
+    if (t == 0) {
+        g_stamp[6] = (uint32_t)__builtin_readcyclecounter();
+        g_stamp[7] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        for (int k = 0; k < 8; ++k) P.morton[start + 1016 + k] = g_stamp[k];
+    }
+#endif
     if (!s.isLast) return;
     if (B <= 64u) {  // small TLAS: wave 0 alone
         if (t < 64) tlas_wave(s, P, B);
+#ifdef RTX_BVH_STAMPS
+        if (t == 0) *(uint32_t*)P.tlasSceneAabb = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
         return;
     }
 #if defined(RTX_BVH_ABL) && RTX_BVH_ABL == 1
@@ -572,6 +601,9 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
     sort_and_build(s, (const float*)P.tlasAabbs, (int)B, P.tlasMorton, P.tlasReorder, (Node*)P.tlasNodes,
                    tlas_words(B));
     __syncthreads();
+#ifdef RTX_BVH_STAMPS
+    if (t == 0) *(uint32_t*)P.tlasSceneAabb = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
     if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

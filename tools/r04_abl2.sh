@@ -14,3 +14,7 @@ for l in lib abl_bvhnotlas abl_bvhnorefit; do
   RTX_LIB=$L/$l/librtx.so timeout -k 10 150 python tools/c2c4_probe.py 20 > $O/c4_$l.json 2> $O/c4_$l.err || { tail -20 $O/c4_$l.err; exit 1; }
   echo "$l $(cat $O/c4_$l.json)"
 done
+RTX_LIB=$L/abl_bvhstamps/librtx.so timeout -k 10 150 python tools/lbvh_stamps.py > $O/stamps.json 2> $O/stamps.err || { tail -20 $O/stamps.err; exit 1; }
+cat $O/stamps.json
+RTX_LIB=$L/abl_bvhstamps/librtx.so RTX_BVH_THREADS=512 timeout -k 10 150 python tools/lbvh_stamps.py > $O/stamps512.json 2> $O/stamps512.err || { tail -20 $O/stamps512.err; exit 1; }
+cat $O/stamps512.json

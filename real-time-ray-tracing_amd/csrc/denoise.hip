@@ -1018,7 +1018,12 @@ __global__ __launch_bounds__(256) void k_lens_flare(DenoisePostParams P, const u
 // separate passes store and reload them.
 constexpr int kScaleLds = 48 * 48;  // render texels staged per workgroup (scale factors up to ~2.5)
 
-__global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const uint2* render) {
+// 256 threads compute the 18x18 scaled apron in two passes (324 = 256 + 68); 384 threads in one pass
+// (the two extra waves leaving after it) measured slower: serial denoise + post 0.274 -> 0.282 ms,
+// pipelined frame 0.869 -> 0.880 (profiles/r04_ab/ablations/scale_post/)
+constexpr int kScaleThreads = 256;
+
+__global__ __launch_bounds__(kScaleThreads) void k_scale_post(DenoisePostParams P, const uint2* render) {
     DN_PRIO();
     __shared__ uint2 sIn[kScaleLds];
     __shared__ uint2 sS[18 * 18];
@@ -1032,7 +1037,7 @@ __global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const u
     const int TW = ix1 - ix0 + 1, TH = iy1 - iy0 + 1;
     const bool staged = TW * TH <= kScaleLds;
     if (staged) {
-        for (int i = threadIdx.x; i < TW * TH; i += 256) sIn[i] = render[(size_t)(iy0 + i / TW) * W + ix0 + i % TW];
+        for (int i = threadIdx.x; i < TW * TH; i += kScaleThreads) sIn[i] = render[(size_t)(iy0 + i / TW) * W + ix0 + i % TW];
         __syncthreads();
     }
     if (staged) {
@@ -1057,7 +1062,7 @@ __global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const u
             for (int i = 0; i < 4; ++i) sW[ax][k][i] = w[i];
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < 18 * 18; i += 256) {
+        for (int i = threadIdx.x; i < 18 * 18; i += kScaleThreads) {
             const int cx = i % 18, ry = i / 18;
             F3 o = f3(0.0f);
             float sw = 0.0f;
@@ -1074,12 +1079,13 @@ __global__ __launch_bounds__(256) void k_scale_post(DenoisePostParams P, const u
         }
     } else {
         const View2 gi{render, W, H};
-        for (int i = threadIdx.x; i < 18 * 18; i += 256) {
+        for (int i = threadIdx.x; i < 18 * 18; i += kScaleThreads) {
             const int sx = clampi(X0 + i % 18, 0, Ws - 1), sy = clampi(Y0 + i / 18, 0, Hs - 1);
             sS[i] = bicubic_scale_px(gi, W, H, sx, sy, Ws, Hs);
         }
     }
     __syncthreads();
+    if (kScaleThreads > 256 && threadIdx.x >= 256) return;
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= Ws || y >= Hs) return;
     const size_t p = (size_t)y * Ws + x;
@@ -1241,7 +1247,8 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         Q.ty0 = t0;
         Q.ty1 = t1;
         if (t1 > t0) {
-            hipLaunchKernelGGL(k_scale_post, dim3((Ws + 15) / 16, (unsigned)(t1 - t0)), b256, 0, s, Q, (const uint2*)cur);
+            hipLaunchKernelGGL(k_scale_post, dim3((Ws + 15) / 16, (unsigned)(t1 - t0)), dim3(kScaleThreads), 0, s, Q,
+                               (const uint2*)cur);
             LAUNCH_CHECK();
         }
         P->finalScaled = P->scaledB;

@@ -70,6 +70,26 @@ RT_DEV void store_box(float* p, const Box& b) {
     p[3] = b.mx.x; p[4] = b.mx.y; p[5] = b.mx.z;
 }
 
+// A box through agent-scope relaxed atomics: stores and loads that are coherent across the XCDs' L2s
+// by themselves (sc1), so the cross-workgroup TLAS leaf boxes need no release fence — on gfx950 an
+// agent-scope release writes back the producer XCD's whole L2, which doubled every batch's gather.
+RT_DEV void store_box_agent(float* p, const Box& b) {
+    const float v[6] = {b.mn.x, b.mn.y, b.mn.z, b.mx.x, b.mx.y, b.mx.z};
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        __hip_atomic_store((uint32_t*)p + k, __float_as_uint(v[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+RT_DEV Box load_box_agent(const float* p) {
+    float v[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        v[k] = __uint_as_float(__hip_atomic_load((const uint32_t*)p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    Box b;
+    b.mn = f3(v[0], v[1], v[2]);
+    b.mx = f3(v[3], v[4], v[5]);
+    return b;
+}
+
 // leaf box k: from LDS (kThr 1024) or from the AABB array this launch wrote (leafG)
 template <int kThr>
 RT_DEV Box leaf_box(const Lds<kThr>& s, const float* leafG, uint32_t k) {
@@ -459,6 +479,68 @@ RT_DEV void tlas_wave(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
 
 }  // namespace
 
+// A scene of more batches than this builds its TLAS in an extra workgroup beside the BLAS builds
+// (tlas_builder); up to this many, the last-arriving workgroup builds it with one wave (tlas_wave).
+constexpr uint32_t kTlasWaveMax = 64;
+
+// The TLAS of a large scene (UpdateTLAS, updateGeometry.cuh:264-364; then sort + Karras over B keys),
+// built by workgroup B of the launch.  Each batch's workgroup publishes its TLAS leaf box (its BLAS
+// root's merged box, computed from the leaf boxes right after the gather) with a release increment
+// of the launch counter; this workgroup, dispatched after every batch's, waits for all B of them,
+// so the TLAS is built while the batches sort, Karras-link and refit.  It resets the
+// counter for the next launch.
+template <int kThr>
+RT_DEV void tlas_builder(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
+    constexpr int kPer = kBatch / kThr;
+    const int t = threadIdx.x;
+    if (t == 0) {
+        while (__hip_atomic_load(P.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < B)
+            __builtin_amdgcn_s_sleep(2);
+    }
+    __syncthreads();  // every box is published; they are read below with coherent loads only
+#if defined(RTX_BVH_ABL) && RTX_BVH_ABL == 1
+    if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;  // timing ablation: no TLAS
+#endif
+    Box rq = box_empty();  // this thread's contribution to the quirk reduction
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t e = (uint32_t)(t + j * kThr);
+        Box rb = box_empty();
+        if (e < B) {
+            // read coherently, then stored back by this workgroup so that its plain re-reads (Morton
+            // keys, the 512-thread refit) see its own stores whatever this XCD's L2 held
+            rb = load_box_agent(P.tlasAabbs + 6 * (size_t)e);
+            store_box(P.tlasAabbs + 6 * (size_t)e, rb);
+            if ((e & 255u) < 128u) {
+                rq.mn = min3(rq.mn, rb.mn);
+                rq.mx = max3(rq.mx, rb.mx);
+            }
+        }
+        if (Lds<kThr>::kLeafLds) store_box(s.leaf[e], rb);
+    }
+    const Box quirk = block_reduce(s, rq);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t e = (uint32_t)(t + j * kThr);
+        uint32_t key = 0xFFFFFFFFu;
+        if (e < B) {  // the leaf centre from the box just loaded (not held across the reduction)
+            const Box lb = leaf_box(s, P.tlasAabbs, e);
+            key = morton_of((lb.mx + lb.mn) / 2.0f, quirk);
+        }
+        s.a.srt.key0[e] = key;
+        s.a.srt.idx0[e] = (uint16_t)e;
+    }
+    if (t == 0) store_box(P.tlasSceneAabb, quirk);
+    sort_and_build(s, (const float*)P.tlasAabbs, (int)B, P.tlasMorton, P.tlasReorder, (Node*)P.tlasNodes,
+                   tlas_words(B));
+    __syncthreads();
+#ifdef RTX_BVH_STAMPS
+    if (t == 0) *(uint32_t*)P.tlasSceneAabb = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
+    if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // kThr 1024: 8 waves/SIMD = 2 workgroups per CU; kThr 512: 4 workgroups per CU.  Either way <= 64
 // VGPRs.
 template <int kThr>
@@ -468,6 +550,10 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
     const int t = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const uint32_t B = P.batchCount;
+    if (b == B) {  // the extra workgroup of a large scene: the TLAS, beside the batches' BLAS builds
+        tlas_builder(s, P, B);
+        return;
+    }
     BVH_RSTAMP(0);
     BVH_STAMP(1);
     const uint32_t start = b * kBatch;
@@ -522,6 +608,39 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
         s.a.srt.idx0[e] = (uint16_t)e;
     }
     if (t == 0) store_box(P.batchSceneAabbs + 6 * (size_t)b, scene);
+    if (B > kTlasWaveMax) {
+        // The TLAS leaf box of this batch — its BLAS root's merged box, box_merge of the root's two
+        // child boxes — published now, before the BLAS is built, so that the TLAS builder runs beside
+        // the batches' sort / Karras / refit.  The refit's boxes are exact min / max merges of the
+        // leaf boxes, so the root's merged box is the exact min / max over the batch's cnt leaf boxes:
+        // the batch box above when every gathered element is a leaf (cnt == active), else a
+        // reduction over the first cnt elements; a one-leaf BLAS's root is (leaf box, zero box).
+        Box root = scene;
+        if (cnt == 1) {
+            Box zero;
+            zero.mn = f3(0.0f);
+            zero.mx = f3(0.0f);
+            root = box_merge(leaf_box(s, P.aabbs + 6 * (size_t)start, 0u), zero);
+        } else if (cnt != active) {
+            Box own2 = box_empty();
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+                const uint32_t e = (uint32_t)(t + j * kThr);
+                if (e < cnt) {
+                    const Box lb = leaf_box(s, P.aabbs + 6 * (size_t)start, e);
+                    own2.mn = min3(own2.mn, lb.mn);
+                    own2.mx = max3(own2.mx, lb.mx);
+                }
+            }
+            __syncthreads();  // the reduction partials reuse the histogram area the keys are not in
+            root = block_reduce(s, own2);
+        }
+        if (t == 0) {  // the box's coherent stores complete before the count that publishes it
+            store_box_agent(P.tlasAabbs + 6 * (size_t)b, root);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(P.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 
     Node* const nodes = (Node*)P.nodes;
     const WordCtx blasWords{kBlasBit, start, kLeafBit | kBlasBit, B * (uint32_t)kBatch + B + start, 1u};
@@ -530,7 +649,17 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
     __syncthreads();
     BVH_STAMP(5);
 
-    // ---- arrival: the last workgroup builds the TLAS
+    if (B > kTlasWaveMax) {
+#ifdef RTX_BVH_STAMPS
+        if (t == 0) {
+            g_stamp[6] = (uint32_t)__builtin_readcyclecounter();
+            g_stamp[7] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            for (int k = 0; k < 8; ++k) P.morton[start + 1016 + k] = g_stamp[k];
+        }
+#endif
+        return;
+    }
+    // ---- arrival (scenes of at most kTlasWaveMax batches): the last workgroup builds the TLAS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
@@ -553,58 +682,11 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
     }
 #endif
     if (!s.isLast) return;
-    if (B <= 64u) {  // small TLAS: wave 0 alone
-        if (t < 64) tlas_wave(s, P, B);
-#ifdef RTX_BVH_STAMPS
-        if (t == 0) *(uint32_t*)P.tlasSceneAabb = (uint32_t)__builtin_amdgcn_s_memrealtime();
-#endif
-        return;
-    }
-#if defined(RTX_BVH_ABL) && RTX_BVH_ABL == 1
-    if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;  // timing ablation: no TLAS
-#endif
-
-    // ---- TLAS (UpdateTLAS, updateGeometry.cuh:264-364; then sort + Karras over B keys)
-    Box rq = box_empty();  // this thread's contribution to the quirk reduction
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const uint32_t e = (uint32_t)(t + j * kThr);
-        Box rb = box_empty();
-        if (e < B) {
-            const Node nd = nodes[(size_t)e * kBatch];
-            Box l, r;
-            l.mn = f3(nd.q0.x, nd.q0.y, nd.q0.z); l.mx = f3(nd.q0.w, nd.q1.x, nd.q1.y);
-            r.mn = f3(nd.q1.z, nd.q1.w, nd.q2.x); r.mx = f3(nd.q2.y, nd.q2.z, nd.q2.w);
-            rb = box_merge(l, r);
-            store_box(P.tlasAabbs + 6 * (size_t)e, rb);
-            if ((e & 255u) < 128u) {
-                rq.mn = min3(rq.mn, rb.mn);
-                rq.mx = max3(rq.mx, rb.mx);
-            }
-        }
-        if (Lds<kThr>::kLeafLds) store_box(s.leaf[e], rb);
-    }
-    const Box quirk = block_reduce(s, rq);
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const uint32_t e = (uint32_t)(t + j * kThr);
-        uint32_t key = 0xFFFFFFFFu;
-        if (e < B) {  // the leaf centre from the box just stored (not held across the reduction)
-            const Box lb = leaf_box(s, P.tlasAabbs, e);
-            key = morton_of((lb.mx + lb.mn) / 2.0f, quirk);
-        }
-        s.a.srt.key0[e] = key;
-        s.a.srt.idx0[e] = (uint16_t)e;
-    }
-    if (t == 0) store_box(P.tlasSceneAabb, quirk);
-    sort_and_build(s, (const float*)P.tlasAabbs, (int)B, P.tlasMorton, P.tlasReorder, (Node*)P.tlasNodes,
-                   tlas_words(B));
-    __syncthreads();
+    // small TLAS: wave 0 alone
+    if (t < 64) tlas_wave(s, P, B);
 #ifdef RTX_BVH_STAMPS
     if (t == 0) *(uint32_t*)P.tlasSceneAabb = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-    if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Batches that fit two 1024-thread workgroups per CU take that shape; more take the 512-thread one,
@@ -620,7 +702,9 @@ extern "C" hipError_t rtk_launch_build_bvh(const BvhBuildParams* p, hipStream_t 
     if (e != hipSuccess) return e;
     const int want = p->threads ? (int)p->threads : forced;
     const bool narrow = want == 512 || (want != 1024 && (int)p->batchCount > 2 * cus);
-    if (narrow) hipLaunchKernelGGL(k_build_bvh<512>, dim3(p->batchCount), dim3(512), 0, stream, *p);
-    else hipLaunchKernelGGL(k_build_bvh<1024>, dim3(p->batchCount), dim3(1024), 0, stream, *p);
+    // one workgroup per batch, and for a large scene the TLAS builder after them
+    const unsigned grid = p->batchCount + (p->batchCount > kTlasWaveMax ? 1u : 0u);
+    if (narrow) hipLaunchKernelGGL(k_build_bvh<512>, dim3(grid), dim3(512), 0, stream, *p);
+    else hipLaunchKernelGGL(k_build_bvh<1024>, dim3(grid), dim3(1024), 0, stream, *p);
     return hipGetLastError();
 }

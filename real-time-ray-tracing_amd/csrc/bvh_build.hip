@@ -4,9 +4,10 @@
 //   UpdateSceneGeometry -> RadixSort -> BuildLBVH   (per 1024-triangle BLAS batch)
 //   UpdateTLAS -> RadixSort -> BuildLBVH             (one TLAS over the batch roots)
 // with ONE kernel: a workgroup builds a whole batch inside LDS (gather -> batch box -> Morton ->
-// 5x6-bit LSD radix sort -> Karras topology -> bottom-up boxes), and the last workgroup to finish
-// (agent-scope release/acquire on an arrival counter, cdna_hip_programming.md Guideline 16) builds
-// the TLAS with the same LDS machinery.  Results are bit-identical to the reference semantics
+// 5x6-bit LSD radix sort -> Karras topology -> bottom-up boxes), and one more workgroup builds the
+// TLAS with the same LDS machinery beside them, from the batches' root boxes, which each batch
+// publishes right after its gather (agent-coherent stores, then a count on a launch counter the TLAS
+// workgroup polls; tlas_builder).  Results are bit-identical to the reference semantics
 // (oracle/bvh.cpp):
 //   * Morton codes: same fp32 ops, no contraction, saturating float->uint
 //   * sort: stable LSD radix on the low 30 bits (all codes < 2^30; padding keys
@@ -56,7 +57,6 @@ struct Lds {
     uint16_t idx1[kBatch];
     float merged[kBatch][6];  // merged box of each internal node; rows 0..15: the box reductions
     float leaf[kLeafLds ? kBatch : 1][6];  // leaf boxes by original local index (kThr 1024)
-    uint32_t isLast;
 };
 
 RT_DEV Box load_box(const float* p) {
@@ -406,13 +406,44 @@ __shared__ uint32_t g_stamp[8];
 #define BVH_RSTAMP(k) do { } while (0)
 #endif
 
-// Sort the keys in key0/idx0 and build the tree of n leaves into `nodes`.
+// A batch's TLAS leaf box, published to the TLAS workgroup (tlas_builder): agent-coherent stores,
+// complete before the count that announces them.  Thread 0 of the batch's workgroup.
+RT_DEV void publish_root(const BvhBuildParams& P, uint32_t b, const Box& root) {
+    store_box_agent(P.tlasAabbs + 6 * (size_t)b, root);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(P.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sort the keys in key0/idx0 and build the tree of n leaves into `nodes`.  pub: publish batch b's
+// root box from the sorted order (the first n sorted elements are the leaves).
 template <int kThr>
 RT_DEV void sort_and_build(Lds<kThr>& s, const float* leafG, int n, uint32_t* mortonOut, uint32_t* reorderOut,
-                           Node* nodes, const WordCtx& w) {
+                           Node* nodes, const WordCtx& w, const BvhBuildParams* pub = nullptr, uint32_t b = 0) {
     __syncthreads();
     radix_sort(s);
     BVH_STAMP(3);
+    if (pub) {
+        __syncthreads();  // idx1 complete; the partials below reuse the histogram area
+        Box own = box_empty();
+#pragma unroll
+        for (int j = 0; j < kBatch / kThr; ++j) {
+            const int e = threadIdx.x + j * kThr;
+            if (e < n) {
+                const Box lb = leaf_box(s, leafG, s.idx1[e]);
+                own.mn = min3(own.mn, lb.mn);
+                own.mx = max3(own.mx, lb.mx);
+            }
+        }
+        Box root = block_reduce(s, own);
+        if (n == 1) {  // a one-leaf BLAS's root is (element 0's box, zero box), as refit() stores it
+            Box zero;
+            zero.mn = f3(0.0f);
+            zero.mx = f3(0.0f);
+            root = box_merge(leaf_box(s, leafG, 0u), zero);
+        }
+        if (threadIdx.x == 0) publish_root(*pub, b, root);
+        __syncthreads();  // the partials are read before Karras reuses the area
+    }
 #pragma unroll
     for (int j = 0; j < kBatch / kThr; ++j) {
         const int e = threadIdx.x + j * kThr;
@@ -430,7 +461,7 @@ RT_DEV void sort_and_build(Lds<kThr>& s, const float* leafG, int n, uint32_t* mo
 // the TLAS's child words: internal nodes after the B*1024 BLAS slots, leaves at their BLAS roots
 RT_DEV WordCtx tlas_words(uint32_t B) { return WordCtx{0u, B * (uint32_t)kBatch, kLeafBit, 0u, (uint32_t)kBatch}; }
 
-// The TLAS of a scene of at most 64 batches, built by wave 0 of the last workgroup alone: the
+// The TLAS of a scene of at most 64 batches, built by wave 0 of the TLAS workgroup alone: the
 // same results as the workgroup path (UpdateTLAS + RadixSort + BuildLBVH over B keys) without
 // its ~20 workgroup barriers.  The stable sort is a rank count (keys below, plus equal keys of
 // lower index: a stable sort's position); the 1024 - B padding keys (0xFFFFFFFF) keep their
@@ -439,15 +470,10 @@ RT_DEV WordCtx tlas_words(uint32_t B) { return WordCtx{0u, B * (uint32_t)kBatch,
 template <int kThr>
 RT_DEV void tlas_wave(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
     const int lane = threadIdx.x;  // 0..63
-    const Node* nodes = (const Node*)P.nodes;
     Box rb = box_empty();
     F3 rc = f3(0.0f);
-    if ((uint32_t)lane < B) {
-        const Node nd = nodes[(size_t)lane * kBatch];
-        Box l, r;
-        l.mn = f3(nd.q0.x, nd.q0.y, nd.q0.z); l.mx = f3(nd.q0.w, nd.q1.x, nd.q1.y);
-        r.mn = f3(nd.q1.z, nd.q1.w, nd.q2.x); r.mx = f3(nd.q2.y, nd.q2.z, nd.q2.w);
-        rb = box_merge(l, r);
+    if ((uint32_t)lane < B) {  // the published box, stored back for the refit's plain reads
+        rb = load_box_agent(P.tlasAabbs + 6 * (size_t)lane);
         rc = (rb.mx + rb.mn) / 2.0f;
         store_box(P.tlasAabbs + 6 * (size_t)lane, rb);
     }
@@ -474,21 +500,19 @@ RT_DEV void tlas_wave(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
     karras(s, (int)B);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     refit(s, P.tlasAabbs, (int)B, (Node*)P.tlasNodes, tlas_words(B));
-    if (lane == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
 
-// A scene of more batches than this builds its TLAS in an extra workgroup beside the BLAS builds
-// (tlas_builder); up to this many, the last-arriving workgroup builds it with one wave (tlas_wave).
+// Up to this many batches the TLAS is built by one wave (tlas_wave), beyond by the whole workgroup.
 constexpr uint32_t kTlasWaveMax = 64;
 
-// The TLAS of a large scene (UpdateTLAS, updateGeometry.cuh:264-364; then sort + Karras over B keys),
-// built by workgroup B of the launch.  Each batch's workgroup publishes its TLAS leaf box (its BLAS
-// root's merged box, computed from the leaf boxes right after the gather) with a release increment
-// of the launch counter; this workgroup, dispatched after every batch's, waits for all B of them,
-// so the TLAS is built while the batches sort, Karras-link and refit.  It resets the
-// counter for the next launch.
+// The TLAS (UpdateTLAS, updateGeometry.cuh:264-364; then sort + Karras over B keys), built by
+// workgroup B of the launch.  Each batch's workgroup publishes its TLAS leaf box (its BLAS root's
+// merged box, computed from the leaf boxes right after the gather) and then counts itself in the
+// launch counter; this workgroup, dispatched after every batch's, waits for all B of them, so the
+// TLAS is built while the batches sort, Karras-link and refit.  It resets the counter for the next
+// launch.
 template <int kThr>
 RT_DEV void tlas_builder(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
     constexpr int kPer = kBatch / kThr;
@@ -502,6 +526,14 @@ RT_DEV void tlas_builder(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
     if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;  // timing ablation: no TLAS
 #endif
+    if (B <= kTlasWaveMax) {  // wave 0 alone
+        if (t < 64) tlas_wave(s, P, B);
+#ifdef RTX_BVH_STAMPS
+        if (t == 0) *(uint32_t*)P.tlasSceneAabb = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
+        if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     Box rq = box_empty();  // this thread's contribution to the quirk reduction
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
@@ -550,7 +582,7 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
     const int t = threadIdx.x;
     const uint32_t b = blockIdx.x;
     const uint32_t B = P.batchCount;
-    if (b == B) {  // the extra workgroup of a large scene: the TLAS, beside the batches' BLAS builds
+    if (b == B) {  // the extra workgroup: the TLAS, beside the batches' BLAS builds
         tlas_builder(s, P, B);
         return;
     }
@@ -608,84 +640,29 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
         s.a.srt.idx0[e] = (uint16_t)e;
     }
     if (t == 0) store_box(P.batchSceneAabbs + 6 * (size_t)b, scene);
-    if (B > kTlasWaveMax) {
-        // The TLAS leaf box of this batch — its BLAS root's merged box, box_merge of the root's two
-        // child boxes — published now, before the BLAS is built, so that the TLAS builder runs beside
-        // the batches' sort / Karras / refit.  The refit's boxes are exact min / max merges of the
-        // leaf boxes, so the root's merged box is the exact min / max over the batch's cnt leaf boxes:
-        // the batch box above when every gathered element is a leaf (cnt == active), else a
-        // reduction over the first cnt elements; a one-leaf BLAS's root is (leaf box, zero box).
-        Box root = scene;
-        if (cnt == 1) {
-            Box zero;
-            zero.mn = f3(0.0f);
-            zero.mx = f3(0.0f);
-            root = box_merge(leaf_box(s, P.aabbs + 6 * (size_t)start, 0u), zero);
-        } else if (cnt != active) {
-            Box own2 = box_empty();
-#pragma unroll
-            for (int j = 0; j < kPer; ++j) {
-                const uint32_t e = (uint32_t)(t + j * kThr);
-                if (e < cnt) {
-                    const Box lb = leaf_box(s, P.aabbs + 6 * (size_t)start, e);
-                    own2.mn = min3(own2.mn, lb.mn);
-                    own2.mx = max3(own2.mx, lb.mx);
-                }
-            }
-            __syncthreads();  // the reduction partials reuse the histogram area the keys are not in
-            root = block_reduce(s, own2);
-        }
-        if (t == 0) {  // the box's coherent stores complete before the count that publishes it
-            store_box_agent(P.tlasAabbs + 6 * (size_t)b, root);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(P.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    // The TLAS leaf box of this batch (its BLAS root's merged box, box_merge of the root's two child
+    // boxes), published as soon as it is known, so that the TLAS workgroup runs beside the batches'
+    // sort / Karras / refit.  The refit's boxes are exact min / max merges of the leaf boxes, and
+    // the BLAS's cnt leaves are the first cnt elements in sorted order: when every gathered element
+    // is a leaf (cnt == active) that is the batch box above; otherwise (a last batch whose padding
+    // triangles sort among the real ones) it is known after the sort (sort_and_build).
+    const bool pubNow = cnt == active;
+    if (pubNow && t == 0) publish_root(P, b, scene);
 
     Node* const nodes = (Node*)P.nodes;
     const WordCtx blasWords{kBlasBit, start, kLeafBit | kBlasBit, B * (uint32_t)kBatch + B + start, 1u};
     BVH_STAMP(2);
-    sort_and_build(s, leafG, (int)cnt, P.morton + start, P.reorder + start, nodes + start, blasWords);
+    sort_and_build(s, leafG, (int)cnt, P.morton + start, P.reorder + start, nodes + start, blasWords,
+                   pubNow ? nullptr : &P, b);
     __syncthreads();
     BVH_STAMP(5);
 
-    if (B > kTlasWaveMax) {
-#ifdef RTX_BVH_STAMPS
-        if (t == 0) {
-            g_stamp[6] = (uint32_t)__builtin_readcyclecounter();
-            g_stamp[7] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-            for (int k = 0; k < 8; ++k) P.morton[start + 1016 + k] = g_stamp[k];
-        }
-#endif
-        return;
-    }
-    // ---- arrival (scenes of at most kTlasWaveMax batches): the last workgroup builds the TLAS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t old = __hip_atomic_fetch_add(P.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t last = (old == B - 1) ? 1u : 0u;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        s.isLast = last;
-    }
-    __syncthreads();
 #ifdef RTX_BVH_STAMPS
     if (t == 0) {
         g_stamp[6] = (uint32_t)__builtin_readcyclecounter();
         g_stamp[7] = (uint32_t)__builtin_amdgcn_s_memrealtime();
         for (int k = 0; k < 8; ++k) P.morton[start + 1016 + k] = g_stamp[k];
     }
-#endif
-    if (!s.isLast) return;
-    // small TLAS: wave 0 alone
-    if (t < 64) tlas_wave(s, P, B);
-#ifdef RTX_BVH_STAMPS
-    if (t == 0) *(uint32_t*)P.tlasSceneAabb = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
 }
 
@@ -702,8 +679,7 @@ extern "C" hipError_t rtk_launch_build_bvh(const BvhBuildParams* p, hipStream_t 
     if (e != hipSuccess) return e;
     const int want = p->threads ? (int)p->threads : forced;
     const bool narrow = want == 512 || (want != 1024 && (int)p->batchCount > 2 * cus);
-    // one workgroup per batch, and for a large scene the TLAS builder after them
-    const unsigned grid = p->batchCount + (p->batchCount > kTlasWaveMax ? 1u : 0u);
+    const unsigned grid = p->batchCount + 1u;  // one workgroup per batch, then the TLAS's
     if (narrow) hipLaunchKernelGGL(k_build_bvh<512>, dim3(grid), dim3(512), 0, stream, *p);
     else hipLaunchKernelGGL(k_build_bvh<1024>, dim3(grid), dim3(1024), 0, stream, *p);
     return hipGetLastError();

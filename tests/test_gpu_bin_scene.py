@@ -128,3 +128,29 @@ def test_one_triangle_last_batch(rtx, oracle, tmp_path, threads):
     gb = oracle.pathtrace(b, w, h, frame_num=1, spp=1, cam=oc, hist_cam=oc, sky_out=oracle.sky(), tex=oracle.textures())
     assert np.array_equal(rgba.reshape(-1, 4), oracle.Denoiser(w, h).draw(gb, 1, delta_time=16.667)["rgba"])
     rt.cleanup()
+
+
+@pytest.mark.parametrize("ntri,threads", [(2 * 1024 + 6, 0), (2 * 1024 + 6, 512), (65 * 1024 + 3, 0), (65 * 1024 + 3, 1024)])
+def test_partial_last_batch_tlas(rtx, oracle, tmp_path, ntri, threads):
+    """A last batch of 6 (3) real and 2 (1) padding triangles, in a 3-batch scene (one-wave TLAS) and
+    a 66-batch one (workgroup TLAS): the batch's leaves are its first real-count elements in SORTED
+    order, padding ones among them, so its TLAS leaf box (published to the TLAS workgroup after the
+    batch's sort) and every node, Morton code and TLAS record stay bit-exact vs the oracle."""
+    tris = terrain_patch(190, 180)[:ntri]
+    path = write_bin(str(tmp_path / ("n%d.bin" % ntri)), tris)
+    rt = make(rtx, tmp_path, path, threads=threads)
+    b, _, _, n = bin_bvh(oracle, path)
+    B = b["batch_count"]
+    assert rt.info().triCount == n == ntri and rt.info().batchCount == B == (ntri + 1023) // 1024
+    for _ in range(2):  # a rebuild reuses the launch counter
+        rt.build_bvh()
+    rt.sync()
+    nodes = rt.download("NODES").view(rtx.NODE_DTYPE)
+    for k in range(B):
+        cnt = 1024 if k < B - 1 else n - (B - 1) * 1024
+        assert nodes[k * 1024:k * 1024 + cnt - 1].tobytes() == b["nodes"][k * 1024:k * 1024 + cnt - 1].tobytes(), k
+    assert np.array_equal(rt.download("MORTON", np.uint32)[:B * 1024], b["morton"])
+    assert np.array_equal(rt.download("TLAS_AABBS", np.float32).reshape(-1, 6), b["tlas_aabbs"])
+    assert np.array_equal(rt.download("TLAS_SCENE_AABB", np.float32), b["tlas_scene_aabb"])
+    assert rt.download("TLAS_NODES").view(rtx.NODE_DTYPE).tobytes() == b["tlas_nodes"].tobytes()
+    rt.cleanup()

@@ -442,7 +442,7 @@ inline bool one_round(uint32_t spp) { return spp >= 1 && ((int)spp + cam_sample_
 #define RTX_CAM_ATTR
 #endif
 template <bool kOneRound>
-__global__ __launch_bounds__(256, 6) RTX_CAM_ATTR void k_pt_camera(PathTraceParams P) {
+__global__ __launch_bounds__(256, kOneRound ? 6 : 4) RTX_CAM_ATTR void k_pt_camera(PathTraceParams P) {
     // stack entries in LDS (the rest in registers): 26 KB per workgroup, 6 workgroups per CU
     // (measured: 16 entries 4 per CU 0.948 ms/frame, 12 entries 5 per CU 0.918, 10 entries 6 per CU
     // 0.900; the default scene's rays hold at most 11 entries)

@@ -60,7 +60,7 @@ for p in (ROOT, PKG):
 HBM_PEAK_GBS = 8000.0   # /opt/skills/guides/MI355X_MICROARCH.md (spec peak)
 L2_PEAK_GBS = 34500.0   # MI355X_MICROARCH.md, L2 (per XCD) section: aggregate L2 bandwidth
 DELTA_MS = 16.667       # fixed AutoExposure step (SURVEY §8d determinism settings)
-PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_kernels.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r04_pmc_kernels.json")  # tools/prof_r03.sh, round-4 run
 PMC_C2C4 = os.path.join(ROOT, "profiles", "r04_pmc_c2c4.json")  # tools/prof_r04_c2c4.sh (configs 2 and 4)
 TERRAIN_CAM = dict(pos=(8.0, 15.0, -6.0), yaw=0.0, pitch=-0.7)  # ~50 % primary hits (tests' camera)
 
@@ -656,7 +656,7 @@ def main():
                    "timed frames (rt_frame_marks); chosen as the longest critical-stream kernel of warm-up frames "
                    "2..%d; the other kernels: the same events over 20 pipelined frames after the timed ones "
                    "(rt_time_frame_kernels); rocprofv3 --kernel-trace --stats of this command: "
-                   "profiles/r03_kernel_stats.csv (this process: warm-up, timed, 1 detail and the 20 split frames)"
+                   "profiles/r04_kernel_stats.csv (this process: warm-up, timed, 1 detail and the 20 split frames)"
                    % (dom, marked, args.warmup)),
         "kernel_ms_split_frames": round(split_dom, 5) if split_dom is not None else None,
     }

@@ -27,7 +27,8 @@ def label(row):
         return "k_trace_primary"
     if "k_build_bvh" in name:
         blocks = grid // wg if wg else 0
-        return "k_build_bvh@958720" if blocks == 937 else "k_build_bvh@%dwg" % blocks
+        # 937 batch workgroups (+ the TLAS workgroup since round 4)
+        return "k_build_bvh@958720" if blocks in (937, 938) else "k_build_bvh@%dwg" % blocks
     return None
 
 

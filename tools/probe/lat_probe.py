@@ -39,7 +39,7 @@ def main():
     B = len(rt.download("TLAS_NODES", np.uint8)) // 64
     root, triBase = B * 1024, B * 1024 + B
     arena = torch.from_numpy(rt.download("BVH_ARENA", np.uint8).copy()).to(dev)
-    lib = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblatprobe.so"))
+    lib = C.CDLL(os.environ.get("LATPROBE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblatprobe.so"))
     lib.lp_run.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32] + [C.c_void_p] * 5
     maxIt = 1100
     order = np.argsort(iters)[::-1]

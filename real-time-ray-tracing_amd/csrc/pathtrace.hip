@@ -502,9 +502,7 @@ __global__ __launch_bounds__(256, kOneRound ? 6 : 4) RTX_CAM_ATTR void k_pt_came
                     if (trav_step<kCamLds, false>(sc, tr, st, trec, stk + tid, 256, &deep)) break;
             }
             ++rays;
-            if (P.statsOut) {
-                atomicAdd(&P.statsOut[p].y, st.visits);
-                atomicAdd(&P.statsOut[p].z, st.tests);
+            if (P.statsOut) {  // the pixel's counters are added after the round loop
                 camV += st.visits;
                 camT += st.tests;
             }
@@ -562,7 +560,11 @@ __global__ __launch_bounds__(256, kOneRound ? 6 : 4) RTX_CAM_ATTR void k_pt_came
     }
     if (active && rays) {
         if (P.raysOut) atomicAdd(&P.raysOut[p], rays);
-        if (P.statsOut) atomicAdd(&P.statsOut[p].x, rays);
+        if (P.statsOut) {
+            atomicAdd(&P.statsOut[p].x, rays);
+            if (camV) atomicAdd(&P.statsOut[p].y, camV);
+            if (camT) atomicAdd(&P.statsOut[p].z, camT);
+        }
     }
     if (P.statsOut) {
         wave_add(camV, &P.ws.counters[kCntVisCam]);

@@ -488,7 +488,6 @@ void rt_destroy(rt_context* ctx) {
     if (ctx->ownPostStream) (void)hipStreamDestroy(ctx->ownPostStream);
     for (void* p : ctx->allocations) (void)hipFree(p);
     if (ctx->fr.q3Host) (void)hipHostFree(ctx->fr.q3Host);
-    if (ctx->fr.q3Ev) (void)hipEventDestroy(ctx->fr.q3Ev);
     for (hipEvent_t e : ctx->markPool)
         if (e) (void)hipEventDestroy(e);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);

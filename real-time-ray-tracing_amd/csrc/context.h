@@ -111,7 +111,6 @@ struct FrameResources {
     // queue 3's length after the last serial path trace, copied to pinned host memory behind it
     // (the fused chain's on/off choice for serial frames)
     uint32_t* q3Host = nullptr;
-    hipEvent_t q3Ev = nullptr;
     bool q3Pending = false;
     uint32_t lastQ3 = 0;
     bool lastChain = false;  // the last path trace ran the fused k_pt_chain (rt_info.lastChain)

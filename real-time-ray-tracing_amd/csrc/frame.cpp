@@ -301,6 +301,11 @@ int sync_streams(rt_context* ctx) {
     if (ctx->sideStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->sideStream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->postStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->postStream));
+    FrameResources& fr = ctx->fr;
+    if (fr.q3Pending) {  // the last serial frame's queue-3 length (rt_path_trace's chain choice)
+        fr.lastQ3 = *fr.q3Host;
+        fr.q3Pending = false;
+    }
     return RT_OK;
 }
 
@@ -654,12 +659,8 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     // (0.436 vs 0.450 ms per rank frame)
     // ... and only while queue 3 is short: a long queue (the terrain view's 3.85 M rays) runs the
     // four kernels faster serially too (4.64 against 5.11 ms per synchronous terrain draw).  The
-    // length is the previous serial frame's, read back without waiting (q3Host, copied behind
-    // that frame's kernels; stale by a frame or more only if that frame has not finished).
-    if (fr.q3Host && fr.q3Pending && hipEventQuery(fr.q3Ev) == hipSuccess) {
-        fr.lastQ3 = *fr.q3Host;
-        fr.q3Pending = false;
-    }
+    // length is that of the last serial frame a host sync completed (q3Host, stored by the frame's
+    // resolve kernel, read in sync_streams: a fixed schedule, no event on the stream).
     p.ws.chain = fr.ws.chain == 2 || (fr.ws.chain == 1 && !ctx->postStream && fr.lastQ3 < kChainMaxQ3);
     fr.lastChain = p.ws.chain && !p.ws.glossy && !p.ws.microfacet;  // as rtk_launch_pt_rest decides
     if (with_detail) {  // per-pixel counters: everything in order on the context stream
@@ -702,18 +703,12 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     }
     PtLaunchHook hook{overlap_hook, ctx};
     if (!side && !fr.q3Pending) {  // serial frames: queue 3's length for the next frame's chain choice
-        if (!fr.q3Host) {
-            HIP_TRY(ctx, hipHostMalloc((void**)&fr.q3Host, sizeof(uint32_t), hipHostMallocDefault));
-            HIP_TRY(ctx, hipEventCreateWithFlags(&fr.q3Ev, hipEventDisableTiming));
-        }
+        if (!fr.q3Host) HIP_TRY(ctx, hipHostMalloc((void**)&fr.q3Host, sizeof(uint32_t), hipHostMallocDefault));
+        p.ws.q3HostOut = fr.q3Host;  // stored by k_pt_resolve (no copy on the stream)
+        fr.q3Pending = true;
     }
     if (shadeSide) HIP_TRY(ctx, rtk_launch_pt_rest_after_shade(&p, ctx->stream, ctx->ptMarks, &hook));
     else HIP_TRY(ctx, rtk_launch_pt_rest(&p, ctx->stream, ctx->ptMarks, ctx->postStream ? &hook : nullptr));
-    if (!side && fr.q3Host && !fr.q3Pending) {
-        HIP_TRY(ctx, hipMemcpyAsync(fr.q3Host, p.ws.counters + kCntQ3, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(ctx, hipEventRecord(fr.q3Ev, ctx->stream));
-        fr.q3Pending = true;
-    }
     if (ctx->postPending && (rc = issue_pending_post(ctx)) != RT_OK) return rc;
     if (ctx->postStream) {
         HIP_TRY(ctx, hipEventRecord(ctx->restDone[g], ctx->stream));

@@ -1073,6 +1073,9 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
 // colour of the pixels with a deferred sample: the fp32 sample average in sample order
 __global__ __launch_bounds__(256) void k_pt_resolve(PathTraceParams P) {
     const uint32_t n = P.ws.counters[kCntPending];
+    // serial frames: queue 3's length into pinned host memory for the next frame's chain choice
+    // (frame.cpp), a vector store over the bus instead of a copy on the stream
+    if (P.ws.q3HostOut && blockIdx.x == 0 && threadIdx.x == 0) *(volatile uint32_t*)P.ws.q3HostOut = P.ws.counters[kCntQ3];
 #pragma unroll 1
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
         const uint32_t e = P.ws.pending[i];

@@ -38,7 +38,13 @@ def main():
         np.save(os.path.join(out, "q%d_iters.npy" % step), it)
         np.save(os.path.join(out, "q%d_rays.npy" % step), np.concatenate([o, d], 1))
         rng = np.random.default_rng(1)
-        orders = {"queue": np.arange(n), "shuffled": rng.permutation(n), "by_iters": np.argsort(-it.astype(np.int64), kind="stable")}
+        sh = rng.permutation(n)
+        keyed = lambda k: sh[np.argsort(k[sh], kind="stable")]  # noqa: E731
+        dy = d[:, 1]
+        orders = {"queue": np.arange(n), "shuffled": sh, "by_iters": np.argsort(-it.astype(np.int64), kind="stable"),
+                  # predictors available before tracing: the ray's y direction (grazing rays skim the terrain)
+                  "dy_desc": keyed(-dy), "dy_clip": keyed(-np.minimum(dy, 0.2)),
+                  "dy_bins8": keyed(-np.minimum(np.floor((dy + 1.0) * 4.0), 4.0))}
         r = dict(rays=n, iters_sum=int(it.sum()), iters_max=int(it.max()),
                  iters_q=[int(x) for x in np.quantile(it, [0.5, 0.9, 0.99, 0.999])])
         for name, ordr in orders.items():

@@ -518,7 +518,10 @@ RT_DEV void tlas_builder(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
     constexpr int kPer = kBatch / kThr;
     const int t = threadIdx.x;
     if (t == 0) {
-        while (__hip_atomic_load(P.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < B)
+        // bounded (~2^24 polls, about a second): a batch that never publishes would leave a wrong
+        // TLAS (which every parity test sees) rather than a wave spinning until the GPU is reset
+        for (uint32_t k = 0; k < (1u << 24) &&
+                             __hip_atomic_load(P.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < B; ++k)
             __builtin_amdgcn_s_sleep(2);
     }
     __syncthreads();  // every box is published; they are read below with coherent loads only

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (record of a measured and reverted A/B: the switch it builds against is no longer in the sources; DESIGN.md has the result)
 # LBVH: triangle records written as whole 64-B lines (abl_fullrec) vs 48 of 64 B (product)
 set -o pipefail
 mkdir -p gpurun_out/fullrec

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (record of a measured and reverted A/B: the switch it builds against is no longer in the sources; DESIGN.md has the result)
 # push-time record touch (RTX_TRAV_PF2): lone-ray anatomy, queue-tracer latency, pipelined frame
 set -o pipefail
 mkdir -p gpurun_out/pf2

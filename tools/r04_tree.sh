@@ -1,4 +1,5 @@
 #!/bin/bash
+# (record of a measured and reverted A/B: the switch it builds against is no longer in the sources; DESIGN.md has the result)
 # sky light-CDF heap: 14 levels in LDS (product) vs 12 (abl_tree4k, the round-3 layout)
 set -o pipefail
 mkdir -p gpurun_out/tree

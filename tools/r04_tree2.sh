@@ -1,4 +1,5 @@
 #!/bin/bash
+# (record of a measured and reverted A/B: the switch it builds against is no longer in the sources; DESIGN.md has the result)
 # sky light-CDF heap levels staged in LDS: 12 (product, 4096 nodes) vs 11 (abl_sky2k) vs 10 (abl_sky1k)
 set -o pipefail
 mkdir -p gpurun_out/tree2

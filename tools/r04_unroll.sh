@@ -1,4 +1,5 @@
 #!/bin/bash
+# (record of a measured and reverted A/B: the switch it builds against is no longer in the sources; DESIGN.md has the result)
 # denoise 5x5 / 7x7 batch loops not unrolled (product) vs fully unrolled (abl_unroll8): parity, serial
 # stages, pipelined frame
 set -o pipefail

@@ -744,8 +744,8 @@ __global__ __launch_bounds__(64) void k_auto_exposure(float* e, const uint32_t* 
 // Workgroup (X, Y) of the W64 x H64 grid takes the 64x64 render block under 1/64 texel (X, Y): its
 // 16x16 quarter texels (one per thread, from the colour), 4x4 sixteenth texels and the 1/64 texel
 // from LDS, each level's clamped reads landing inside the block (the level's last texel is in the
-// block that covers the edge).  The last workgroup to finish — a device-scope counter after a
-// release fence, an acquire fence before reading — counts the histogram over the 1/64 image and
+// block that covers the edge).  The last workgroup to finish — a device-scope counter, the 1/64
+// texels published with agent-coherent stores — counts the histogram over the 1/64 image and
 // runs the exposure update, and re-arms the counter.
 struct LdsLevel {  // clamped reads of an image level, of the block staged in LDS
     const uint2* s;
@@ -784,19 +784,29 @@ __global__ __launch_bounds__(256) void k_downscale_chain(DenoisePostParams P, co
     }
     __syncthreads();
     if (t == 0) {
-        P.c64[Y * W64 + X] = down4(LdsLevel{s16, W16, H16, X * 4, Y * 4, 4}, X, Y);
-        __threadfence();
-        sLast = atomicAdd(counter, 1u) == gridDim.x * gridDim.y - 1;
+        // The 1/64 texel goes out as an agent-scope relaxed atomic store (coherent across the XCDs'
+        // L2s by itself), complete before this workgroup's count; the last workgroup reads the
+        // texels with agent-scope loads.  No release / acquire fence: on gfx950 those write back and
+        // invalidate the XCD's whole L2 (buffer_wbl2 / buffer_inv), once per workgroup.
+        const uint2 v = down4(LdsLevel{s16, W16, H16, X * 4, Y * 4, 4}, X, Y);
+        __hip_atomic_store((unsigned long long*)&P.c64[Y * W64 + X], ((unsigned long long)v.y << 32) | v.x,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sLast = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                gridDim.x * gridDim.y - 1;
     }
     __syncthreads();
     if (!sLast) return;
-    __threadfence();
     if (t < 64) sHist[t] = 0u;
     __syncthreads();
     const int tw = W64 < 32 ? W64 : 32, th = H64 < 32 ? H64 : 32;
     for (int i = t; i < 32 * 32; i += 256) {
         const int x = i & 31, y = i >> 5;
-        if (x < tw && y < th) atomicAdd(&sHist[histogram_bin(P.c64[y * W64 + x])], 1u);
+        if (x < tw && y < th) {
+            const unsigned long long q = __hip_atomic_load((const unsigned long long*)&P.c64[y * W64 + x],
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicAdd(&sHist[histogram_bin(make_uint2((uint32_t)q, (uint32_t)(q >> 32)))], 1u);
+        }
     }
     __syncthreads();
     if (t < 64) {

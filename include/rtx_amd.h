@@ -24,6 +24,9 @@ extern "C" {
 #define RT_ERR_IO (-3)          /* config / data file problem */
 #define RT_ERR_STATE (-4)       /* call out of order (e.g. draw before init) */
 #define RT_ERR_NO_DEVICE (-5)   /* no gfx950 device visible */
+#define RT_ERR_DEVICE (-6)      /* a kernel reported a failure (rt_last_error has the text): the LBVH's
+                                   TLAS workgroup timed out waiting for a batch; the frames since the
+                                   last check may be wrong, the renderer re-armed itself */
 
 typedef struct rt_context rt_context;
 

@@ -25,8 +25,6 @@
 //              LDS: four workgroups per CU, so 937 batches (the 958,720-triangle scene, BASELINE
 //              config 4) run in one round on 256 CUs instead of two rounds of 512.
 // The launcher takes 512 when the batches would not fit 2 per CU.
-#include <stdlib.h>
-
 #include "bvh_kernels.h"
 #include "rt_device.h"
 
@@ -70,20 +68,18 @@ RT_DEV void store_box(float* p, const Box& b) {
     p[3] = b.mx.x; p[4] = b.mx.y; p[5] = b.mx.z;
 }
 
-// A box through agent-scope relaxed atomics: stores and loads that are coherent across the XCDs' L2s
-// by themselves (sc1), so the cross-workgroup TLAS leaf boxes need no release fence — on gfx950 an
-// agent-scope release writes back the producer XCD's whole L2, which doubled every batch's gather.
+// A TLAS leaf box through the cross-workgroup hand-off of rt_device.h (xwg_*: agent-coherent stores
+// and loads, no release fence — on gfx950 an agent-scope release writes back the producer XCD's
+// whole L2, which doubled every batch's gather).
 RT_DEV void store_box_agent(float* p, const Box& b) {
     const float v[6] = {b.mn.x, b.mn.y, b.mn.z, b.mx.x, b.mx.y, b.mx.z};
 #pragma unroll
-    for (int k = 0; k < 6; ++k)
-        __hip_atomic_store((uint32_t*)p + k, __float_as_uint(v[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < 6; ++k) xwg_store((uint32_t*)p + k, __float_as_uint(v[k]));
 }
 RT_DEV Box load_box_agent(const float* p) {
     float v[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k)
-        v[k] = __uint_as_float(__hip_atomic_load((const uint32_t*)p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (int k = 0; k < 6; ++k) v[k] = __uint_as_float(xwg_load((const uint32_t*)p + k));
     Box b;
     b.mn = f3(v[0], v[1], v[2]);
     b.mx = f3(v[3], v[4], v[5]);
@@ -418,11 +414,13 @@ __shared__ uint32_t g_stamp[8];
 #endif
 
 // A batch's TLAS leaf box, published to the TLAS workgroup (tlas_builder): agent-coherent stores,
-// complete before the count that announces them.  Thread 0 of the batch's workgroup.
+// complete before the count that announces them (xwg_arrive).  Thread 0 of the batch's workgroup.
+// P.skipPublish names a batch that publishes nothing: fault injection for the TLAS wait's timeout
+// path ([debug] bvhSkipPublish, tests only; 0xFFFFFFFF otherwise).
 RT_DEV void publish_root(const BvhBuildParams& P, uint32_t b, const Box& root) {
+    if (b == P.skipPublish) return;
     store_box_agent(P.tlasAabbs + 6 * (size_t)b, root);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(P.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    xwg_arrive(P.counter);
 }
 
 // Sort the keys in key0/idx0 and build the tree of n leaves into `nodes`.  pub: publish batch b's
@@ -522,22 +520,39 @@ constexpr uint32_t kTlasWaveMax = 64;
 // workgroup B of the launch.  Each batch's workgroup publishes its TLAS leaf box (its BLAS root's
 // merged box, computed from the leaf boxes right after the gather) and then counts itself in the
 // launch counter; this workgroup, dispatched after every batch's, waits for all B of them, so the
-// TLAS is built while the batches sort, Karras-link and refit.  It resets the counter for the next
-// launch.
+// TLAS is built while the batches sort, Karras-link and refit.
+//
+// The wait is bounded by the wall clock (P.waitTicks of s_memrealtime, 1 s by default): a batch
+// that never publishes must not leave a wave spinning until the GPU is reset.  On a timeout the TLAS
+// is still built (from the boxes that are there: the grid drains normally), and the number of
+// missing batches goes to the host's status word, which rt_sync / rt_build_bvh report as
+// RT_ERR_DEVICE and answer by re-arming the counters.  The counter is re-armed here by subtracting
+// B, not by storing 0: a late publisher's count then still lands, and the counter is back at 0 when
+// the launch ends whatever the timing.
+RT_DEV void tlas_wait(const BvhBuildParams& P, uint32_t B) {
+    if (threadIdx.x == 0) {
+        uint32_t seen = xwg_load(P.counter);
+        if (seen < B) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while ((seen = xwg_load(P.counter)) < B && __builtin_amdgcn_s_memrealtime() - t0 < P.waitTicks)
+                __builtin_amdgcn_s_sleep(2);
+        }
+        if (seen < B) report_status(P.status, kStatusTlasTimeout, B - seen);
+        xwg_acquire();
+    }
+    __syncthreads();  // the boxes are read below with agent-coherent loads only
+}
+RT_DEV void tlas_rearm(const BvhBuildParams& P, uint32_t B) {
+    __hip_atomic_fetch_sub(P.counter, B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int kThr>
 RT_DEV void tlas_builder(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
     constexpr int kPer = kBatch / kThr;
     const int t = threadIdx.x;
-    if (t == 0) {
-        // bounded (~2^24 polls, about a second): a batch that never publishes would leave a wrong
-        // TLAS (which every parity test sees) rather than a wave spinning until the GPU is reset
-        for (uint32_t k = 0; k < (1u << 24) &&
-                             __hip_atomic_load(P.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < B; ++k)
-            __builtin_amdgcn_s_sleep(2);
-    }
-    __syncthreads();  // every box is published; they are read below with coherent loads only
+    tlas_wait(P, B);
 #if defined(RTX_BVH_ABL) && RTX_BVH_ABL == 1
-    if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) tlas_rearm(P, B);
     return;  // timing ablation: no TLAS
 #endif
     if (B <= kTlasWaveMax) {  // wave 0 alone
@@ -545,7 +560,7 @@ RT_DEV void tlas_builder(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
 #ifdef RTX_BVH_STAMPS
         if (t == 0) *(uint32_t*)P.tlasSceneAabb = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-        if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0) tlas_rearm(P, B);
         return;
     }
     Box rq = box_empty();  // this thread's contribution to the quirk reduction
@@ -584,7 +599,7 @@ RT_DEV void tlas_builder(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
 #ifdef RTX_BVH_STAMPS
     if (t == 0) *(uint32_t*)P.tlasSceneAabb = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
-    if (t == 0) __hip_atomic_store(P.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) tlas_rearm(P, B);
 }
 
 // kThr 1024: 8 waves/SIMD = 2 workgroups per CU; kThr 512: 4 workgroups per CU.  Either way <= 64
@@ -688,18 +703,11 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
 }
 
 // Batches that fit two 1024-thread workgroups per CU take that shape; more take the 512-thread one,
-// four per CU ([render] bvhThreads, or RTX_BVH_THREADS=512|1024, forces one: tests and A/B).
+// four per CU ([render] bvhThreads forces one: tests and A/B).  p->cus is the device's CU count,
+// queried once by rt_init for the context's device.
 extern "C" hipError_t rtk_launch_build_bvh(const BvhBuildParams* p, hipStream_t stream) {
-    static int forced = [] {
-        const char* a = getenv("RTX_BVH_THREADS");
-        return a ? atoi(a) : 0;
-    }();
-    int dev = 0, cus = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e != hipSuccess) return e;
-    const int want = p->threads ? (int)p->threads : forced;
-    const bool narrow = want == 512 || (want != 1024 && (int)p->batchCount > 2 * cus);
+    const int want = (int)p->threads;
+    const bool narrow = want == 512 || (want != 1024 && p->batchCount > 2 * p->cus);
     const unsigned grid = p->batchCount + 1u;  // one workgroup per batch, then the TLAS's
     if (narrow) hipLaunchKernelGGL(k_build_bvh<512>, dim3(grid), dim3(512), 0, stream, *p);
     else hipLaunchKernelGGL(k_build_bvh<1024>, dim3(grid), dim3(1024), 0, stream, *p);

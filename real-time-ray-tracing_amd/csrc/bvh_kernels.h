@@ -3,6 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// words of rt_context::status, the pinned host block kernels report failures into (rt_device.h
+// report_status; checked by sync_streams and rt_build_bvh)
+constexpr int kStatusTlasTimeout = 0;  // the TLAS workgroup gave up waiting: the number of missing batches
+
 struct BvhBuildParams {
     const float* vertices;     // [nv][3]
     const float* normals;      // [nv][3]
@@ -23,8 +27,12 @@ struct BvhBuildParams {
     uint32_t* tlasMorton;      // [1024]
     uint32_t* tlasReorder;     // [1024]
     void* tlasNodes;           // [B] = nodes + 64 * B*1024 bytes
-    uint32_t* counter;         // arrival counter, zero between launches
+    uint32_t* counter;         // arrival counter, zero between launches (re-armed by the TLAS workgroup)
     uint32_t threads;          // workgroup shape: 0 = by batch count, 512 or 1024 ([render] bvhThreads)
+    uint32_t cus;              // the device's CU count (rt_init), for the shape choice
+    uint32_t* status;          // pinned host words of device failure reports (rt_device.h report_status)
+    uint64_t waitTicks;        // the TLAS workgroup's wait bound in s_memrealtime ticks
+    uint32_t skipPublish;      // fault injection: this batch does not publish (0xFFFFFFFF: none)
 };
 
 struct TraceCamera {

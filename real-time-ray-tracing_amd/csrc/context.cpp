@@ -329,6 +329,8 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
     ctx->stripCount = rttoml::find_or_int(doc, "render", "stripCount", 1);
     ctx->stripIndex = rttoml::find_or_int(doc, "render", "stripIndex", 0);
     ctx->materialOverride = rttoml::find_or_int(doc, "render", "materialOverride", -1);
+    ctx->bvhSkipPublish = (uint32_t)rttoml::find_or_int(doc, "debug", "bvhSkipPublish", -1);
+    ctx->bvhWaitMs = rttoml::find_or_float(doc, "debug", "bvhWaitMs", 1000.0f);
     if (ctx->screenW <= 0 || ctx->screenH <= 0 || ctx->screenW > 16384 || ctx->screenH > 16384 || ctx->spp < 1 ||
         ctx->spp > 64 || ctx->chunkDim < 1 || ctx->chunkDim > 8 ||
         (ctx->bvhThreads != 0 && ctx->bvhThreads != 512 && ctx->bvhThreads != 1024)) {
@@ -400,7 +402,12 @@ int rt_init(rt_context* ctx) {
         ctx->err = std::string("librtx is built for gfx950, device is ") + prop.gcnArchName;
         return RT_ERR_NO_DEVICE;
     }
-
+    ctx->cuCount = prop.multiProcessorCount;
+    int wallKhz = 0;
+    if (hipDeviceGetAttribute(&wallKhz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && wallKhz > 0)
+        ctx->wallTicksPerMs = (uint64_t)wallKhz;
+    HIP_TRY(ctx, hipHostMalloc((void**)&ctx->status, 64, hipHostMallocDefault));
+    memset(ctx->status, 0, 64);
 
     // the context stream (the trace chain, a frame's critical path); with RTX_STREAMS=prio it is
     // created at the highest priority and the side / internal post streams at the lowest, otherwise
@@ -488,6 +495,7 @@ void rt_destroy(rt_context* ctx) {
     if (ctx->ownPostStream) (void)hipStreamDestroy(ctx->ownPostStream);
     for (void* p : ctx->allocations) (void)hipFree(p);
     if (ctx->fr.q3Host) (void)hipHostFree(ctx->fr.q3Host);
+    if (ctx->status) (void)hipHostFree(ctx->status);
     for (hipEvent_t e : ctx->markPool)
         if (e) (void)hipEventDestroy(e);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -587,6 +595,7 @@ void bvh_select(rt_context* ctx, int k) {
 int rt_build_bvh(rt_context* ctx) {
     if (!ctx) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_build_bvh before rt_init"; return RT_ERR_STATE; }
+    if (int rc = check_device_status(ctx)) return rc;  // a previous build's failure, once it is known
     hipStream_t stream = ctx->stream;
     ctx->bvhPrebuilt = false;  // an explicit build supersedes a synchronous draw's prebuild
     if (!ctx->postStream) ctx->buildOnSide[ctx->bvhSet] = false;
@@ -617,6 +626,10 @@ int rt_build_bvh(rt_context* ctx) {
     p.tlasNodes = ctx->dTlasNodes;
     p.counter = ctx->dCounter;
     p.threads = (uint32_t)ctx->bvhThreads;
+    p.cus = (uint32_t)ctx->cuCount;
+    p.status = ctx->status;
+    p.waitTicks = (uint64_t)((double)ctx->bvhWaitMs * (double)ctx->wallTicksPerMs);
+    p.skipPublish = ctx->bvhSkipPublish;
     HIP_TRY(ctx, rtk_launch_build_bvh(&p, stream));
     if (ctx->postStream) {
         HIP_TRY(ctx, hipEventRecord(ctx->buildDone[ctx->bvhSet], stream));

@@ -110,7 +110,8 @@ struct FrameResources {
     int lastSlot = 0;                  // slot of the last path trace (RT_ARR_PT_Q*)
     // queue 3's length after the last serial path trace, copied to pinned host memory behind it
     // (the fused chain's on/off choice for serial frames)
-    uint32_t* q3Host = nullptr;
+    unsigned long long* q3Host = nullptr;  // {length, tag} stored by k_pt_resolve (poll_q3)
+    uint32_t q3Tag = 0;                    // tag of the serial frame whose length is pending
     bool q3Pending = false;
     uint32_t lastQ3 = 0;
     bool lastChain = false;  // the last path trace ran the fused k_pt_chain (rt_info.lastChain)
@@ -177,6 +178,10 @@ struct rt_context {
     int stripCount = 1, stripIndex = 0;  // [render] stripCount/stripIndex: interleaved row blocks (row_of)
     int device = -1;
     int materialOverride = -1;  // [render] materialOverride: one material for every triangle (tests)
+    // [debug] fault injection (tests): a batch whose TLAS leaf box is never published, and the TLAS
+    // workgroup's wait bound (rt_device.h report_status)
+    uint32_t bvhSkipPublish = 0xFFFFFFFFu;
+    float bvhWaitMs = 1000.0f;
 
     std::string err;
     bool inited = false;
@@ -192,6 +197,9 @@ struct rt_context {
     uint32_t B = 0, nv = 0;
 
     // ---- device
+    int cuCount = 0;                   // the device's CUs (LBVH workgroup shape)
+    uint64_t wallTicksPerMs = 100000;  // s_memrealtime rate (hipDeviceAttributeWallClockRate)
+    uint32_t* status = nullptr;        // pinned host words the kernels report failures into (kStatus*)
     hipStream_t stream = nullptr;      // stream every stage is enqueued on
     hipStream_t ownStream = nullptr;   // the one rt_init created (destroyed by rt_destroy)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -285,6 +293,8 @@ int rt_create_stream(rt_context* ctx, hipStream_t* s, bool high);  // context.cp
 extern "C" int ensure_bvh_pair(rt_context* ctx);  // frame.cpp: second LBVH set, side stream, build events
 int rt_frame_init(rt_context* ctx);  // frame.cpp: sky tables, textures, G-buffers
 int sync_streams(rt_context* ctx);   // frame.cpp: context, post and side streams
+void poll_q3(rt_context* ctx);       // frame.cpp: the last serial frame's queue-3 length, if stored
+int check_device_status(rt_context* ctx);  // frame.cpp: kernel failure reports (RT_ERR_DEVICE)
 bool strip_local_denoise(const rt_context* ctx, uint32_t& a, uint32_t& b);  // frame.cpp: next denoise's rows
 extern "C" int copy_rgba_out(rt_context* ctx, void* dst);  // frame.cpp: the last frame's RGBA8 to host memory
 extern "C" size_t rt_alloc_bytes(const rt_context* ctx, int name);  // frame.cpp: allocated size of a render buffer

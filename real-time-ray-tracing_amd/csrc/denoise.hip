@@ -784,16 +784,14 @@ __global__ __launch_bounds__(256) void k_downscale_chain(DenoisePostParams P, co
     }
     __syncthreads();
     if (t == 0) {
-        // The 1/64 texel goes out as an agent-scope relaxed atomic store (coherent across the XCDs'
-        // L2s by itself), complete before this workgroup's count; the last workgroup reads the
-        // texels with agent-scope loads.  No release / acquire fence: on gfx950 those write back and
-        // invalidate the XCD's whole L2 (buffer_wbl2 / buffer_inv), once per workgroup.
+        // the 1/64 texel handed to the last workgroup through rt_device.h's xwg_* (agent-coherent
+        // store, then the count; no release fence: on gfx950 that writes back and invalidates the
+        // XCD's whole L2, once per workgroup); the last one takes one acquire
         const uint2 v = down4(LdsLevel{s16, W16, H16, X * 4, Y * 4, 4}, X, Y);
-        __hip_atomic_store((unsigned long long*)&P.c64[Y * W64 + X], ((unsigned long long)v.y << 32) | v.x,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        sLast = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                gridDim.x * gridDim.y - 1;
+        xwg_store((unsigned long long*)&P.c64[Y * W64 + X], ((unsigned long long)v.y << 32) | v.x);
+        const bool last = xwg_arrive(counter) == gridDim.x * gridDim.y - 1;
+        if (last) xwg_acquire();
+        sLast = last;
     }
     __syncthreads();
     if (!sLast) return;
@@ -803,8 +801,7 @@ __global__ __launch_bounds__(256) void k_downscale_chain(DenoisePostParams P, co
     for (int i = t; i < 32 * 32; i += 256) {
         const int x = i & 31, y = i >> 5;
         if (x < tw && y < th) {
-            const unsigned long long q = __hip_atomic_load((const unsigned long long*)&P.c64[y * W64 + x],
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long q = xwg_load((const unsigned long long*)&P.c64[y * W64 + x]);
             atomicAdd(&sHist[histogram_bin(make_uint2((uint32_t)q, (uint32_t)(q >> 32)))], 1u);
         }
     }

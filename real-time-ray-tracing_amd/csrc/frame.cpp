@@ -301,12 +301,37 @@ int sync_streams(rt_context* ctx) {
     if (ctx->sideStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->sideStream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->postStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->postStream));
+    poll_q3(ctx);
+    return check_device_status(ctx);
+}
+
+// The last serial frame's queue-3 length (rt_path_trace's chain choice), if k_pt_resolve has
+// stored it: the pinned word pairs the length with the tag of the frame that asked for it, so a
+// host that never syncs still picks it up at its next path trace, without waiting.
+void poll_q3(rt_context* ctx) {
     FrameResources& fr = ctx->fr;
-    if (fr.q3Pending) {  // the last serial frame's queue-3 length (rt_path_trace's chain choice)
-        fr.lastQ3 = *fr.q3Host;
-        fr.q3Pending = false;
-    }
-    return RT_OK;
+    if (!fr.q3Pending) return;
+    const unsigned long long v = __atomic_load_n(fr.q3Host, __ATOMIC_ACQUIRE);
+    if ((uint32_t)(v >> 32) != fr.q3Tag) return;
+    fr.lastQ3 = (uint32_t)v;
+    fr.q3Pending = false;
+}
+
+// Failures the kernels reported into the pinned status words (rt_device.h report_status): the
+// LBVH's TLAS workgroup timed out waiting for a batch's publication.  The error is reported once,
+// and the launch counters of both LBVH sets are re-armed (a batch that never published left its
+// set's counter one short).  Called after the streams are idle (sync_streams) or before a build.
+int check_device_status(rt_context* ctx) {
+    const uint32_t missing = __atomic_load_n(&ctx->status[kStatusTlasTimeout], __ATOMIC_ACQUIRE);
+    if (!missing) return RT_OK;
+    if (ctx->sideStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->sideStream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (const BvhBufs& b : ctx->bvh)
+        if (b.counter) HIP_TRY(ctx, hipMemset(b.counter, 0, 64));
+    __atomic_store_n(&ctx->status[kStatusTlasTimeout], 0u, __ATOMIC_RELEASE);
+    ctx->err = "LBVH build: the TLAS workgroup timed out waiting for " + std::to_string(missing) +
+               " batch publication(s); the TLAS of that build (and the frames traced on it) may be wrong";
+    return RT_ERR_DEVICE;
 }
 
 // UpdateFrame's timer (kernel.cu:67-71): the frame time rt_draw already took, the fixed one
@@ -661,6 +686,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     // four kernels faster serially too (4.64 against 5.11 ms per synchronous terrain draw).  The
     // length is that of the last serial frame a host sync completed (q3Host, stored by the frame's
     // resolve kernel, read in sync_streams: a fixed schedule, no event on the stream).
+    poll_q3(ctx);
     p.ws.chain = fr.ws.chain == 2 || (fr.ws.chain == 1 && !ctx->postStream && fr.lastQ3 < kChainMaxQ3);
     fr.lastChain = p.ws.chain && !p.ws.glossy && !p.ws.microfacet;  // as rtk_launch_pt_rest decides
     if (with_detail) {  // per-pixel counters: everything in order on the context stream
@@ -703,8 +729,12 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     }
     PtLaunchHook hook{overlap_hook, ctx};
     if (!side && !fr.q3Pending) {  // serial frames: queue 3's length for the next frame's chain choice
-        if (!fr.q3Host) HIP_TRY(ctx, hipHostMalloc((void**)&fr.q3Host, sizeof(uint32_t), hipHostMallocDefault));
+        if (!fr.q3Host) {
+            HIP_TRY(ctx, hipHostMalloc((void**)&fr.q3Host, sizeof(unsigned long long), hipHostMallocDefault));
+            *fr.q3Host = 0ull;
+        }
         p.ws.q3HostOut = fr.q3Host;  // stored by k_pt_resolve (no copy on the stream)
+        p.ws.q3Tag = ++fr.q3Tag;
         fr.q3Pending = true;
     }
     if (shadeSide) HIP_TRY(ctx, rtk_launch_pt_rest_after_shade(&p, ctx->stream, ctx->ptMarks, &hook));

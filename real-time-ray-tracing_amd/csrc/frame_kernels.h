@@ -110,7 +110,8 @@ struct PtWorkspace {
     int microfacet;             // materials can be the microfacet one (materialOverride 4): GGX compiled in
     int chain = 1;              // default materials: trace<3> .. resume<4> as one launch (k_pt_chain)
     uint32_t* itersOut = nullptr;  // optional [cap]: traversal iterations per queue entry (rt_trace_rays)
-    uint32_t* q3HostOut = nullptr; // optional, pinned host memory: queue 3's length, stored by k_pt_resolve
+    unsigned long long* q3HostOut = nullptr;  // optional, pinned host memory: {queue 3's length, q3Tag},
+    uint32_t q3Tag = 0;                       // stored by k_pt_resolve in one 64-bit store
 };
 
 // The frame's traced-ray count is kept as partial sums in kRayCounterSlots slots 128 B apart

@@ -1075,7 +1075,9 @@ __global__ __launch_bounds__(256) void k_pt_resolve(PathTraceParams P) {
     const uint32_t n = P.ws.counters[kCntPending];
     // serial frames: queue 3's length into pinned host memory for the next frame's chain choice
     // (frame.cpp), a vector store over the bus instead of a copy on the stream
-    if (P.ws.q3HostOut && blockIdx.x == 0 && threadIdx.x == 0) *(volatile uint32_t*)P.ws.q3HostOut = P.ws.counters[kCntQ3];
+    if (P.ws.q3HostOut && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(P.ws.q3HostOut, ((unsigned long long)P.ws.q3Tag << 32) | P.ws.counters[kCntQ3], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 #pragma unroll 1
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
         const uint32_t e = P.ws.pending[i];

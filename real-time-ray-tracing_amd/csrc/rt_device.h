@@ -100,4 +100,45 @@ RT_DEV Box box_merge(const Box& a, const Box& b) {  // AABBCompact::GetMerged or
     Box r; r.mx = max3(a.mx, b.mx); r.mn = min3(a.mn, b.mn); return r;
 }
 
+// ---- Cross-workgroup hand-offs inside one launch: producers publish values, then count
+// themselves on a launch counter; one consumer workgroup (the LBVH's TLAS workgroup, the downscale
+// chain's last workgroup) reads them once the count is complete.
+//
+// The producer side carries no release fence on purpose: on gfx950 an agent-scope release is
+// `buffer_wbl2 sc1`, a write-back of the producer XCD's whole L2, which doubled the LBVH gather
+// phase and cost the downscale chain a write-back per workgroup.  Instead the
+// values go out as agent-scope atomic stores — `global_store ... sc1`, written through to the
+// memory side, coherent across the XCDs' L2s by themselves — and `s_waitcnt vmcnt(0)` holds the
+// count back until they are complete: on gfx9 vmcnt counts stores too.  The consumer observes the
+// count, then takes an agent-scope acquire (`buffer_inv sc1`: once, in one workgroup) and reads
+// the values with agent-scope loads.  That ordering argument is specific to gfx950 (gfx10+ count
+// stores in vscnt, not vmcnt), so these helpers refuse to compile for anything else.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "rt_device.h xwg_* hand-offs rely on gfx950's sc1 write-through stores and vmcnt store counting"
+#endif
+RT_DEV void xwg_store(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+RT_DEV void xwg_store(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+RT_DEV uint32_t xwg_load(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+RT_DEV unsigned long long xwg_load(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the producer's count, after its xwg_store values are complete; returns the count before it
+RT_DEV uint32_t xwg_arrive(uint32_t* counter) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the consumer, once it has seen the complete count
+RT_DEV void xwg_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+
+// Device-side failure report to the host: a word of pinned host memory (rt_context::status, one
+// word per failure kind, bvh_kernels.h kStatus*, so a plain store suffices: no PCIe atomics), which
+// sync_streams checks after its stream synchronisations.
+RT_DEV void report_status(uint32_t* status, int word, uint32_t value) {
+    if (status) __hip_atomic_store(status + word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace rtd

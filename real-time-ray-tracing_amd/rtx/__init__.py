@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(_PKG, "lib", "librtx.so")
 DATA_DIR = os.path.join(_PKG, "data")
 
 RT_OK = 0
-ERRORS = {-1: "RT_ERR_ARG", -2: "RT_ERR_HIP", -3: "RT_ERR_IO", -4: "RT_ERR_STATE", -5: "RT_ERR_NO_DEVICE"}
+ERRORS = {-1: "RT_ERR_ARG", -2: "RT_ERR_HIP", -3: "RT_ERR_IO", -4: "RT_ERR_STATE", -5: "RT_ERR_NO_DEVICE", -6: "RT_ERR_DEVICE"}
 
 # rt_array_name (include/rtx_amd.h)
 ARR = dict(VERTICES=0, INDICES=1, NORMALS=2, TRI_POS=3, AABBS=4, MORTON=5, REORDER=6, NODES=7, TLAS_AABBS=8,

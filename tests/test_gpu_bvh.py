@@ -3,6 +3,8 @@ indices, node topology and boxes, TLAS — default scene and the ~1M-triangle va
 workgroup shapes of the build kernel ([render] bvhThreads: 1024 threads with leaf boxes in LDS,
 512 threads with two elements each and leaf boxes read back from the AABB array; 0 picks by the
 batch count: 1024 for the default scene's 60 batches, 512 for the 1M scene's 937)."""
+import time
+
 import numpy as np
 import pytest
 
@@ -68,5 +70,40 @@ def test_bvh_rebuild_is_idempotent(rtx, tmp_path, threads):
         rt.build_bvh()
     rt.sync()
     assert np.array_equal(rt.download("NODES"), first)
+    assert np.array_equal(rt.download("TLAS_NODES"), tlas)
+    rt.cleanup()
+
+
+@pytest.mark.parametrize("chunk_dim,threads", [(1, 1024), (2, 512)])
+def test_tlas_wait_timeout_is_reported(rtx, tmp_path, chunk_dim, threads):
+    """The TLAS workgroup's bounded wait (bvh_build.hip tlas_wait): batch 1 never publishes its leaf
+    box ([debug] bvhSkipPublish fault injection), so the wait ends at its 20-ms bound.  The build
+    still drains, the failure reaches the host as RT_ERR_DEVICE at the next sync with the number of
+    missing batches, is reported once, and the launch counters are re-armed: the next faulty build
+    again misses exactly one batch (without the re-arm its count would start one short)."""
+    extra = "bvhThreads = %d\n\n[debug]\nbvhSkipPublish = 1\nbvhWaitMs = 20\n" % threads
+    cfg = rtx.write_config(str(tmp_path / "fault.toml"), 64, 64, chunk_dim=chunk_dim, extra=extra)
+    rt = rtx.RayTracer(64, 64, cfg).init()
+    assert rt.info().batchCount > (64 if chunk_dim > 1 else 1)  # the workgroup-wide TLAS path for chunk_dim 2
+    for _ in range(2):
+        rt.build_bvh()
+        with pytest.raises(rtx.RtError, match=r"RT_ERR_DEVICE .*for 1 batch publication"):
+            rt.sync()
+        rt.sync()  # reported once
+    rt.build_bvh()
+    time.sleep(0.5)  # the faulty build has ended (its wait is bounded at 20 ms)
+    with pytest.raises(rtx.RtError, match="rt_build_bvh: RT_ERR_DEVICE"):  # a known report stops the next build
+        rt.build_bvh()
+    rt.sync()
+    rt.cleanup()
+
+
+def test_tlas_no_fault_no_report(rtx, tmp_path):
+    """Healthy builds back to back with the bounded wait: no report, the TLAS equals the first one."""
+    rt = build_gpu(rtx, tmp_path, 1, threads=1024)
+    tlas = rt.download("TLAS_NODES").copy()
+    for _ in range(20):
+        rt.build_bvh()
+    rt.sync()
     assert np.array_equal(rt.download("TLAS_NODES"), tlas)
     rt.cleanup()

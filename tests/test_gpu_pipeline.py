@@ -162,3 +162,31 @@ def test_draw_device_target_sync_and_async(rtx, oracle, tmp_path, default_scene)
             assert (img[:, w * 4:] == 7).all()
         assert np.array_equal(last, o["rgba"])
         rt.cleanup()
+
+
+def test_chain_choice_refreshes_without_sync(rtx, tmp_path):
+    """Serial frames whose host never calls rt_sync still learn queue 3's length: the
+    resolve kernel stores {length, frame tag} into pinned memory and the next rt_path_trace picks it
+    up without waiting (frame.cpp poll_q3).  The terrain view's queue 3 (~3.9 M rays at 1080p 4 spp)
+    is past the fused chain's limit, so once the first frame's length is known the frames run the
+    four-kernel bounce stages (rt_info.lastChain 0) — with no host sync in between."""
+    import time
+
+    w, h = 1920, 1080
+    rt = rtx.RayTracer(w, h, rtx.write_config(str(tmp_path / "q3.toml"), w, h, spp=4)).init()
+    rt.set_delta_time(16.667)
+    cam = rt.camera
+    cam.pos[:] = (8.0, 15.0, -6.0)
+    cam.yaw, cam.pitch = 0.0, -0.7
+    rt.camera = cam
+    chains = []
+    for f in range(1, 6):
+        rt.build_bvh()
+        rt.path_trace(f)
+        rt.denoise_post(f)
+        chains.append(rt.info().lastChain)
+        time.sleep(0.1)  # the GPU finishes the frame meanwhile; the host does not synchronise
+    assert chains[0] == 1, chains  # nothing known yet: the short-queue default
+    assert chains[-1] == 0, chains  # the long queue-3 length arrived without an rt_sync
+    rt.sync()
+    rt.cleanup()

@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Per-kernel summary of separate rocprofv3 --pmc passes (tools/prof.sh).
+
+    python tools/pmc_report.py <out.json> <pass_dir>... [--key KEY] [--workload TEXT]
+
+Kernels are named by their symbol with boolean template arguments dropped and integer ones kept
+(k_spatial5<3, false> -> k_spatial5<3>, k_temporal<true> -> k_temporal); k_build_bvh is labelled by
+its workgroup count (k_build_bvh@61wg, @938wg).  Per kernel the median per-dispatch value of every
+counter is taken, then (MI355X_MICROARCH.md HBM, L2 and SQ sections):
+  hbm_bytes          = (2 * FETCH_SIZE + WRITE_SIZE) * 1024   (FETCH_SIZE, KB, counts half the bytes
+                       of wide reads on gfx950, so it is doubled; WRITE_SIZE in KB)
+  l2_hit_rate        = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
+  valu_busy_frac     = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES
+  wait_inst_any_frac = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES   (issue stalls)
+  wait_any_frac      = SQ_WAIT_ANY / SQ_WAVE_CYCLES        (parked on s_waitcnt / barriers)
+  valu_per_wave, lds_per_wave = SQ_INSTS_VALU, SQ_INSTS_LDS per wave
+  us                 = the dispatch's duration (median over the passes' dispatches)
+The path-trace stage's HBM bytes (`stage_hbm_bytes`, the seven kernels bench.py names) and the
+denoise/post chain's (`denoise_hbm_bytes`) are sums of per-kernel medians."""
+import collections
+import csv
+import glob
+import json
+import re
+import statistics
+import sys
+
+STAGE = ("k_pt_camera", "k_pt_shade0", "k_trace_queue<3>", "k_pt_resume<3>", "k_trace_queue<4>",
+         "k_pt_resume<4>", "k_pt_resolve")
+DENOISE = ("k_temporal", "k_spatial7", "k_spatial5<3>", "k_spatial5<6>", "k_spatial5<12>", "k_temporal2",
+           "k_downscale_chain", "k_scale_post")
+
+
+def short(name, grid, wg):
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+    n = re.sub(r"<(\d+)(, (true|false))+>", r"<\1>", n)
+    n = re.sub(r"<(true|false)(, (true|false))*>", "", n)
+    if n == "k_build_bvh" and wg:
+        n += "@%dwg" % (grid // wg)
+    return n
+
+
+def main():
+    args = sys.argv[1:]
+    key = workload = None
+    if "--key" in args:
+        i = args.index("--key")
+        key = args[i + 1]
+        del args[i:i + 2]
+    if "--workload" in args:
+        i = args.index("--workload")
+        workload = args[i + 1]
+        del args[i:i + 2]
+    out_path, dirs = args[0], args[1:]
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    dur = collections.defaultdict(list)
+    for d in dirs:
+        for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+            per = collections.defaultdict(lambda: collections.defaultdict(float))
+            span = {}
+            for r in csv.DictReader(open(f)):
+                k = short(r["Kernel_Name"], int(r["Grid_Size"] or 0), int(r["Workgroup_Size"] or 0))
+                per[(k, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+                span[(k, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            for (k, did), c in per.items():
+                for n, v in c.items():
+                    vals[k][n].append(v)
+                dur[k].append(span[(k, did)])
+    kernels = {}
+    for k, cv in vals.items():
+        c = {n: statistics.median(v) for n, v in cv.items()}
+        e = {"dispatches": max(len(v) for v in cv.values()), "us": round(statistics.median(dur[k]), 2)}
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            e["hbm_bytes"] = int(round((2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024))
+            e["fetch_bytes_doubled"] = int(round(2.0 * c["FETCH_SIZE"] * 1024))
+            e["write_bytes"] = int(round(c["WRITE_SIZE"] * 1024))
+        hit, miss = c.get("TCC_HIT_sum"), c.get("TCC_MISS_sum")
+        if hit is not None and miss is not None and hit + miss > 0:
+            e["l2_hit_rate"] = round(hit / (hit + miss), 4)
+        wc, w = c.get("SQ_WAVE_CYCLES"), c.get("SQ_WAVES")
+        if wc:
+            for n, f in (("SQ_ACTIVE_INST_VALU", "valu_busy_frac"), ("SQ_WAIT_INST_ANY", "wait_inst_any_frac"),
+                         ("SQ_WAIT_ANY", "wait_any_frac")):
+                if n in c:
+                    e[f] = round(c[n] / wc, 4)
+        if w:
+            e["waves"] = int(w)
+            for n, f in (("SQ_INSTS_VALU", "valu_per_wave"), ("SQ_INSTS_LDS", "lds_per_wave")):
+                if n in c:
+                    e[f] = round(c[n] / w, 1)
+        e["counters_median"] = c
+        kernels[k] = e
+    res = {"workload_key": key, "workload": workload, "passes": dirs, "kernels": kernels,
+           "stage_hbm_bytes": sum(kernels[k].get("hbm_bytes", 0) for k in STAGE if k in kernels) or None,
+           "denoise_hbm_bytes": sum(kernels[k].get("hbm_bytes", 0) for k in DENOISE if k in kernels) or None,
+           "correction": "FETCH_SIZE doubled (gfx950 counts half the bytes of wide reads), KB x 1024",
+           "note": "every counter group from its own rocprofv3 --pmc run; medians over all dispatches of the kernel"}
+    with open(out_path, "w") as f:
+        json.dump(res, f, indent=1)
+    order = sorted(kernels, key=lambda k: -kernels[k]["us"] * kernels[k]["dispatches"])
+    for k in order:
+        e = kernels[k]
+        print("%-22s n=%4d %9.2f us %s" % (k[:22], e["dispatches"], e["us"], " ".join(
+            "%s=%s" % (f, e[f]) for f in ("hbm_bytes", "l2_hit_rate", "valu_busy_frac", "wait_inst_any_frac",
+                                          "wait_any_frac", "waves", "valu_per_wave", "lds_per_wave") if f in e)))
+
+
+if __name__ == "__main__":
+    main()

@@ -30,17 +30,18 @@ fixed as N grows ("strong" scaling).  Timing: barrier + device sync on both side
 K frames, max over ranks; value = rays of all ranks / that time.
 
 Roofline: per path-trace kernel, algorithmic bytes from the GPU's own work
-counters (node visits x 64 B, triangle tests x 48 B, texel taps, queue records) over its average
-duration in the TIMED frames themselves: every path-trace kernel of the K timed frames is bracketed
-by HIP events on the stream it runs on (rt_frame_marks_begin / _read).  The roofline's top-level
-kernel is the longest kernel of the frame's critical (context) stream; the camera kernel runs on
-a side stream overlapped with the previous frame's chain (its duration there measures the overlap)
-and is listed with the others.  The process running the timed frames launches nothing else of the
-frame's path-trace kernels (the side measurements run in a child process), so a rocprofv3
+counters (node visits x 64 B, triangle tests x 48 B, texel taps, queue records); per denoise / post
+kernel its compulsory G-buffer / colour bytes (denoise_bytes); each over the kernel's HIP-event
+duration inside pipelined frames.  The top-level kernel is the longest kernel of the stream that
+binds the pipelined frame — the stream whose kernels add up to the most time in the warm-up frames,
+which have every kernel bracketed by HIP events (rt_frame_marks_begin / _read) — and it is timed in
+every one of the K timed frames the same way.  The process running the timed frames launches nothing
+else of the frame's kernels (the side measurements run in a child process), so a rocprofv3
 --kernel-trace --stats of this command gives, in this process's stats file, averages over exactly
-the warm-up + timed + detail frames.  The BVH and textures are cache-resident, so the memory
-ceiling that applies is L2 (MI355X_MICROARCH.md: 34.5 TB/s) and the measured HBM traffic (rocprofv3
-PMC passes) sits far below the algorithmic bytes; the limiter the SQ counters show is latency.
+the warm-up + timed + detail + split frames.  The BVH and textures are cache-resident, so the memory
+ceiling of the path-trace kernels is L2 (MI355X_MICROARCH.md: 34.5 TB/s) and their HBM traffic
+(rocprofv3 PMC passes) sits far below the algorithmic bytes; the denoise kernels are priced against
+HBM, with the PMC pass's VALU-busy share beside it.
 """
 import argparse
 import json
@@ -60,7 +61,7 @@ for p in (ROOT, PKG):
 HBM_PEAK_GBS = 8000.0   # /opt/skills/guides/MI355X_MICROARCH.md (spec peak)
 L2_PEAK_GBS = 34500.0   # MI355X_MICROARCH.md, L2 (per XCD) section: aggregate L2 bandwidth
 DELTA_MS = 16.667       # fixed AutoExposure step (SURVEY §8d determinism settings)
-PMC_FILE = os.path.join(ROOT, "profiles", "r04_pmc_kernels.json")  # tools/prof_r03.sh, round-4 run
+PMC_FILE = os.path.join(ROOT, "profiles", "r05_pmc_kernels.json")  # tools/prof.sh pmc of the pipelined frames
 PMC_C2C4 = os.path.join(ROOT, "profiles", "r04_pmc_c2c4.json")  # tools/prof_r04_c2c4.sh (configs 2 and 4)
 TERRAIN_CAM = dict(pos=(8.0, 15.0, -6.0), yaw=0.0, pitch=-0.7)  # ~50 % primary hits (tests' camera)
 
@@ -69,6 +70,53 @@ TERRAIN_CAM = dict(pos=(8.0, 15.0, -6.0), yaw=0.0, pitch=-0.7)  # ~50 % primary 
 # per queue entry its 80-B record (5 float4) written + read and its 20-B hit record, per camera
 # sample its 20-B hit record, per pixel the 30-B G-buffer
 NODE_B, TRI_B, TEX_B, QREC_B, HIT_B, GBUF_B = 64, 48, 48 * 8, 80, 20, 30
+
+# the frame's three streams and the kernels each runs when pipelined
+CONTEXT_KERNELS = ("k_trace_queue<3>", "k_pt_resume<3>", "k_trace_queue<4>", "k_pt_resume<4>", "k_pt_resolve")
+DENOISE_KERNELS = ("k_temporal", "k_spatial7", "k_spatial5<3>", "k_spatial5<6>", "k_spatial5<12>", "k_temporal2",
+                   "k_downscale_chain", "k_scale_post")
+
+
+def denoise_stats(rt, W, H):
+    """Inputs of the denoise kernels' algorithmic bytes, from the last denoised frame: surface pixels
+    (G-buffer depth below the reference's sky depth) and the pixels of the 16x16 tiles above the
+    local / large noise thresholds (the tiles SpatialFilter7x7 and the a-trous passes filter; the
+    others copy through)."""
+    p = rt.params.denoise
+    W16, H16 = (W + 15) // 16, (H + 15) // 16
+    n16 = rt.get_buffer("NOISE_LEVEL16", (H16, W16), np.float16).astype(np.float32)
+    depth = rt.get_buffer("DEPTH", (H, W), np.float16).astype(np.float32)
+    tile_px = np.full((H16, W16), 256.0)
+    tile_px[-1, :] = 16 * (H - 16 * (H16 - 1))
+    tile_px[:, -1] *= (W - 16 * (W16 - 1)) / 16.0
+    act7 = ~(n16 < p.noise_threshold_local)
+    act5 = ~(n16 < p.noise_threshold_large)
+    return {"pixels": W * H, "surface_px": int((depth < 10e9).sum()), "local_active_px": int(tile_px[act7].sum()),
+            "large_active_px": int(tile_px[act5].sum()), "local_active_tiles": round(float(act7.mean()), 4),
+            "large_active_tiles": round(float(act5.mean()), 4)}
+
+
+def denoise_bytes(st, Ws, Hs):
+    """Compulsory bytes of each denoise / post kernel per launch of the whole-frame chain (DESIGN.md
+    §4.2): every input pixel the kernel needs read once, every output written once; stencil taps'
+    re-reads of neighbours are cache hits and not counted.  Colour / normal / albedo / accumulation /
+    history texels are 8 B (half4), depth 2, motion 4, RGBA8 4.  The noise-gated passes run over the
+    active-tile lists: SpatialFilter7x7 and the first two a-trous passes touch only their lists' tiles,
+    TemporalFilter writes the other tiles' output into the accumulation buffer as well."""
+    P, S, A7, A5 = st["pixels"], st["surface_px"], st["local_active_px"], st["large_active_px"]
+    apron7 = 22 * 22 / 256.0 * (8 + 8 + 2)  # SpatialFilter7x7's LDS-staged colour, normal, depth apron
+    return {
+        # colour, normal, depth in, colour + history depth out; surface: motion, history; gated tiles
+        # also into the accumulation buffer
+        "k_temporal": 28 * P + 12 * S + 8 * (P - A7),
+        "k_spatial7": int((apron7 + 8 + 2) * A7),  # list 0: apron, out, the noise epilogue's depth
+        "k_spatial5<3>": 26 * A5,                 # list 1: colour, normal, depth in, colour out
+        "k_spatial5<6>": 26 * A5,
+        "k_spatial5<12>": 24 * P + 10 * A5,       # every tile: colour, albedo in, colour out (+ normal, depth)
+        "k_temporal2": 28 * P,                    # colour, motion, history in, history out
+        "k_downscale_chain": 8 * P + P // 2 + P // 32,  # colour in, 1/4 and 1/16 levels out
+        "k_scale_post": 8 * P + 12 * Ws * Hs,     # render colour in, scaled half4 + RGBA8 out
+    }
 
 
 def parse():
@@ -233,16 +281,49 @@ def kernel_roofline(q, W, rows, S, kernels_ms, pmc, workload_matches):
             "k_pt_resume<4>": {"rays": n4}, "k_pt_resolve": {}}
     out = {}
     for k, ms in kernels_ms.items():
+        if k not in alg:
+            continue
         a = alg[k] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         e = {"ms": round(ms, 5), "algorithmic_bytes": int(alg[k]), "achieved_GBs": round(a, 1),
              "frac_l2": round(a / L2_PEAK_GBS, 4), "work": work[k]}
-        if pmc and workload_matches and k in pmc.get("kernels", {}):
-            pk = pmc["kernels"][k]
-            for f in ("hbm_bytes", "l2_hit_rate", "wait_inst_any_frac", "valu_busy_frac"):
-                if f in pk:
-                    e[f] = pk[f]
+        add_pmc(e, k, pmc, workload_matches)
         out[k] = e
     return out
+
+
+def add_pmc(e, k, pmc, workload_matches):
+    if pmc and workload_matches and k in pmc.get("kernels", {}):
+        pk = pmc["kernels"][k]
+        for f in ("hbm_bytes", "l2_hit_rate", "wait_inst_any_frac", "wait_any_frac", "valu_busy_frac",
+                  "valu_per_wave"):
+            if f in pk:
+                e[f] = pk[f]
+
+
+def denoise_roofline(st, Ws, Hs, kernels_ms, pmc, workload_matches):
+    """Per denoise / post kernel: compulsory bytes (denoise_bytes) over its HIP-event ms against HBM.
+    The active tiles' stencil arithmetic, not bandwidth, sets most of these kernels' time: the PMC
+    pass's VALU-busy share says how far they are from their issue bound."""
+    alg = denoise_bytes(st, Ws, Hs)
+    out = {}
+    for k in DENOISE_KERNELS:
+        ms = kernels_ms.get(k)
+        if ms is None:
+            continue
+        a = alg[k] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        e = {"ms": round(ms, 5), "algorithmic_bytes": int(alg[k]), "achieved_GBs": round(a, 1),
+             "frac_hbm": round(a / HBM_PEAK_GBS, 4)}
+        add_pmc(e, k, pmc, workload_matches)
+        out[k] = e
+    return out
+
+
+def stream_kernels(shade_on_side):
+    """The kernels of each stream of a pipelined frame: side (camera rays [+ shade]), context (the
+    bounce / shadow queue chain [+ shade]), post (denoise + post)."""
+    side = ("k_pt_camera", "k_pt_shade0") if shade_on_side else ("k_pt_camera",)
+    ctx = CONTEXT_KERNELS if shade_on_side else ("k_pt_shade0",) + CONTEXT_KERNELS
+    return {"side": [k for k in side], "context": list(ctx), "post": list(DENOISE_KERNELS)}
 
 
 def pmc_c2c4(kernel, key):
@@ -380,7 +461,7 @@ def extras_child(args):
     fp.finish()
     rt.ray_count(reset=True)
     nt = 20
-    rt.frame_marks_begin(nt)
+    rt.frame_marks_begin(nt, rtx.RayTracer.PT_KERNELS)
     torch.cuda.synchronize()
     ta = time.perf_counter()
     for k in range(nt):
@@ -521,13 +602,13 @@ def main():
     pipeline = not args.no_pipeline
     fp = FramePipeline(rt, dev, pipelined=pipeline, world=world, rank=rank, backend=args.dist_backend)
 
-    # warm-up; frames 2..W with every path-trace kernel bracketed by HIP events, which picks the
-    # roofline's kernel: the longest on the frame's critical (context) stream (pipelined, the camera
-    # kernel and the shade kernel behind it run on the side stream beside the previous
-    # frame's tracers)
-    side = {"k_pt_camera", "k_pt_shade0"} if pipeline and rt.info().shadeOnSide else {"k_pt_camera"}
-    crit = [k for k in rtx.RayTracer.PT_KERNELS if not (pipeline and k in side)]
-    dom = "k_trace_queue<3>"
+    # warm-up; frames 2..W with every kernel (path trace and denoise / post) bracketed by HIP events
+    # on its stream.  The stream whose kernels add up to the most time per frame binds the
+    # pipelined frame (the denoise / post stream since round 4); the roofline's kernel
+    # is that stream's longest.  Serial frames: every kernel is on the critical path.
+    streams = stream_kernels(bool(rt.info().shadeOnSide)) if pipeline else {
+        "serial": list(rtx.RayTracer.FRAME_KERNELS)}
+    dom, bind, stream_ms, warm_ms = "k_trace_queue<3>", None, {}, {}
     if args.warmup >= 2:
         fp.frame(1)
         fp.finish()
@@ -536,7 +617,9 @@ def main():
             fp.frame(1 + k)
         fp.finish()
         warm_ms, _ = rt.frame_marks_read()
-        dom = max(crit, key=lambda k: warm_ms[k])
+        stream_ms = {n: round(sum(warm_ms.get(k, 0.0) for k in ks), 5) for n, ks in streams.items()}
+        bind = max(stream_ms, key=stream_ms.get)
+        dom = max(streams[bind], key=lambda k: warm_ms.get(k, 0.0))
     else:
         for k in range(args.warmup):
             fp.frame(1 + k)
@@ -605,7 +688,9 @@ def main():
     }
 
     # ---- per-kernel roofline over this rank's strip: work counters of one detail launch (after the
-    # timed frames), kernel durations from the timed frames' events
+    # timed frames), kernel durations from the timed frames' events; the denoise kernels' gating
+    # statistics from the last timed frame (whole-frame denoise: one GPU)
+    dst = denoise_stats(rt, W, H) if world == 1 else None
     rt.path_trace(last + 1, detail=True)
     st = rt.download("PT_STATS", np.uint32).reshape(-1, 4).astype(np.uint64)  # zero outside this rank's rows
     n_rays, visits, tests, diffuse = (int(st[:, k].sum()) for k in range(4))
@@ -633,30 +718,42 @@ def main():
     if timed_dom is not None:
         split = dict(split, **{dom: timed_dom})
     per = kernel_roofline(counters, W, rows, S, split, pmc, matches)
-    d = per[dom]
+    dn = denoise_roofline(dst, args.width, args.height, split, pmc, matches) if dst else {}
     stage_bytes = sum(e["algorithmic_bytes"] for e in per.values())
     stage_ms = sum(e["ms"] for e in per.values())
+    d = per.get(dom) or dn[dom]
+    on_l2 = dom in per
+    peak = L2_PEAK_GBS if on_l2 else HBM_PEAK_GBS
+    a = d["achieved_GBs"]
     result["roofline"] = {
-        "bound": "l2", "limiter": "latency",
+        "bound": "l2" if on_l2 else "hbm", "limiter": "latency",
         "kernel": dom, "kernel_ms": d["ms"], "algorithmic_bytes": d["algorithmic_bytes"],
-        "achieved": d["achieved_GBs"], "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": d["frac_l2"],
+        "achieved": a, "peak": peak, "unit": "GB/s", "frac": round(a / peak, 4),
         "traffic": d.get("hbm_bytes"),
         "traffic_source": os.path.relpath(PMC_FILE, ROOT) if matches else None,
-        "note": "kernel = the longest kernel on the frame's critical (context) stream; BVH nodes, triangles and "
-                "textures (~34 MB) stay in L2 / Infinity Cache: the applicable memory ceiling is L2 bandwidth, HBM "
-                "traffic is far below the algorithmic bytes, and the kernels wait on dependent node loads "
-                "(latency), not on bandwidth",
-        "kernels": per,
+        "valu_busy_frac": d.get("valu_busy_frac"),
+        "binding_stream": bind,
+        "stream_kernel_ms": stream_ms,
+        "note": ("kernel = the longest kernel of the stream that binds the frame: the stream whose kernels add up to "
+                 "the most time per frame in the marked warm-up frames (stream_kernel_ms; pipelined: side = camera "
+                 "rays + shade, context = the bounce / shadow queue chain, post = denoise + post).  "
+                 + ("A path-trace kernel: BVH nodes, triangles and textures (~34 MB) stay in L2 / Infinity Cache, so "
+                    "the memory ceiling is L2 bandwidth; it waits on dependent node loads (latency)." if on_l2 else
+                    "A denoise / post kernel: algorithmic bytes are its compulsory G-buffer / colour traffic against "
+                    "HBM; its time is the noise-gated tiles' stencil arithmetic and its waves' wait for issue slots "
+                    "beside the next frame's path-trace waves (valu_busy_frac: share of wave time issuing VALU)")),
+        "kernels": dict(per, **dn),
+        "denoise_gating": dst,
         "stage": {"kernels": " -> ".join(per), "algorithmic_bytes": stage_bytes, "sum_kernel_ms": round(stage_ms, 5),
                   "achieved_GBs": round(stage_bytes / (stage_ms * 1e-3) / 1e9, 1),
                   "frac_l2": round(stage_bytes / (stage_ms * 1e-3) / 1e9 / L2_PEAK_GBS, 4),
                   "rays": n_rays, "node_visits": visits, "tri_tests": tests, "diffuse_events": diffuse,
                   "hbm_bytes": pmc.get("stage_hbm_bytes") if matches else None},
         "timing": ("%s: HIP events right before / after it on the stream it runs on, in every one of the %d "
-                   "timed frames (rt_frame_marks); chosen as the longest critical-stream kernel of warm-up frames "
-                   "2..%d; the other kernels: the same events over 20 pipelined frames after the timed ones "
+                   "timed frames (rt_frame_marks); chosen from warm-up frames 2..%d with every kernel marked; the "
+                   "other kernels: the same events over 20 pipelined frames after the timed ones "
                    "(rt_time_frame_kernels); rocprofv3 --kernel-trace --stats of this command: "
-                   "profiles/r04_kernel_stats.csv (this process: warm-up, timed, 1 detail and the 20 split frames)"
+                   "profiles/r05_kernel_stats.csv (this process: warm-up, timed, 1 detail and the 20 split frames)"
                    % (dom, marked, args.warmup)),
         "kernel_ms_split_frames": round(split_dom, 5) if split_dom is not None else None,
     }

@@ -361,13 +361,17 @@ int rt_time_path_trace_kernels(rt_context* ctx, int iters, float* kernel_ms, int
 /* The same split over `iters` whole frames (LBVH build + path trace + denoise/post of frames
  * first_frame, first_frame + 1, ...) run exactly as a caller runs them: on a pipelined context
  * (rt_set_post_stream) each kernel is timed on the stream it runs on, beside the other streams'
- * work.  Waits for the frames.  Measurement aid for bench.py's per-kernel roofline. */
+ * work.  With n >= 15 entries 7..14 are the denoise / post chain's kernels (TemporalFilter,
+ * SpatialFilter7x7, the three a-trous passes, TemporalFilter2, the DownScale4 / histogram /
+ * AutoExposure chain, the scale / sharpen / tone map / dither pass), each averaged over the frames
+ * that launched it.  Waits for the frames.  Measurement aid for bench.py's per-kernel roofline. */
 int rt_time_frame_kernels(rt_context* ctx, int first_frame, int iters, float* kernel_ms, int n);
 
-/* The same split recorded inside the caller's own frames: the next `frames` path traces bracket
- * the kernels whose bit is set in kernel_mask (bit k = kernel k, order as above) with HIP events on
- * the stream each runs on (two events per kernel, no synchronisation); rt_frame_marks_read waits,
- * writes the per-kernel average milliseconds over the frames recorded (n >= 7; -1 for kernels not
+/* The same split recorded inside the caller's own frames: the next `frames` frames (each a path
+ * trace and the rt_denoise_post that follows it) bracket the kernels whose bit is set in
+ * kernel_mask (bit k = kernel k, the 15 kernels above) with HIP events on the stream each runs on
+ * (two events per kernel, no synchronisation); rt_frame_marks_read waits, writes the per-kernel
+ * average milliseconds over the frames recorded (n >= 7 entries, up to 15; -1 for kernels not
  * marked) and stops recording.  bench.py's warm-up and timed frames use it. */
 int rt_frame_marks_begin(rt_context* ctx, int frames, uint32_t kernel_mask);
 int rt_frame_marks_read(rt_context* ctx, float* kernel_ms, int n, int* frames_recorded);

@@ -193,6 +193,26 @@ extern "C" long orc_div_const_mismatches(float d, uint32_t stride) {
     return bad;
 }
 
+// rt_div_rcp(x, d, RN(1/d)) (the denoiser's depth weights, rtmath.h) against the IEEE division,
+// over every stride-th float bit pattern x with x = 0 or 2^-30 <= |x| <= 2^30, plus +-inf and NaN:
+// mismatches (NaN compared as NaN)
+extern "C" long orc_div_rcp_mismatches(float d, uint32_t stride) {
+    volatile float dv = d;
+    const float c = 1.0f / dv;
+    long bad = 0;
+    auto check = [&](float x) {
+        const float ref = x / dv, got = rt_div_rcp(x, d, c);
+        if (memcmp(&ref, &got, 4) != 0 && !(ref != ref && got != got)) ++bad;
+    };
+    for (uint64_t u = 0; u < (1ull << 32); u += stride) {
+        const float x = rtm::bits_to_float((uint32_t)u);
+        const float ax = fabsf(x);
+        if (ax >= 0x1p-30f && ax <= 0x1p30f) check(x);
+    }
+    for (float x : {0.0f, -0.0f, INFINITY, -INFINITY, NAN}) check(x);
+    return bad;
+}
+
 // UpdateFrame's dynamic resolution (kernel.cu:77-100), restated: outside the targetFps +-2 band
 // the width is scaled (int *= float) by sqrt(target frame time / dt); it is then snapped to the
 // nearest multiple of 16 (ties of 8 round up), clamped by clampi to [minW, maxW], and the height

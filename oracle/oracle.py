@@ -90,6 +90,8 @@ def lib() -> C.CDLL:
         L.orc_rtmath.restype = C.c_float
         L.orc_div_const_mismatches.argtypes = [C.c_float, C.c_uint32]
         L.orc_div_const_mismatches.restype = C.c_long
+        L.orc_div_rcp_mismatches.argtypes = [C.c_float, C.c_uint32]
+        L.orc_div_rcp_mismatches.restype = C.c_long
         L.orc_unorm16_mismatches.argtypes = []
         L.orc_unorm16_mismatches.restype = C.c_int
         L.orc_f2h_n.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]

@@ -713,33 +713,44 @@ int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms) {
 
 // per-kernel HIP-event split of `iters` path traces: serial ones (stage 2 of rt_time_stage) or,
 // with `frames` set, whole frames (BVH + path trace + denoise/post) as the caller runs them, so
-// on a pipelined context each kernel is timed beside the other streams' work (bench.py)
+// on a pipelined context each kernel is timed beside the other streams' work (bench.py).  Kernels
+// 0..6 are the path trace's, 7..14 (frames only, n >= 15) the denoise / post chain's; a denoise
+// kernel's average is over the frames that launched it (its events read 0 ms otherwise).
 static int time_kernels(rt_context* ctx, int first_frame, int iters, float* kernel_ms, int n, bool frames) {
     if (!ctx || !kernel_ms || iters < 1 || n < kPtKernels || first_frame < 1) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_time_*_kernels before rt_init"; return RT_ERR_STATE; }
-    std::vector<hipEvent_t> marks((size_t)iters * 2 * kPtKernels, nullptr);
+    const int nk = frames ? (n < kFrameKernels ? n : kFrameKernels) : kPtKernels;
+    std::vector<hipEvent_t> marks((size_t)iters * 2 * kFrameKernels, nullptr);
     int rc = RT_OK;
-    for (auto& m : marks)
-        if (hipEventCreate(&m) != hipSuccess) { rc = RT_ERR_HIP; ctx->err = "hipEventCreate failed"; break; }
-    for (int k = 0; k < kPtKernels; ++k) kernel_ms[k] = 0.0f;
+    for (size_t i = 0; i < marks.size(); ++i) {
+        if ((int)(i % (2 * kFrameKernels)) / 2 >= nk) continue;  // kernels the caller does not ask for
+        if (hipEventCreate(&marks[i]) != hipSuccess) { rc = RT_ERR_HIP; ctx->err = "hipEventCreate failed"; break; }
+    }
+    for (int k = 0; k < n; ++k) kernel_ms[k] = k < nk ? 0.0f : -1.0f;
     for (int i = 0; i < iters && rc == RT_OK; ++i) {
         const int f = first_frame + i;
         if (frames) rc = rt_build_bvh(ctx);
-        ctx->ptMarks = marks.data() + (size_t)i * 2 * kPtKernels;
+        ctx->ptMarks = marks.data() + (size_t)i * 2 * kFrameKernels;
         if (rc == RT_OK) rc = rt_path_trace(ctx, f, 0);
         ctx->ptMarks = nullptr;
         if (rc == RT_OK && frames) rc = rt_denoise_post(ctx, f, 0);
-        if (rc == RT_OK && !frames && hipEventSynchronize(marks[(size_t)i * 2 * kPtKernels + 2 * kPtKernels - 1]) != hipSuccess)
+        ctx->dnMarks = nullptr;
+        if (rc == RT_OK && !frames && hipEventSynchronize(marks[(size_t)i * 2 * kFrameKernels + 2 * kPtKernels - 1]) != hipSuccess)
             rc = RT_ERR_HIP;
     }
     if (rc == RT_OK) rc = sync_streams(ctx);
+    std::vector<int> cnt(nk, 0);
     for (int i = 0; i < iters && rc == RT_OK; ++i)
-        for (int k = 0; k < kPtKernels && rc == RT_OK; ++k) {
+        for (int k = 0; k < nk && rc == RT_OK; ++k) {
             float ms = 0.0f;
-            hipEvent_t* m = marks.data() + (size_t)i * 2 * kPtKernels;
+            hipEvent_t* m = marks.data() + (size_t)i * 2 * kFrameKernels;
             if (hipEventElapsedTime(&ms, m[2 * k], m[2 * k + 1]) != hipSuccess) { rc = RT_ERR_HIP; ctx->err = "HIP event timing failed"; }
-            kernel_ms[k] += ms / (float)iters;
+            if (k < kPtKernels || ms > 0.0f) {
+                kernel_ms[k] += ms;
+                ++cnt[k];
+            }
         }
+    for (int k = 0; k < nk; ++k) kernel_ms[k] = cnt[k] ? kernel_ms[k] / (float)cnt[k] : 0.0f;
     for (auto& m : marks)
         if (m) (void)hipEventDestroy(m);
     return rc;
@@ -761,10 +772,11 @@ int rt_time_frame_kernels(rt_context* ctx, int first_frame, int iters, float* ke
 }
 
 int rt_frame_marks_begin(rt_context* ctx, int frames, uint32_t kernel_mask) {
-    if (!ctx || frames < 0 || frames > 100000 || (kernel_mask & ~((1u << kPtKernels) - 1u)) != 0) return RT_ERR_ARG;
+    if (!ctx || frames < 0 || frames > 100000 || (kernel_mask & ~((1u << kFrameKernels) - 1u)) != 0) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_frame_marks_begin before rt_init"; return RT_ERR_STATE; }
     if (int rc = sync_streams(ctx)) return rc;  // the events of earlier frames are complete
-    const size_t need = (size_t)frames * 2 * kPtKernels;
+    ctx->dnMarks = nullptr;
+    const size_t need = (size_t)frames * 2 * kFrameKernels;
     while (ctx->markPool.size() < need) {
         hipEvent_t e = nullptr;
         HIP_TRY(ctx, hipEventCreate(&e));
@@ -772,7 +784,7 @@ int rt_frame_marks_begin(rt_context* ctx, int frames, uint32_t kernel_mask) {
     }
     ctx->markRing.assign(need, nullptr);  // unmarked kernels keep null entries (no event recorded)
     for (size_t i = 0; i < need; ++i)
-        if (kernel_mask & (1u << ((i % (2 * kPtKernels)) / 2))) ctx->markRing[i] = ctx->markPool[i];
+        if (kernel_mask & (1u << ((i % (2 * kFrameKernels)) / 2))) ctx->markRing[i] = ctx->markPool[i];
     ctx->markMask = kernel_mask;
     ctx->markFrames = frames;
     ctx->markNext = 0;
@@ -783,19 +795,27 @@ int rt_frame_marks_read(rt_context* ctx, float* kernel_ms, int n, int* frames_re
     if (!ctx || !kernel_ms || n < kPtKernels) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_frame_marks_read before rt_init"; return RT_ERR_STATE; }
     if (int rc = sync_streams(ctx)) return rc;
-    const int frames = ctx->markNext;
-    for (int k = 0; k < kPtKernels; ++k) kernel_ms[k] = (ctx->markMask & (1u << k)) ? 0.0f : -1.0f;
-    for (int i = 0; i < frames; ++i)
-        for (int k = 0; k < kPtKernels; ++k) {
-            if (!(ctx->markMask & (1u << k))) continue;
-            const hipEvent_t* m = ctx->markRing.data() + (size_t)i * 2 * kPtKernels;
+    const int frames = ctx->markNext, nk = n < kFrameKernels ? n : kFrameKernels;
+    for (int k = 0; k < nk; ++k) {
+        kernel_ms[k] = -1.0f;
+        if (!(ctx->markMask & (1u << k))) continue;
+        float sum = 0.0f;
+        int cnt = 0;
+        for (int i = 0; i < frames; ++i) {
+            const hipEvent_t* m = ctx->markRing.data() + (size_t)i * 2 * kFrameKernels;
             float ms = 0.0f;
             HIP_TRY(ctx, hipEventElapsedTime(&ms, m[2 * k], m[2 * k + 1]));
-            kernel_ms[k] += ms / (float)frames;
+            if (k < kPtKernels || ms > 0.0f) {  // a denoise kernel the frame did not launch reads 0
+                sum += ms;
+                ++cnt;
+            }
         }
+        kernel_ms[k] = cnt ? sum / (float)cnt : 0.0f;
+    }
     if (frames_recorded) *frames_recorded = frames;
     ctx->markFrames = 0;
     ctx->markNext = 0;
+    ctx->dnMarks = nullptr;
     return RT_OK;
 }
 

@@ -119,13 +119,17 @@ struct FrameResources {
     bool histValid = false;
     // denoise + post (denoising.cu, postprocessing.cu)
     uint2* colorB = nullptr;       // ping-pong partner of color
-    uint2* accum = nullptr;        // AccumulationColorBuffer
+    uint2* accum = nullptr;        // AccumulationColorBuffer (the latest)
+    uint2* accumAlt = nullptr;     // the list chain writes this one and swaps (null: in place only)
     uint2* histBuf[2] = {};        // HistoryColorBuffer pair: histBuf[histIdx] is the latest, TemporalFilter2
     int histIdx = 0;               // writes the other one, then they swap roles
     uint16_t* histDepth = nullptr; // HistoryDepthBuffer
     uint16_t* noise8 = nullptr;
     uint16_t* noise16 = nullptr;
     uint32_t* chainCounter = nullptr;  // k_downscale_chain's finished-workgroup count (re-armed by its last one)
+    uint32_t* tileList = nullptr;  // the noise-gated passes' active-tile lists (denoise.hip)
+    uint32_t tileCap = 0;
+    int tileParity = 0;            // counter set of the next list frame
     uint2* c4 = nullptr;
     uint2* c16 = nullptr;
     uint2* c64 = nullptr;
@@ -236,7 +240,9 @@ struct rt_context {
     bool shadeOnSide = false;
     DenoisePostParams postParams{};
     hipEvent_t* ptMarks = nullptr;  // set only inside rt_time_path_trace_kernels
-    // rt_frame_marks_begin: events around every path-trace kernel of the next markFrames path traces
+    hipEvent_t* dnMarks = nullptr;  // the denoise marks of the frame the last marked path trace traced
+    // rt_frame_marks_begin: events around the marked kernels of the next markFrames frames (path trace
+    // and denoise / post: 2 * kFrameKernels ring entries per frame)
     std::vector<hipEvent_t> markPool, markRing;  // ring: pool entries of the marked kernels, else null
     uint32_t markMask = 0;
     int markFrames = 0, markNext = 0;

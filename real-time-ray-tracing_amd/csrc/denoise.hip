@@ -133,6 +133,15 @@ RT_DEV F3 bicubic_smooth(const View2& im, F2 uv) {
     return smooth_sum(t, q);
 }
 
+// (dV - d) / sigma_depth of pass k (0 TemporalFilter, 1 SpatialFilter7x7, 2 the a-trous passes):
+// rt_div_rcp with the launch's reciprocal, the IEEE quotient for every depth difference (0 or
+// |a| >= 2^-24, half depths) when the host found sigma in its range; the division otherwise
+template <bool kRcp>
+RT_DEV float depth_ratio(const DenoisePostParams& P, int k, float a, float sigma) {
+    if (kRcp) return rt_div_rcp(a, sigma, P.rcpDepth[k]);
+    return a / sigma;
+}
+
 // 16-row tile row of this workgroup: launches may cover tile rows [P.ty0, P.ty1) only
 RT_DEV int tile_y(const DenoisePostParams& P) { return (int)blockIdx.y + P.ty0; }
 
@@ -148,7 +157,7 @@ RT_DEV T tree_sum32(T v) {
 // one per 8x8 tile, with k_tile_noise's lane layout and shuffle-tree order; thread 0 then
 // averages the four half-rounded tile values into the 16x16 noise level.  Reads outside the
 // image clamp to its edge, which always lands inside this workgroup's tile.
-RT_DEV void noise_epilogue(const DenoisePostParams& P, const uint2* sOut, uint16_t* sN8, int BX, int TY) {
+RT_DEV float noise_epilogue(const DenoisePostParams& P, const uint2* sOut, uint16_t* sN8, int BX, int TY) {
     const int W = (int)P.W, H = (int)P.H;
     const int W8 = (W + 7) / 8, H8 = (H + 7) / 8, W16 = (W + 15) / 16, H16 = (H + 15) / 16;
     const int tid = threadIdx.x;
@@ -183,37 +192,102 @@ RT_DEV void noise_epilogue(const DenoisePostParams& P, const uint2* sOut, uint16
         }
     }
     __syncthreads();
+    float n16 = 0.0f;
     if (tid == 0 && BX < W16 && TY < H16) {
         // n8.at(2x + i, 2y + j) clamped to the tile grid: tile i/j falls back to 0 past its edge
         const int i1 = 2 * BX + 1 < W8 ? 1 : 0, j1 = 2 * TY + 1 < H8 ? 2 : 0;
         const float v1 = h2f(sN8[0]), v2 = h2f(sN8[i1]), v3 = h2f(sN8[j1]), v4 = h2f(sN8[i1 + j1]);
-        P.noise16[TY * W16 + BX] = (uint16_t)f2h((v1 + v2 + v3 + v4) / 4);
+        const uint16_t h = (uint16_t)f2h((v1 + v2 + v3 + v4) / 4);
+        P.noise16[TY * W16 + BX] = h;
+        n16 = h2f(h);
     }
+    return n16;  // thread 0: the tile's 16x16 noise level as the passes after it read it
+}
+
+// ---- Active-tile lists (the whole-frame chain).  The noise-gated passes
+// (SpatialFilter7x7 against noise_threshold_local, the a-trous passes against _large) leave a tile
+// below its threshold unchanged, so instead of every pass copying those tiles through its ping-pong
+// buffer: TemporalFilter's epilogue sorts each tile by the noise level it just computed — a tile
+// above the local threshold goes to list 0 (SpatialFilter7x7 runs only on those), the others write
+// their TemporalFilter output straight into this frame's accumulation buffer (SpatialFilter7x7's copy
+// of them; the chain alternates two accumulation buffers, since TemporalFilter reads the previous
+// frame's) and go to list 1 if they are above the large threshold; SpatialFilter7x7's epilogue puts its tiles
+// above the large threshold on list 1.  The first two a-trous passes run only on list 1; the taps of
+// the second and third pass that land in a tile off the list read the accumulation buffer (the
+// value every copy would have carried), and the third pass, which also applies the albedo, covers
+// every tile.
+//
+// Layout of P.tileList: counters [parity][list][16 partitions] 32 words (128 B) apart (a tile goes
+// to partition tile % 16: one device-scope counter per workgroup would serialise), then the entries
+// [list][partition][tileCap / 16 + 1].  Each frame appends under its parity and TemporalFilter
+// zeroes the other parity's counters, which the previous frame was the last to read.
+constexpr int kListParts = 16;
+RT_DEV uint32_t* list_counter(const DenoisePostParams& P, int parity, int list, int part) {
+    return P.tileList + ((parity * 2 + list) * kListParts + part) * 32;
+}
+RT_DEV uint32_t list_cap(const DenoisePostParams& P) { return P.tileCap / kListParts + 1; }
+RT_DEV uint32_t* list_entries(const DenoisePostParams& P, int list, int part) {
+    return P.tileList + 2 * 2 * kListParts * 32 + (list * kListParts + part) * list_cap(P);
+}
+RT_DEV void list_append(const DenoisePostParams& P, int list, uint32_t tile) {
+    const int part = (int)(tile % kListParts);
+    const uint32_t i = atomicAdd(list_counter(P, P.tileParity, list, part), 1u);
+    list_entries(P, list, part)[i] = tile;
+}
+// The list kernels launch one workgroup per list slot (16 partitions x (tileCap / 16 + 1), the list's
+// capacity): workgroup b takes entry b / 16 of partition b % 16 and leaves at once past that
+// partition's count.  A persistent grid walking the list instead held the tap arithmetic's uniform
+// values across its loop: 106 SGPRs with spills into VGPR lanes, 145-149 VGPRs against the one-tile
+// kernels' 126-129.
+RT_DEV bool list_tile(const DenoisePostParams& P, int list, uint32_t& tile) {
+    const uint32_t part = blockIdx.x % kListParts, j = blockIdx.x / kListParts;
+    if (j >= *list_counter(P, P.tileParity, list, (int)part)) return false;
+    tile = list_entries(P, list, (int)part)[j];
+    return true;
 }
 
 // ------------------------------------------------------------------ TemporalFilter
+template <bool kRcp>
 RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, int y);
 
-// kNoise: also the tile noise levels of the output (noise_epilogue)
-template <bool kNoise>
+// kNoise: also the tile noise levels of the output (noise_epilogue); kList: and the tile's place on
+// the active-tile lists (above), with the output of a tile SpatialFilter7x7 leaves unchanged also
+// written to this frame's accumulation buffer (P.accumAlt: P.accum, the previous frame's, is read
+// at reprojected positions by every workgroup); kRcp: the depth weight's division by reciprocal
+template <bool kNoise, bool kList, bool kRcp>
 __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uint2* in, uint2* out) {
     DN_PRIO();
     __shared__ uint2 sOut[kNoise ? 256 : 1];
     __shared__ uint16_t sN8[4];
+    __shared__ int sCopy;
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     const int W = (int)P.W, H = (int)P.H;
+    if (kList && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2 * kListParts)  // the other parity's
+        *list_counter(P, P.tileParity ^ 1, (int)threadIdx.x / kListParts, (int)threadIdx.x % kListParts) = 0u;
     if (x < W && y < H) {
-        const uint2 res = temporal_pixel(P, in, x, y);
+        const uint2 res = temporal_pixel<kRcp>(P, in, x, y);
         out[(size_t)y * W + x] = res;
         if (kNoise) sOut[threadIdx.x] = res;
         if (P.histDepthInTemporal) P.histDepth[(size_t)y * W + x] = P.depth[(size_t)y * W + x];
     }
     if (kNoise) {
         __syncthreads();
-        noise_epilogue(P, sOut, sN8, (int)blockIdx.x, tile_y(P));
+        const float n16 = noise_epilogue(P, sOut, sN8, (int)blockIdx.x, tile_y(P));
+        if (kList) {
+            if (threadIdx.x == 0) {
+                const uint32_t tile = (uint32_t)(tile_y(P) * (int)((P.W + 15) / 16) + (int)blockIdx.x);
+                const bool act7 = !(n16 < P.dn.noise_threshold_local), act5 = !(n16 < P.dn.noise_threshold_large);
+                if (act7) list_append(P, 0, tile);
+                else if (act5) list_append(P, 1, tile);
+                sCopy = act7 ? 0 : 1;
+            }
+            __syncthreads();
+            if (sCopy && x < W && y < H) P.accumAlt[(size_t)y * W + x] = sOut[threadIdx.x];
+        }
     }
 }
 
+template <bool kRcp>
 RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, int y) {
     const int W = (int)P.W, H = (int)P.H;
     const View2 col{in, W, H}, nrm{P.normal, W, H}, acc{P.accum, (int)P.histW, (int)P.histH};
@@ -250,7 +324,7 @@ RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, 
             const F3 n = rgb_of(nq[j]);
             float w = 1.0f;
             w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.temporal_denoise_sigma_normal);
-            const float dd = (dV - d) / P.dn.temporal_denoise_sigma_depth;
+            const float dd = depth_ratio<kRcp>(P, 0, dV - d, P.dn.temporal_denoise_sigma_depth);
             w *= DN_EXP(-0.5f * dd * dd);
             w *= (mV != mask_of(q)) ? 1.0f / P.dn.temporal_denoise_sigma_material : 1.0f;
             w *= cG3[xo + yo * 3];
@@ -357,34 +431,34 @@ __global__ __launch_bounds__(256) void k_noise_visualize(DenoisePostParams P, ui
 
 // ------------------------------------------------------------------ SpatialFilter7x7
 // 16x16 tile + 3-pixel apron staged in LDS (22 x 22 entries of colour, normal, depth).
-struct Tap7 { uint2 c; uint2 n; float d; };
-
-template <int kParity>
+template <int kParity, bool kRcp>
 RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD, int tx,
                             int ty);
 
-template <bool kNoise>
-__global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uint2* in, uint2* out) {
-    DN_PRIO();
-    __shared__ uint2 sC[22 * 22];
-    __shared__ uint2 sN[22 * 22];
-    __shared__ float sD[22 * 22];
-    __shared__ uint2 sOut[kNoise ? 256 : 1];
-    __shared__ uint16_t sN8[4];
+struct S7Lds {
+    uint2 C[22 * 22];
+    uint2 N[22 * 22];
+    float D[22 * 22];
+    uint2 Out[256];
+    uint16_t N8[4];
+};
+
+// one 16x16 tile (BX, TY) of SpatialFilter7x7 into `out`: the apron staged (when filtered), the
+// pixel filtered or copied (gated), the result also kept in L.Out for a noise epilogue
+template <bool kRcp>
+RT_DEV void spatial7_tile(const DenoisePostParams& P, const uint2* in, uint2* out, S7Lds& L, int BX, int TY,
+                          bool gated, int lid) {
     const int W = (int)P.W, H = (int)P.H;
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    const int TY = tile_y(P);
-    const int x = blockIdx.x * 16 + tx, y = TY * 16 + ty;
-    const int W16 = (W + 15) / 16;
-    const bool gated = kDnGateAll || h2f(P.noise16[TY * W16 + blockIdx.x]) < P.dn.noise_threshold_local;
+    const int tx = lid & 15, ty = lid >> 4;
+    const int x = BX * 16 + tx, y = TY * 16 + ty;
     const View2 col{in, W, H}, nrm{P.normal, W, H};
     const View1 dep{P.depth, W, H};
     if (!gated) {
-        for (int i = threadIdx.x; i < 22 * 22; i += 256) {
-            const int lx = blockIdx.x * 16 - 3 + i % 22, ly = TY * 16 - 3 + i / 22;
-            sC[i] = col.at(lx, ly);
-            sN[i] = nrm.at(lx, ly);
-            sD[i] = dep.at(lx, ly);
+        for (int i = lid; i < 22 * 22; i += 256) {
+            const int lx = BX * 16 - 3 + i % 22, ly = TY * 16 - 3 + i / 22;
+            L.C[i] = col.at(lx, ly);
+            L.N[i] = nrm.at(lx, ly);
+            L.D[i] = dep.at(lx, ly);
         }
     }
     __syncthreads();
@@ -392,18 +466,44 @@ __global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uin
         const size_t p = (size_t)y * W + x;
         // the tap set alternates with the frame parity: both sets compiled with constant offsets
         const uint2 res = gated ? in[p]
-                          : (P.frameNum % 2 == 0 ? spatial7_pixel<0>(P, sC, sN, sD, tx, ty)
-                                                 : spatial7_pixel<1>(P, sC, sN, sD, tx, ty));
+                          : (P.frameNum % 2 == 0 ? spatial7_pixel<0, kRcp>(P, L.C, L.N, L.D, tx, ty)
+                                                 : spatial7_pixel<1, kRcp>(P, L.C, L.N, L.D, tx, ty));
         out[p] = res;
-        if (kNoise) sOut[threadIdx.x] = res;
-    }
-    if (kNoise) {
-        __syncthreads();
-        noise_epilogue(P, sOut, sN8, (int)blockIdx.x, tile_y(P));
+        L.Out[lid] = res;
     }
 }
 
-template <int kParity>
+template <bool kNoise, bool kRcp>
+__global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uint2* in, uint2* out) {
+    DN_PRIO();
+    __shared__ S7Lds L;
+    const int TY = tile_y(P), W16 = ((int)P.W + 15) / 16;
+    const bool gated = kDnGateAll || h2f(P.noise16[TY * W16 + blockIdx.x]) < P.dn.noise_threshold_local;
+    spatial7_tile<kRcp>(P, in, out, L, (int)blockIdx.x, TY, gated, (int)threadIdx.x);
+    if (kNoise) {
+        __syncthreads();
+        noise_epilogue(P, L.Out, L.N8, (int)blockIdx.x, TY);
+    }
+}
+
+// SpatialFilter7x7 over active-tile list 0 only (tile rows outside [ty0, ty1) are skipped), with the
+// noise epilogue, which puts tiles above the large threshold on list 1
+template <bool kRcp>
+__global__ __launch_bounds__(256) void k_spatial7_list(DenoisePostParams P, const uint2* in, uint2* out) {
+    DN_PRIO();
+    __shared__ S7Lds L;
+    const int W16 = ((int)P.W + 15) / 16;
+    uint32_t tile;
+    if (!list_tile(P, 0, tile)) return;
+    const int BX = (int)(tile % (uint32_t)W16), TY = (int)(tile / (uint32_t)W16);
+    if (TY < P.ty0 || TY >= P.ty1) return;
+    spatial7_tile<kRcp>(P, in, out, L, BX, TY, false, (int)threadIdx.x);
+    __syncthreads();
+    const float n16 = noise_epilogue(P, L.Out, L.N8, BX, TY);
+    if (threadIdx.x == 0 && !(n16 < P.dn.noise_threshold_large)) list_append(P, 1, tile);
+}
+
+template <int kParity, bool kRcp>
 RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD, int tx,
                             int ty) {
     const int ci = (tx + 3) + (ty + 3) * 22;
@@ -444,7 +544,7 @@ RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const u
                 if (isnan3(n)) n = f3(0.0f);
                 float w = 1.0f;
                 w *= DN_POW(fmaxf(dot(nV, n), 0.0001f), P.dn.local_denoise_sigma_normal);
-                const float dd = (dV - d) / P.dn.local_denoise_sigma_depth;
+                const float dd = depth_ratio<kRcp>(P, 1, dV - d, P.dn.local_denoise_sigma_depth);
                 w *= DN_EXP(-0.5f * dd * dd);
                 w *= (mV != mask_of(q)) ? 1.0f / P.dn.local_denoise_sigma_material : 1.0f;
                 w *= cG7[xo + yo * 7];
@@ -462,74 +562,122 @@ RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const u
 }
 
 // ------------------------------------------------------------------ SpatialFilterGlobal5x5<S>
-// kAlbedo: ApplyAlbedo (denoising.cu:160-171) fused into the store of the last wide pass
-template <int S, bool kAlbedo>
-__global__ DN5_BOUNDS void k_spatial5(DenoisePostParams P, const uint2* in, uint2* out) {
-    DN_PRIO();
+// Tiles of list 1 (above noise_threshold_large) around tile (TX, TY): bit (dy + 2) * 5 + (dx + 2)
+// for tile (TX + dx, TY + dy), |dx|, |dy| <= 2 (the reach of a stride-12 tap).  Every wave builds it
+// from its own lanes 0..24, so the value is wave-uniform without LDS or a barrier.
+RT_DEV uint32_t active_neighbourhood(const DenoisePostParams& P, int TX, int TY) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const int W16 = ((int)P.W + 15) / 16, H16 = ((int)P.H + 15) / 16;
+    const int tx = TX + lane % 5 - 2, ty = TY + lane / 5 - 2;
+    bool a = false;
+    if (lane < 25 && tx >= 0 && ty >= 0 && tx < W16 && ty < H16)
+        a = !(h2f(P.noise16[ty * W16 + tx]) < P.dn.noise_threshold_large);
+    return (uint32_t)__ballot(a);
+}
+
+// One pixel of SpatialFilterGlobal5x5<S> in a filtered tile (TX, TY).  kRedirect: `in` holds only
+// the list-1 tiles, so a tap whose (clamped) texel lies in a tile off the list (its bit clear in
+// `act`) reads `alt`, the accumulation buffer those tiles would have been copied from.
+template <int S, bool kRcp, bool kRedirect>
+RT_DEV uint2 spatial5_pixel(const DenoisePostParams& P, const uint2* in, const uint2* alt, uint32_t act, int x, int y,
+                            int TX, int TY) {
     const int W = (int)P.W, H = (int)P.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
-    if (x >= W || y >= H) return;
     const size_t p = (size_t)y * W + x;
-    const int W16 = (W + 15) / 16;
     const uint2 c0 = in[p];
     uint2 res = c0;
-    if (!kDnGateAll && !(h2f(P.noise16[tile_y(P) * W16 + blockIdx.x]) < P.dn.noise_threshold_large)) {
-        const View2 col{in, W, H}, nrm{P.normal, W, H};
-        const View1 dep{P.depth, W, H};
-        F3 nV = rgb_of(P.normal[p]);
-        F3 cV = rgb_of(c0);
-        const uint32_t mV = mask_of(c0);
-        float dV = h2f(P.depth[p]);
-        if (isnan3(cV)) cV = f3(0.0f);
-        if (dV != dV) dV = 0.0f;
-        if (isnan3(nV)) nV = f3(0.0f);
-        if (dV < 10e9f) {
-            F3 sum = f3(0.0f);
-            float sw = 0.0f;
-            // taps in batches of kDnBatch: a batch's loads are issued together, then its weights
-            // computed (the branches of rt_powf otherwise keep the compiler from hoisting the next
-            // tap's loads, one memory round trip per tap)
+    F3 nV = rgb_of(P.normal[p]);
+    F3 cV = rgb_of(c0);
+    const uint32_t mV = mask_of(c0);
+    float dV = h2f(P.depth[p]);
+    if (isnan3(cV)) cV = f3(0.0f);
+    if (dV != dV) dV = 0.0f;
+    if (isnan3(nV)) nV = f3(0.0f);
+    if (dV < 10e9f) {
+        F3 sum = f3(0.0f);
+        float sw = 0.0f;
+        // taps in batches of kDnBatch: a batch's loads are issued together, then its weights
+        // computed (the branches of rt_powf otherwise keep the compiler from hoisting the next
+        // tap's loads, one memory round trip per tap)
 #pragma unroll
-            for (int k0 = 0; k0 < 25; k0 += kDnBatch) {
-                uint2 qv[kDnBatch], nq[kDnBatch];
-                float dv[kDnBatch];
+        for (int k0 = 0; k0 < 25; k0 += kDnBatch) {
+            uint2 qv[kDnBatch], nq[kDnBatch];
+            float dv[kDnBatch];
 #pragma unroll
-                for (int m = 0; m < kDnBatch; ++m) {
-                    const int k = k0 + m < 25 ? k0 + m : 24;
-                    const int sx = x + (k % 5 - 2) * S, sy = y + (k / 5 - 2) * S;
-                    qv[m] = col.at(sx, sy);
-                    dv[m] = dep.at(sx, sy);
-                    nq[m] = nrm.at(sx, sy);
+            for (int m = 0; m < kDnBatch; ++m) {
+                const int k = k0 + m < 25 ? k0 + m : 24;
+                const int cx = clampi(x + (k % 5 - 2) * S, 0, W - 1), cy = clampi(y + (k / 5 - 2) * S, 0, H - 1);
+                const size_t q = (size_t)cy * W + cx;
+                const uint2* src = in;
+                if (kRedirect) {
+                    const int bit = ((cy >> 4) - TY + 2) * 5 + ((cx >> 4) - TX + 2);
+                    src = ((act >> bit) & 1u) ? in : alt;
                 }
-#pragma unroll
-                for (int m = 0; m < kDnBatch; ++m) {
-                    const int k = k0 + m;
-                    if (k >= 25) break;
-                    const int i = k % 5, j = k / 5;
-                    const uint2 q = qv[m];
-                    F3 cc = rgb_of(q);
-                    const float d = dv[m];
-                    const F3 n = rgb_of(nq[m]);
-                    float w = 1.0f;
-                    w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.large_denoise_sigma_normal);
-                    const float dd = (dV - d) / P.dn.large_denoise_sigma_depth;
-                    w *= DN_EXP(-0.5f * dd * dd);
-                    w *= (mV != mask_of(q)) ? 1.0f / P.dn.large_denoise_sigma_material : 1.0f;
-                    w *= cG5[i + j * 5];
-                    if (isnan3(cc)) { cc = f3(0.0f); w = 0.0f; }
-                    sum = sum + cc * w;
-                    sw += w;
-                }
+                qv[m] = src[q];
+                dv[m] = h2f(P.depth[q]);
+                nq[m] = P.normal[q];
             }
-            if (isnan3(sum)) sum = f3(0.0f);
-            if (sw != sw) sw = 0.0f;
-            F3 fin = sw == 0 ? f3(0.0f) : sum / sw;
-            if (isnan3(fin)) fin = f3(0.0f);
-            res = pack_color(fin, mV);
+#pragma unroll
+            for (int m = 0; m < kDnBatch; ++m) {
+                const int k = k0 + m;
+                if (k >= 25) break;
+                const int i = k % 5, j = k / 5;
+                const uint2 q = qv[m];
+                F3 cc = rgb_of(q);
+                const float d = dv[m];
+                const F3 n = rgb_of(nq[m]);
+                float w = 1.0f;
+                w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.large_denoise_sigma_normal);
+                const float dd = depth_ratio<kRcp>(P, 2, dV - d, P.dn.large_denoise_sigma_depth);
+                w *= DN_EXP(-0.5f * dd * dd);
+                w *= (mV != mask_of(q)) ? 1.0f / P.dn.large_denoise_sigma_material : 1.0f;
+                w *= cG5[i + j * 5];
+                if (isnan3(cc)) { cc = f3(0.0f); w = 0.0f; }
+                sum = sum + cc * w;
+                sw += w;
+            }
         }
+        if (isnan3(sum)) sum = f3(0.0f);
+        if (sw != sw) sw = 0.0f;
+        F3 fin = sw == 0 ? f3(0.0f) : sum / sw;
+        if (isnan3(fin)) fin = f3(0.0f);
+        res = pack_color(fin, mV);
     }
+    return res;
+}
+
+// every tile of the launch's rows: tiles below the large threshold pass their input through (from
+// `alt` when kRedirect: `in` holds only the list-1 tiles); kAlbedo: ApplyAlbedo (denoising.cu:160-171)
+// fused into the store of the last wide pass
+template <int S, bool kAlbedo, bool kRcp, bool kRedirect>
+__global__ DN5_BOUNDS void k_spatial5(DenoisePostParams P, const uint2* in, uint2* out, const uint2* alt) {
+    DN_PRIO();
+    const int W = (int)P.W, H = (int)P.H;
+    const int TX = (int)blockIdx.x, TY = tile_y(P);
+    const int x = TX * 16 + (threadIdx.x & 15), y = TY * 16 + (threadIdx.x >> 4);
+    const int W16 = (W + 15) / 16;
+    const bool active = !kDnGateAll && !(h2f(P.noise16[TY * W16 + TX]) < P.dn.noise_threshold_large);
+    uint32_t act = 0u;
+    if (kRedirect && active) act = active_neighbourhood(P, TX, TY);  // before any lane leaves
+    if (x >= W || y >= H) return;
+    const size_t p = (size_t)y * W + x;
+    uint2 res = active ? spatial5_pixel<S, kRcp, kRedirect>(P, in, alt, act, x, y, TX, TY) : (kRedirect ? alt : in)[p];
     if (kAlbedo) res = pack_color(rgb_of(res) * rgb_of(P.albedo[p]), 0x3C00u);  // w = half(1.0)
     out[p] = res;
+}
+
+// SpatialFilterGlobal5x5<S> over active-tile list 1 only (tile rows outside [ty0, ty1) are skipped):
+// `out` is written in those tiles only
+template <int S, bool kRcp, bool kRedirect>
+__global__ DN5_BOUNDS void k_spatial5_list(DenoisePostParams P, const uint2* in, uint2* out, const uint2* alt) {
+    DN_PRIO();
+    const int W = (int)P.W, H = (int)P.H, W16 = (W + 15) / 16;
+    uint32_t tile;
+    if (!list_tile(P, 1, tile)) return;
+    const int TX = (int)(tile % (uint32_t)W16), TY = (int)(tile / (uint32_t)W16);
+    if (TY < P.ty0 || TY >= P.ty1) return;
+    const uint32_t act = kRedirect ? active_neighbourhood(P, TX, TY) : 0u;
+    const int x = TX * 16 + (threadIdx.x & 15), y = TY * 16 + (threadIdx.x >> 4);
+    if (x < W && y < H) out[(size_t)y * W + x] = spatial5_pixel<S, kRcp, kRedirect>(P, in, alt, act, x, y, TX, TY);
 }
 
 // ------------------------------------------------------------------ ApplyAlbedo (in place, pointwise)
@@ -539,80 +687,6 @@ __global__ __launch_bounds__(256) void k_apply_albedo(DenoisePostParams P, const
     const F3 c = rgb_of(in[p]);
     const F3 a = rgb_of(P.albedo[p]);
     out[p] = pack_color(c * a, 0x3C00u);  // w = half(1.0)
-}
-
-// ------------------------------------------------------------------ TemporalFilter2
-__global__ __launch_bounds__(256) void k_temporal2(DenoisePostParams P, const uint2* in, uint2* out) {
-    DN_PRIO();
-    const int W = (int)P.W, H = (int)P.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
-    if (x >= W || y >= H) return;
-    const size_t p = (size_t)y * W + x;
-    const View2 col{in, W, H}, hc{P.histColor, (int)P.histW, (int)P.histH};
-    // Loads in two batches — the 3x3 neighbourhood with the motion vector, then the history texels
-    // it points at — and the reference's early-outs (history off screen, every history texel of
-    // another material) as one select of the output.  Written as branches, the compiler split each
-    // neighbour load into a mask read and a dependent colour read and sank the history reads below
-    // the discard test: ~13 dependent round trips per pixel instead of 2.
-    uint2 qs[9];
-#pragma unroll
-    for (int j = 0; j < 9; ++j) qs[j] = col.at(x + j % 3 - 1, y + j / 3 - 1);  // qs[4]: the pixel
-    const uint32_t mvq = P.motion[p];
-    const F2 mv = {h2f(mvq & 0xFFFFu) - 0.5f, h2f(mvq >> 16) - 0.5f};
-    const F2 inv = {1.0f / (float)W, 1.0f / (float)H};
-    const F2 uv = {((float)x + 0.5f) * inv.x, ((float)y + 0.5f) * inv.y};
-    const F2 huv = {uv.x + mv.x, uv.y + mv.y};
-    const bool onScreen = !(huv.x < 0 || huv.y < 0 || huv.x > 1.0f || huv.y > 1.0f);
-    const SmoothTaps ht = smooth_taps(hc, huv);  // clamped reads: safe off screen too
-    const int hx = (int)floorf(huv.x * (float)hc.W), hy = (int)floorf(huv.y * (float)hc.H);
-    uint2 hq[4];
-    uint32_t hm[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        hq[i] = hc.at(ht.t0x + (i & 1), ht.t0y + (i >> 1));
-        hm[i] = mask_of(hc.at(hx + i % 2, hy + i / 2));
-    }
-    const uint2 c0 = qs[4];
-    const F3 cV = ycocg_inv(ycocg(rgb_of(c0)));
-    const int mV = (int)mask_of(c0);
-    const float FLTMIN = 1.17549435e-38f, FLTMAX = 3.402823466e+38f;
-    F3 nMax = f3(FLTMIN), nMin = f3(FLTMAX), nMax2 = f3(FLTMIN), nMin2 = f3(FLTMAX);
-#pragma unroll
-    for (int j = 0; j < 9; ++j) {
-        const int xo = j % 3, yo = j / 3;
-        const bool same = (int)mask_of(qs[j]) == mV;
-        const F3 cc = ycocg(rgb_of(qs[j]));
-        nMax = same ? fmax3(nMax, cc) : nMax;
-        nMin = same ? fmin3(nMin, cc) : nMin;
-        if (abs(xo - 1) + abs(yo - 1) <= 1) {
-            nMax2 = same ? fmax3(nMax2, cc) : nMax2;
-            nMin2 = same ? fmin3(nMin2, cc) : nMin2;
-        }
-    }
-    nMax = (nMax + nMax2) / 2.0f;
-    nMin = (nMin + nMin2) / 2.0f;
-    F3 cH = smooth_sum(ht, hq);
-    const F3 cHy = clamp3(ycocg(cH), nMin, nMax);
-    cH = ycocg_inv(cHy);
-    const float lumaMin = nMin.x, lumaMax = nMax.x, lumaC = ycocg(cV).x;
-    float discard = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) discard += (mV != (int)hm[i]) ? 1.0f : 0.0f;
-    discard /= 4.0f;
-    cH = cH * (1.0f - discard) + cV * discard;
-    const float lumaH = ycocg(cH).x;
-    float blend = 3.0f / 4.0f;
-    blend *= 0.2f + 0.8f * clampf(0.5f * fminf(fabsf(lumaH - lumaMin), fabsf(lumaH - lumaMax)) /
-                                 fmaxf(fmaxf(lumaH, lumaC), 1e-4f));
-    float wA = blend * fmaxf(0.0001f, 1.0f / (lumaC + 4.0f));
-    float wB = (1.0f - blend) * fmaxf(0.0001f, 1.0f / (lumaH + 4.0f));
-    const float ws = safe_divide(1.0f, wA + wB);
-    wA *= ws;
-    wB *= ws;
-    F3 o = cV * wA + cH * wB;
-    if (isnan3(o)) o = f3(0.0f);
-    const uint2 blended = pack_color(o, (uint32_t)mV & 0xFFFFu);
-    out[p] = onScreen && discard != 1.0f ? blended : c0;
 }
 
 // ------------------------------------------------------------------ post
@@ -755,6 +829,102 @@ struct LdsLevel {  // clamped reads of an image level, of the block staged in LD
     }
 };
 
+// ------------------------------------------------------------------ TemporalFilter2
+RT_DEV uint2 temporal2_pixel(const DenoisePostParams& P, const uint2* in, int x, int y) {
+    const int W = (int)P.W, H = (int)P.H;
+    const size_t p = (size_t)y * W + x;
+    const View2 col{in, W, H}, hc{P.histColor, (int)P.histW, (int)P.histH};
+    // Loads in two batches — the 3x3 neighbourhood with the motion vector, then the history texels
+    // it points at — and the reference's early-outs (history off screen, every history texel of
+    // another material) as one select of the output.  Written as branches, the compiler split each
+    // neighbour load into a mask read and a dependent colour read and sank the history reads below
+    // the discard test: ~13 dependent round trips per pixel instead of 2.
+    uint2 qs[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) qs[j] = col.at(x + j % 3 - 1, y + j / 3 - 1);  // qs[4]: the pixel
+    const uint32_t mvq = P.motion[p];
+    const F2 mv = {h2f(mvq & 0xFFFFu) - 0.5f, h2f(mvq >> 16) - 0.5f};
+    const F2 inv = {1.0f / (float)W, 1.0f / (float)H};
+    const F2 uv = {((float)x + 0.5f) * inv.x, ((float)y + 0.5f) * inv.y};
+    const F2 huv = {uv.x + mv.x, uv.y + mv.y};
+    const bool onScreen = !(huv.x < 0 || huv.y < 0 || huv.x > 1.0f || huv.y > 1.0f);
+    const SmoothTaps ht = smooth_taps(hc, huv);  // clamped reads: safe off screen too
+    const int hx = (int)floorf(huv.x * (float)hc.W), hy = (int)floorf(huv.y * (float)hc.H);
+    uint2 hq[4];
+    uint32_t hm[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        hq[i] = hc.at(ht.t0x + (i & 1), ht.t0y + (i >> 1));
+        hm[i] = mask_of(hc.at(hx + i % 2, hy + i / 2));
+    }
+    const uint2 c0 = qs[4];
+    const F3 cV = ycocg_inv(ycocg(rgb_of(c0)));
+    const int mV = (int)mask_of(c0);
+    const float FLTMIN = 1.17549435e-38f, FLTMAX = 3.402823466e+38f;
+    F3 nMax = f3(FLTMIN), nMin = f3(FLTMAX), nMax2 = f3(FLTMIN), nMin2 = f3(FLTMAX);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        const int xo = j % 3, yo = j / 3;
+        const bool same = (int)mask_of(qs[j]) == mV;
+        const F3 cc = ycocg(rgb_of(qs[j]));
+        nMax = same ? fmax3(nMax, cc) : nMax;
+        nMin = same ? fmin3(nMin, cc) : nMin;
+        if (abs(xo - 1) + abs(yo - 1) <= 1) {
+            nMax2 = same ? fmax3(nMax2, cc) : nMax2;
+            nMin2 = same ? fmin3(nMin2, cc) : nMin2;
+        }
+    }
+    nMax = (nMax + nMax2) / 2.0f;
+    nMin = (nMin + nMin2) / 2.0f;
+    F3 cH = smooth_sum(ht, hq);
+    const F3 cHy = clamp3(ycocg(cH), nMin, nMax);
+    cH = ycocg_inv(cHy);
+    const float lumaMin = nMin.x, lumaMax = nMax.x, lumaC = ycocg(cV).x;
+    float discard = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) discard += (mV != (int)hm[i]) ? 1.0f : 0.0f;
+    discard /= 4.0f;
+    cH = cH * (1.0f - discard) + cV * discard;
+    const float lumaH = ycocg(cH).x;
+    float blend = 3.0f / 4.0f;
+    blend *= 0.2f + 0.8f * clampf(0.5f * fminf(fabsf(lumaH - lumaMin), fabsf(lumaH - lumaMax)) /
+                                 fmaxf(fmaxf(lumaH, lumaC), 1e-4f));
+    float wA = blend * fmaxf(0.0001f, 1.0f / (lumaC + 4.0f));
+    float wB = (1.0f - blend) * fmaxf(0.0001f, 1.0f / (lumaH + 4.0f));
+    const float ws = safe_divide(1.0f, wA + wB);
+    wA *= ws;
+    wB *= ws;
+    F3 o = cV * wA + cH * wB;
+    if (isnan3(o)) o = f3(0.0f);
+    const uint2 blended = pack_color(o, (uint32_t)mV & 0xFFFFu);
+    return onScreen && discard != 1.0f ? blended : c0;
+}
+
+// kDown: also DownScale4's first level of the tile (its 4 x 4 quarter texels, each a 4 x 4 box that
+// lies inside the 16 x 16 tile, clamped reads included), so the downscale chain starts from c4
+template <bool kDown>
+__global__ __launch_bounds__(256) void k_temporal2(DenoisePostParams P, const uint2* in, uint2* out) {
+    DN_PRIO();
+    __shared__ uint2 sT[kDown ? 256 : 1];
+    const int W = (int)P.W, H = (int)P.H;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
+    if (x < W && y < H) {
+        const uint2 r = temporal2_pixel(P, in, x, y);
+        out[(size_t)y * W + x] = r;
+        if (kDown) sT[threadIdx.x] = r;
+    }
+    if (kDown) {
+        __syncthreads();
+        const int t = (int)threadIdx.x, W4 = (W + 3) / 4, H4 = (H + 3) / 4;
+        const int ox = (int)blockIdx.x * 4 + (t & 3), oy = tile_y(P) * 4 + (t >> 2);
+        if (t < 16 && ox < W4 && oy < H4)
+            P.c4[oy * W4 + ox] = down4(LdsLevel{sT, W, H, (int)blockIdx.x * 16, tile_y(P) * 16, 16}, ox, oy);
+    }
+}
+
+
+// kFromC4: TemporalFilter2 already wrote the first level (k_temporal2<true>)
+template <bool kFromC4>
 __global__ __launch_bounds__(256) void k_downscale_chain(DenoisePostParams P, const uint2* in, uint32_t* counter) {
     DN_PRIO();
     __shared__ uint2 s4[16 * 16];
@@ -768,9 +938,13 @@ __global__ __launch_bounds__(256) void k_downscale_chain(DenoisePostParams P, co
     {
         const int ox = X * 16 + (t & 15), oy = Y * 16 + (t >> 4);
         if (ox < W4 && oy < H4) {
-            const uint2 v = down4(View2{in, W, H}, ox, oy);
-            s4[t] = v;
-            P.c4[oy * W4 + ox] = v;
+            if (kFromC4) {
+                s4[t] = P.c4[oy * W4 + ox];
+            } else {
+                const uint2 v = down4(View2{in, W, H}, ox, oy);
+                s4[t] = v;
+                P.c4[oy * W4 + ox] = v;
+            }
         }
     }
     __syncthreads();
@@ -1169,6 +1343,17 @@ __global__ __launch_bounds__(256) void k_hdr_out(const uint2* color, float4* hdr
         if (e__ != hipSuccess) return e__;      \
     } while (0)
 
+// HIP events around denoise kernel k (P->marks: bench.py's per-kernel split of whole frames)
+static hipError_t dn_mark(const DenoisePostParams* P, int k, int end, hipStream_t s) {
+    if (!P->marks || !P->marks[2 * k + end]) return hipSuccess;
+    return hipEventRecord(P->marks[2 * k + end], s);
+}
+#define DN_MARK(k, end)                                                 \
+    do {                                                                \
+        hipError_t e__ = dn_mark(P, (k), (end), s);                     \
+        if (e__ != hipSuccess) return e__;                              \
+    } while (0)
+
 // Tile rows of each pass.  The full frame computes every tile; a strip-local denoise (multi-GPU,
 // rows [rowA, rowB) in 64-row blocks) computes each pass only on the rows the passes after it
 // read for the strip: the stencil radii of the chain summed backwards from the strip — 3 rows for
@@ -1254,9 +1439,11 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         Q.ty0 = t0;
         Q.ty1 = t1;
         if (t1 > t0) {
+            DN_MARK(7, 0);
             hipLaunchKernelGGL(k_scale_post, dim3((Ws + 15) / 16, (unsigned)(t1 - t0)), dim3(kScaleThreads), 0, s, Q,
                                (const uint2*)cur);
             LAUNCH_CHECK();
+            DN_MARK(7, 1);
         }
         P->finalScaled = P->scaledB;
         return hipSuccess;
@@ -1285,6 +1472,18 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         return hipSuccess;
     };
     // ---- TemporalSpatialDenoising (denoising.cu:51-188)
+    // The whole chain with the tile noise levels computed in the passes' epilogues runs the
+    // noise-gated passes over active-tile lists (above); rcp: the depth weights' divisor of pass k
+    // as a reciprocal (DenoisePostParams::rcpDepthOk)
+    // TemporalFilter reads the previous frame's accumulation buffer at reprojected positions while
+    // it also writes tiles of this frame's, so the list chain writes the other buffer of a pair
+    // (accumAlt; the host swaps them) — not with a caller-bound buffer, nor a strip-local denoise
+    const bool useList = P->tileList && P->accumAlt && !P->stripLocal && P->temporal && P->frameNum != 1 &&
+                         P->localSpatial && P->wideSpatial && !P->visualize && !kDnGateAll;
+    uint2* const accOut = useList ? P->accumAlt : P->accum;
+    P->listUsed = useList ? 1 : 0;
+    const bool rcpT = (P->rcpDepthOk & 1) != 0, rcp7 = (P->rcpDepthOk & 2) != 0, rcp5 = (P->rcpDepthOk & 4) != 0;
+    const dim3 gList((unsigned)(kListParts * (P->tileCap / kListParts + 1)));  // one workgroup per list slot
     bool noise1 = false, histDepthDone = false;
     if (P->temporal && P->frameNum != 1) {
         noise1 = P->localSpatial && !P->visualize;
@@ -1293,9 +1492,19 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
             // the whole frame without the debug outlines (which rewrite depth): TemporalFilter2's
             // HistoryDepthBuffer copy rides on this pass's depth reads
             Q.histDepthInTemporal = histDepthDone = P->temporal2 && !P->stripLocal && !P->visualize;
-            if (noise1) hipLaunchKernelGGL(k_temporal<true>, g, b256, 0, s, Q, (const uint2*)cur, dst);
-            else hipLaunchKernelGGL(k_temporal<false>, g, b256, 0, s, Q, (const uint2*)cur, dst);
+            DN_MARK(0, 0);
+            if (useList) {
+                if (rcpT) hipLaunchKernelGGL((k_temporal<true, true, true>), g, b256, 0, s, Q, (const uint2*)cur, dst);
+                else hipLaunchKernelGGL((k_temporal<true, true, false>), g, b256, 0, s, Q, (const uint2*)cur, dst);
+            } else if (noise1) {
+                if (rcpT) hipLaunchKernelGGL((k_temporal<true, false, true>), g, b256, 0, s, Q, (const uint2*)cur, dst);
+                else hipLaunchKernelGGL((k_temporal<true, false, false>), g, b256, 0, s, Q, (const uint2*)cur, dst);
+            } else {
+                if (rcpT) hipLaunchKernelGGL((k_temporal<false, false, true>), g, b256, 0, s, Q, (const uint2*)cur, dst);
+                else hipLaunchKernelGGL((k_temporal<false, false, false>), g, b256, 0, s, Q, (const uint2*)cur, dst);
+            }
             LAUNCH_CHECK();
+            DN_MARK(0, 1);
         }
         next_from(dst);
     }
@@ -1303,14 +1512,21 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
     if (P->localSpatial) {
         if (!noise1 && (e = noise(1)) != hipSuccess) return e;
         noise2 = P->wideSpatial && !P->visualize;
-        uint2* dst = P->temporal ? P->accum : spare;
+        uint2* dst = P->temporal ? accOut : spare;
         if (tiles(3, Q, g)) {
-            if (noise2) {
-                hipLaunchKernelGGL(k_spatial7<true>, g, b256, 0, s, Q, (const uint2*)cur, dst);
+            DN_MARK(1, 0);
+            if (useList) {  // list 0 only; TemporalFilter wrote the other tiles into the accumulation buffer
+                if (rcp7) hipLaunchKernelGGL(k_spatial7_list<true>, gList, b256, 0, s, Q, (const uint2*)cur, dst);
+                else hipLaunchKernelGGL(k_spatial7_list<false>, gList, b256, 0, s, Q, (const uint2*)cur, dst);
+            } else if (noise2) {
+                if (rcp7) hipLaunchKernelGGL((k_spatial7<true, true>), g, b256, 0, s, Q, (const uint2*)cur, dst);
+                else hipLaunchKernelGGL((k_spatial7<true, false>), g, b256, 0, s, Q, (const uint2*)cur, dst);
             } else {
-                hipLaunchKernelGGL(k_spatial7<false>, g, b256, 0, s, Q, (const uint2*)cur, dst);
+                if (rcp7) hipLaunchKernelGGL((k_spatial7<false, true>), g, b256, 0, s, Q, (const uint2*)cur, dst);
+                else hipLaunchKernelGGL((k_spatial7<false, false>), g, b256, 0, s, Q, (const uint2*)cur, dst);
             }
             LAUNCH_CHECK();
+            DN_MARK(1, 1);
         }
         next_from(dst);
     } else if (P->temporal) {
@@ -1322,21 +1538,48 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
             next_from(spare);
         }
         if (!noise2 && (e = noise(2)) != hipSuccess) return e;
-        // a: a colour buffer other than the one being read; b: the other colour buffer
+        // a: a colour buffer other than the one being read; b: the other colour buffer.  With the
+        // lists the first pass reads the accumulation buffer (cur) and every pass's taps outside
+        // list 1 read it too (alt)
         uint2* a = cur == P->colorA ? P->colorB : cur == P->colorB ? P->colorA : spare;
         uint2* b = a == P->colorA ? P->colorB : P->colorA;
+        const uint2* alt = cur;
         if (tiles(3, Q, g)) {
-            hipLaunchKernelGGL((k_spatial5<3, false>), g, b256, 0, s, Q, (const uint2*)cur, a);
+            DN_MARK(2, 0);
+            if (useList) {
+                if (rcp5) hipLaunchKernelGGL((k_spatial5_list<3, true, false>), gList, b256, 0, s, Q, (const uint2*)cur, a, alt);
+                else hipLaunchKernelGGL((k_spatial5_list<3, false, false>), gList, b256, 0, s, Q, (const uint2*)cur, a, alt);
+            } else {
+                if (rcp5) hipLaunchKernelGGL((k_spatial5<3, false, true, false>), g, b256, 0, s, Q, (const uint2*)cur, a, alt);
+                else hipLaunchKernelGGL((k_spatial5<3, false, false, false>), g, b256, 0, s, Q, (const uint2*)cur, a, alt);
+            }
             LAUNCH_CHECK();
+            DN_MARK(2, 1);
         }
 #if !(defined(RTX_DN_ABL) && RTX_DN_ABL == 1)  // timing ablation only: two a-trous passes fewer
         if (tiles(2, Q, g)) {
-            hipLaunchKernelGGL((k_spatial5<6, false>), g, b256, 0, s, Q, (const uint2*)a, b);
+            DN_MARK(3, 0);
+            if (useList) {
+                if (rcp5) hipLaunchKernelGGL((k_spatial5_list<6, true, true>), gList, b256, 0, s, Q, (const uint2*)a, b, alt);
+                else hipLaunchKernelGGL((k_spatial5_list<6, false, true>), gList, b256, 0, s, Q, (const uint2*)a, b, alt);
+            } else {
+                if (rcp5) hipLaunchKernelGGL((k_spatial5<6, false, true, false>), g, b256, 0, s, Q, (const uint2*)a, b, alt);
+                else hipLaunchKernelGGL((k_spatial5<6, false, false, false>), g, b256, 0, s, Q, (const uint2*)a, b, alt);
+            }
             LAUNCH_CHECK();
+            DN_MARK(3, 1);
         }
         if (tiles(1, Q, g)) {
-            hipLaunchKernelGGL((k_spatial5<12, true>), g, b256, 0, s, Q, (const uint2*)b, a);
+            DN_MARK(4, 0);
+            if (useList) {
+                if (rcp5) hipLaunchKernelGGL((k_spatial5<12, true, true, true>), g, b256, 0, s, Q, (const uint2*)b, a, alt);
+                else hipLaunchKernelGGL((k_spatial5<12, true, false, true>), g, b256, 0, s, Q, (const uint2*)b, a, alt);
+            } else {
+                if (rcp5) hipLaunchKernelGGL((k_spatial5<12, true, true, false>), g, b256, 0, s, Q, (const uint2*)b, a, alt);
+                else hipLaunchKernelGGL((k_spatial5<12, true, false, false>), g, b256, 0, s, Q, (const uint2*)b, a, alt);
+            }
             LAUNCH_CHECK();
+            DN_MARK(4, 1);
         }
 #endif
         cur = a;
@@ -1377,11 +1620,19 @@ static hipError_t denoise_phase3(DenoisePostParams* P, hipStream_t s) {
     dim3 g;
     uint2* cur = P->svgfOut;
     const bool histDepthDone = P->histDepthDone != 0;
+    // the whole frame with every post pass on runs DownScale4 x 3 + Histogram2 + AutoExposure as
+    // k_downscale_chain; TemporalFilter2 then also writes the first DownScale4 level
+    const bool chain = P->postProcess && P->downScale && P->histogramOn && !P->stripLocal;
+    bool down = false;
     if (P->temporal2) {
+        down = chain && P->frameNum != 1;
         if (P->frameNum != 1) {
             if (tiles(1, Q, g)) {
-                hipLaunchKernelGGL(k_temporal2, g, b256, 0, s, Q, (const uint2*)cur, P->histColorOut);
+                DN_MARK(5, 0);
+                if (down) hipLaunchKernelGGL(k_temporal2<true>, g, b256, 0, s, Q, (const uint2*)cur, P->histColorOut);
+                else hipLaunchKernelGGL(k_temporal2<false>, g, b256, 0, s, Q, (const uint2*)cur, P->histColorOut);
                 LAUNCH_CHECK();
+                DN_MARK(5, 1);
             }
         } else if ((e = hipMemcpyAsync(P->histColorOut, cur, Pn * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) {
             return e;
@@ -1398,11 +1649,14 @@ static hipError_t denoise_phase3(DenoisePostParams* P, hipStream_t s) {
     }
     // ---- PostProcessing (postprocessing.cu:5-161) up to the histogram: the DownScale4 chain and
     // the histogram over this context's rows (64-row aligned strips keep each level's texels local)
-    if (P->postProcess && P->downScale && P->histogramOn && !P->stripLocal) {
+    if (chain) {
         // the whole frame with every pass on: the three DownScale4 levels, Histogram2 and
         // AutoExposure in one launch
-        hipLaunchKernelGGL(k_downscale_chain, dim3(W64, H64), b256, 0, s, *P, (const uint2*)cur, P->chainCounter);
+        DN_MARK(6, 0);
+        if (down) hipLaunchKernelGGL(k_downscale_chain<true>, dim3(W64, H64), b256, 0, s, *P, (const uint2*)cur, P->chainCounter);
+        else hipLaunchKernelGGL(k_downscale_chain<false>, dim3(W64, H64), b256, 0, s, *P, (const uint2*)cur, P->chainCounter);
         LAUNCH_CHECK();
+        DN_MARK(6, 1);
         P->exposureDone = 1;
     } else if (P->postProcess) {
         const int ra = P->stripLocal ? (int)P->rowA : 0, rb = P->stripLocal ? (int)P->rowB : H;

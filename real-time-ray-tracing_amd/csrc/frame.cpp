@@ -230,7 +230,18 @@ int run_denoise(rt_context* ctx, DenoisePostParams& p, hipStream_t s) {
         ctx->err = "collective hook failed (G-buffers)";
         return RT_ERR_STATE;
     }
+    if (p.marks)  // every marked pair recorded once up front: a kernel this frame does not launch reads 0 ms
+        for (int k = 0; k < 2 * kDnKernels; ++k)
+            if (p.marks[k]) HIP_TRY(ctx, hipEventRecord(p.marks[k], s));
+    // taken when the denoise is issued (a deferred one runs after the earlier frames' swaps)
+    p.tileParity = ctx->fr.tileParity;
+    p.accum = ctx->fr.accum;
+    p.accumAlt = ctx->fr.accumAlt;
     HIP_TRY(ctx, rtk_denoise_phase(&p, s, 0));
+    if (p.listUsed) {  // the list chain wrote the other accumulation buffer; the next list frame
+        ctx->fr.tileParity ^= 1;  // appends under the other counters
+        std::swap(ctx->fr.accum, ctx->fr.accumAlt);
+    }
     // the histogram is recomputed only with the post chain on; summing a stale one again would
     // multiply it by the rank count every frame
     if (p.stripLocal && p.postProcess && ctx->hook(ctx->hookArg, RT_HOOK_HISTOGRAM, (void*)s, &x) != 0) {
@@ -472,6 +483,7 @@ int rt_frame_init(rt_context* ctx) {
     }
     ALLOC(fr.colorB, P * 8);
     ALLOC(fr.accum, P * 8);
+    ALLOC(fr.accumAlt, P * 8);  // the list chain's other accumulation buffer (denoise.hip active-tile lists)
     ALLOC(fr.histBuf[0], P * 8);
     ALLOC(fr.histBuf[1], P * 8);
     ALLOC(fr.histDepth, P * 2);
@@ -481,6 +493,12 @@ int rt_frame_init(rt_context* ctx) {
     ALLOC(fr.noise16, ((W + 15) / 16) * ((H + 15) / 16) * 2);
     ALLOC(fr.chainCounter, 4);
     HIP_TRY(ctx, hipMemset(fr.chainCounter, 0, 4));
+    {  // active-tile lists (denoise.hip): 2 x 2 x 16 counters 128 B apart, then 2 x 16 partitions of entries
+        fr.tileCap = (uint32_t)(((W + 15) / 16) * ((H + 15) / 16));
+        const size_t words = 2 * 2 * 16 * 32 + 2 * 16 * (size_t)(fr.tileCap / 16 + 1);
+        ALLOC(fr.tileList, words * 4);
+        HIP_TRY(ctx, hipMemset(fr.tileList, 0, words * 4));
+    }
     ALLOC(fr.c4, W4 * H4 * 8);
     ALLOC(fr.c16, W16 * H16 * 8);
     ALLOC(fr.c64, ((W16 + 3) / 4) * ((H16 + 3) / 4) * 8);
@@ -709,7 +727,8 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     // rt_frame_marks_begin: this path trace's kernels are bracketed by events (caller's timed frames)
     hipEvent_t* const savedMarks = ctx->ptMarks;
     if (!ctx->ptMarks && ctx->markNext < ctx->markFrames)
-        ctx->ptMarks = ctx->markRing.data() + (size_t)(ctx->markNext++) * 2 * kPtKernels;
+        ctx->ptMarks = ctx->markRing.data() + (size_t)(ctx->markNext++) * 2 * kFrameKernels;
+    ctx->dnMarks = ctx->ptMarks ? ctx->ptMarks + 2 * kPtKernels : nullptr;  // for this frame's rt_denoise_post
     struct MarksReset {  // every return path leaves ptMarks as it found it
         rt_context* c;
         hipEvent_t* m;
@@ -803,6 +822,16 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.maxWhite = ctx->params.post.maxWhite;
     p.gamma = ctx->params.post.gamma;
     p.dn = ctx->params.denoise;
+    {  // the depth weights' divisors as reciprocals (rtmath.h rt_div_rcp), where that is exact
+        const float sig[3] = {p.dn.temporal_denoise_sigma_depth, p.dn.local_denoise_sigma_depth,
+                              p.dn.large_denoise_sigma_depth};
+        p.rcpDepthOk = 0;
+        for (int k = 0; k < 3; ++k) {
+            volatile float d = sig[k];  // the IEEE reciprocal, as the oracle's check computes it
+            p.rcpDepth[k] = 1.0f / d;
+            if (rt_div_rcp_ok(sig[k])) p.rcpDepthOk |= 1 << k;
+        }
+    }
     p.colorA = fr.color;
     p.colorB = fr.colorB;
     p.normal = fr.normal;
@@ -826,6 +855,10 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     p.noise8 = fr.noise8;
     p.noise16 = fr.noise16;
     p.chainCounter = fr.chainCounter;
+    p.tileList = fr.tileList;
+    p.tileCap = fr.tileCap;
+    p.tileParity = fr.tileParity;
+    p.listUsed = 0;
     p.exposureDone = 0;
     p.histDepthInTemporal = 0;
     p.c4 = fr.c4;
@@ -845,6 +878,8 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     fr.outPitch = fr.drawTarget ? fr.drawPitch : (uint32_t)ctx->screenW;
     p.bluenoise = ctx->dBlueNoise;
     p.hdrOut = with_hdr ? fr.hdr : nullptr;
+    p.marks = ctx->dnMarks;  // the frame's denoise marks (rt_frame_marks_begin / rt_time_frame_kernels)
+    ctx->dnMarks = nullptr;
     p.bloom = ps.enablePostProcess && ps.enableBloomEffect;
     p.toneMappingType = ctx->params.post.toneMappingType;
     p.bloom4 = fr.bloom4;
@@ -1174,6 +1209,9 @@ int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
                           : name == RT_BUF_HISTOGRAM ? (void**)&fr.histogram : (void**)&fr.rgba;
             HIP_TRY(ctx, hipMemcpy(device_ptr, *slot, need, hipMemcpyDeviceToDevice));
             if (name == RT_BUF_RGBA8 && fr.outRgba == fr.rgba) fr.outRgba = (uint32_t*)device_ptr;
+            // a caller-owned accumulation buffer stays the one the filters write in place: the
+            // list chain, which alternates two, is off from here on
+            if (name == RT_BUF_ACCUMULATION) fr.accumAlt = nullptr;
             *slot = device_ptr;
             return RT_OK;
         }

@@ -186,7 +186,8 @@ struct DenoisePostParams {
     const uint2* albedo;
     uint16_t* depth;            // written only by the noise-visualize debug pass
     const uint32_t* motion;
-    uint2* accum;               // AccumulationColorBuffer
+    uint2* accum;               // AccumulationColorBuffer (the previous frame's, which TemporalFilter reads)
+    uint2* accumAlt;            // the list chain's output accumulation buffer (null: none, filters write accum)
     uint2* histColor;           // HistoryColorBuffer of the previous frame (read by TemporalFilter2)
     uint2* histColorOut;        // HistoryColorBuffer written this frame (the other of the pair)
     uint16_t* histDepth;        // HistoryDepthBuffer
@@ -217,7 +218,18 @@ struct DenoisePostParams {
     int histDepthInTemporal;    // k_temporal also copies depth into the history depth (per launch)
     uint2* svgfOut;             // phase 2 -> 3: the colour buffer TemporalSpatialDenoising ended in
     int histDepthDone;          // phase 2 -> 3: k_temporal already wrote the history depth
+    uint32_t* tileList;         // active-tile lists of the noise-gated passes (denoise.hip), or null
+    uint32_t tileCap;           // tiles the lists can hold (16x16 tiles of the allocated render size)
+    int tileParity;             // this frame's counter set (the other one is zeroed by TemporalFilter)
+    int listUsed;               // out (phase 0 / 2): the chain ran over the lists; the host flips tileParity
+    float rcpDepth[3];          // RN(1 / sigma_depth) of TemporalFilter, SpatialFilter7x7, the a-trous passes
+    int rcpDepthOk;             // bit k: that sigma is in rt_div_rcp's range (else the taps divide)
+    hipEvent_t* marks;          // optional, host side only: 2 * kDnKernels events, marks[2k] / [2k + 1]
+                                // recorded right before / after denoise kernel k (null entries: not marked)
 };
+// the denoise / post kernels of a whole-frame chain, in launch order (the marks' kernel index)
+constexpr int kDnKernels = 8;  // k_temporal, k_spatial7, k_spatial5<3>, <6>, <12>, k_temporal2,
+                               // k_downscale_chain, k_scale_post
 
 extern "C" hipError_t rtk_denoise_post(DenoisePostParams* p, hipStream_t stream);
 // phase 0: denoise .. DownScale4 + Histogram2; phase 1: AutoExposure .. RGBA8 (finalColor of phase 0 in).
@@ -237,6 +249,7 @@ extern "C" hipError_t rtk_launch_scan_ex(const float* in, float* out, float* sum
                                          int postfix, hipStream_t stream);
 // kernels of one path-trace launch: camera, shade, trace<3>, resume<3>, trace<4>, resume<4>, resolve
 constexpr int kPtKernels = 7;
+constexpr int kFrameKernels = kPtKernels + kDnKernels;  // a frame's marks: path trace, then denoise / post
 struct PtLaunchHook {
     hipError_t (*fn)(void* arg, int kernel);  // after each kernel is enqueued (1 = shade, 2 = trace<3>, ...)
     void* arg;

@@ -329,39 +329,53 @@ RT_HD float exp2_core(float f) {
     return f_fma(p, f, 1.0f);
 }
 
-// p * 2^n for p in [0.7, 1.5], n in [-151, 128], one rounding (into the subnormal range too)
+// p * 2^n for p in [0.7, 1.5], n in [-151, 128], one rounding (into the subnormal range too):
+// p * 2^n1 is exact (2^n1 normal) and the product with f2 (1, 2 or 2^-64) rounds once.  Selects, no
+// branches (the per-tap exp / pow of the denoiser run it in every lane).
 RT_HD float scale2(float p, int n) {
-    if (n > 127) return p * 2.0f * bits_to_float((uint32_t)(n - 1 + 127) << 23);
-    if (n >= -126) return p * bits_to_float((uint32_t)(n + 127) << 23);
-    return (p * bits_to_float((uint32_t)(n + 64 + 127) << 23)) * bits_to_float((uint32_t)(-64 + 127) << 23);
+    const bool hi = n > 127, lo = n < -126;
+    const int n1 = hi ? n - 1 : lo ? n + 64 : n;
+    const float f2 = hi ? 2.0f : lo ? bits_to_float((uint32_t)(-64 + 127) << 23) : 1.0f;
+    return (p * bits_to_float((uint32_t)(n1 + 127) << 23)) * f2;
 }
 
-// 2^(hi + lo), |lo| <= ulp(hi)
+// 2^(hi + lo), |lo| <= ulp(hi); hi >= 128 gives +inf, hi < -152 gives +0 (selects, no branches)
 RT_HD float exp2_pair(float hi, float lo) {
-    if (hi >= 128.0f) return bits_to_float(0x7F800000u);
-    if (hi < -152.0f) return 0.0f;
-    const float n = __builtin_rintf(hi);
-    const float f = (hi - n) + lo;  // hi - n is exact
-    return scale2(exp2_core(f), (int)n);
+    const float hc = __builtin_fminf(__builtin_fmaxf(hi, -160.0f), 136.0f);  // keeps the exponent arithmetic in range
+    const float n = __builtin_rintf(hc);
+    const float f = (hc - n) + lo;  // hc - n is exact
+    const float r = scale2(exp2_core(f), (int)n);
+    return hi != hi ? hi : hi >= 128.0f ? bits_to_float(0x7F800000u) : hi < -152.0f ? 0.0f : r;
 }
 
-// log2(x) = hi + lo for finite x > 0
+// 1 / d for d in [1.70, 2.42] (log2_pair's 2 + r) to ~2^-24 relative: the linear minimax seed
+// (relative error 1.5 %) and two Newton steps, fma only — the same bits on the GPU and the host,
+// unlike the hardware reciprocal, and without the division's scale / fixup sequence.
+RT_HD float recip_log_den(float d) {
+    float y = f_fma(-0.239016f, d, 0.985076f);  // c1 (a + b) = 0.98508, c1 = 2 / (ab + (a + b)^2 / 4)
+    y = f_fma(y, f_fma(-d, y, 1.0f), y);
+    return f_fma(y, f_fma(-d, y, 1.0f), y);
+}
+
+// log2(x) = hi + lo for finite x > 0 (~2^-44 relative).  Division-free: r / (2 + r) is r times the
+// Newton reciprocal above, corrected once by its exact remainder to within an ulp (so the second
+// remainder, which carries the low part, is exact as well); subnormal x and the mantissa fold take
+// selects.
 RT_HD void log2_pair(float x, float& hi, float& lo) {
-    uint32_t b = float_to_bits(x);
-    int e = 0;
-    if (b < 0x00800000u) {  // subnormal: scale by 2^23
-        x *= 8388608.0f;
-        b = float_to_bits(x);
-        e = -23;
-    }
-    e += (int)(b >> 23) - 127;
+    const bool sub = float_to_bits(x) < 0x00800000u;
+    const uint32_t b = float_to_bits(sub ? x * 8388608.0f : x);  // subnormal: scale by 2^23
+    int e = (int)(b >> 23) - (sub ? 150 : 127);
     float m = bits_to_float((b & 0x007FFFFFu) | 0x3F800000u);  // [1, 2)
-    if (m > 1.41421354f) { m *= 0.5f; e += 1; }
+    const bool fold = m > 1.41421354f;
+    m = fold ? m * 0.5f : m;
+    e += fold ? 1 : 0;
     const float r = m - 1.0f;  // exact
     // ln(1 + r) = 2 atanh(s), s = r / (2 + r), s carried as s_hi + s_lo
     const float d = 2.0f + r, dl = r - (d - 2.0f);  // 2 + r exactly as d + dl
-    const float s = r / d;
-    const float sl = (f_fma(-s, d, r) - s * dl) / d;
+    const float y = recip_log_den(d);
+    const float s0 = r * y;
+    const float s = f_fma(f_fma(-s0, d, r), y, s0);      // r / d within an ulp
+    const float sl = (f_fma(-s, d, r) - s * dl) * y;    // the exact remainder over d: r / (2 + r) - s
     const float s2 = s * s;
     float q = 1.0f / 13.0f;
     q = f_fma(q, s2, 1.0f / 11.0f);
@@ -483,6 +497,25 @@ RT_HD float atan2f_fcore(float y, float x) {
 }
 }  // namespace rtm
 
+// a / b for a divisor b that many lanes share (the denoiser's sigmas), with c = RN(1 / b) computed
+// once: two remainder corrections (Markstein) turn a * c into the IEEE quotient as long as the
+// quotient and the remainders stay normal — for 2^-20 <= |b| <= 2^20 and a = 0 or
+// 2^-30 <= |a| <= 2^30 (every such float a, for the denoiser's default sigmas and a sample of
+// others: tools/div_exhaustive.c, tests/test_rtmath.py).  Zero, infinite and NaN a return a * c,
+// which is the quotient there too.  Five instructions instead of the division's ten and its
+// reciprocal; callers keep the division for a divisor outside that range.
+RT_HD float rt_div_rcp(float a, float b, float c) {
+    const float q0 = a * c;
+    const float q1 = rtm::f_fma(rtm::f_fma(-q0, b, a), c, q0);
+    const float q2 = rtm::f_fma(rtm::f_fma(-q1, b, a), c, q1);
+    return (a != 0.0f && __builtin_fabsf(q0) < rtm::bits_to_float(0x7F800000u)) ? q2 : q0;
+}
+// whether rt_div_rcp may stand for a / b (host side, once per divisor)
+inline bool rt_div_rcp_ok(float b) {
+    const float ab = b < 0.0f ? -b : b;
+    return ab >= 0x1p-20f && ab <= 0x1p20f;
+}
+
 // x / 65535 for a 16-bit texel value x (Load2DFuncUshort4's unorm conversion), correctly rounded:
 // the product with c = RN(1/65535) corrected by one fma step (Markstein).  Equal to the IEEE
 // division for every x in [0, 65535] (checked exhaustively: tests/test_rtmath.py); 3 instructions
@@ -499,12 +532,11 @@ RT_HD float rt_exp2f(float x) {
 }
 
 RT_HD float rt_expf(float x) {
-    if (x != x) return x;
-    if (x > 89.0f) return rtm::bits_to_float(0x7F800000u);
-    if (x < -104.0f) return 0.0f;
-    // Cody-Waite: x = n ln2 + r, ln2 = 0.693145752 (16 bits) + 1.42860677e-06
-    const float n = __builtin_rintf(x * 1.44269502162933349609f);
-    float r = rtm::f_fma(-n, 0.693145751953125f, x);
+    // Cody-Waite: x = n ln2 + r, ln2 = 0.693145752 (16 bits) + 1.42860677e-06; the range checks are
+    // selects on the result (x clamped into range for the arithmetic), not branches
+    const float xc = __builtin_fminf(__builtin_fmaxf(x, -104.0f), 89.0f);
+    const float n = __builtin_rintf(xc * 1.44269502162933349609f);
+    float r = rtm::f_fma(-n, 0.693145751953125f, xc);
     r = rtm::f_fma(-n, 1.428606765330187e-06f, r);
     // e^r, |r| <= 0.35: Taylor to degree 8
     float p = 2.4801587301587302e-05f;
@@ -516,7 +548,8 @@ RT_HD float rt_expf(float x) {
     p = rtm::f_fma(p, r, 0.5f);
     p = rtm::f_fma(p, r, 1.0f);
     p = rtm::f_fma(p, r, 1.0f);
-    return rtm::scale2(p, (int)n);
+    const float v = rtm::scale2(p, (int)n);
+    return x != x ? x : x > 89.0f ? rtm::bits_to_float(0x7F800000u) : x < -104.0f ? 0.0f : v;
 }
 
 RT_HD float rt_log2f(float x) {

@@ -376,6 +376,9 @@ class RayTracer:
 
     PT_KERNELS = ("k_pt_camera", "k_pt_shade0", "k_trace_queue<3>", "k_pt_resume<3>", "k_trace_queue<4>",
                   "k_pt_resume<4>", "k_pt_resolve")
+    DN_KERNELS = ("k_temporal", "k_spatial7", "k_spatial5<3>", "k_spatial5<6>", "k_spatial5<12>", "k_temporal2",
+                  "k_downscale_chain", "k_scale_post")
+    FRAME_KERNELS = PT_KERNELS + DN_KERNELS
 
     def time_path_trace_kernels(self, iters=10):
         """Average ms of each path-trace kernel (HIP events on the context stream)."""
@@ -384,25 +387,25 @@ class RayTracer:
         return dict(zip(self.PT_KERNELS, (float(v) for v in ms)))
 
     def time_frame_kernels(self, first_frame: int, iters: int = 10):
-        """Average ms of each path-trace kernel over `iters` whole frames run as the caller runs
-        them (pipelined when a post stream is set); waits for the frames."""
-        ms = (C.c_float * len(self.PT_KERNELS))()
+        """Average ms of each path-trace and denoise / post kernel over `iters` whole frames run as
+        the caller runs them (pipelined when a post stream is set); waits for the frames."""
+        ms = (C.c_float * len(self.FRAME_KERNELS))()
         self._check(self.lib.rt_time_frame_kernels(self.h, first_frame, iters, ms, len(ms)), "rt_time_frame_kernels")
-        return dict(zip(self.PT_KERNELS, (float(v) for v in ms)))
+        return dict(zip(self.FRAME_KERNELS, (float(v) for v in ms)))
 
     def frame_marks_begin(self, frames: int, kernels=None):
-        """Bracket the path-trace kernels named in `kernels` (all when None) of the next `frames`
-        path traces with HIP events on the streams they run on."""
-        names = self.PT_KERNELS if kernels is None else kernels
-        mask = sum(1 << self.PT_KERNELS.index(k) for k in names)
+        """Bracket the kernels named in `kernels` (all 15 when None) of the next `frames` frames with
+        HIP events on the streams they run on."""
+        names = self.FRAME_KERNELS if kernels is None else kernels
+        mask = sum(1 << self.FRAME_KERNELS.index(k) for k in names)
         self._check(self.lib.rt_frame_marks_begin(self.h, frames, mask), "rt_frame_marks_begin")
 
     def frame_marks_read(self):
         """({kernel: average ms over the recorded frames} for the marked kernels, frames recorded); waits."""
-        ms = (C.c_float * len(self.PT_KERNELS))()
+        ms = (C.c_float * len(self.FRAME_KERNELS))()
         n = C.c_int()
         self._check(self.lib.rt_frame_marks_read(self.h, ms, len(ms), C.byref(n)), "rt_frame_marks_read")
-        return {k: float(v) for k, v in zip(self.PT_KERNELS, ms) if v >= 0.0}, n.value
+        return {k: float(v) for k, v in zip(self.FRAME_KERNELS, ms) if v >= 0.0}, n.value
 
     # ---- camera file I/O and offscreen image dumps
     def save_camera(self, path: str):

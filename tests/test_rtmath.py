@@ -113,3 +113,15 @@ def test_div_by_pi_constants_equal_division(oracle, d):
     """pt_common.h div_pi / div_two_pi: x * RN(1/d) plus one fma correction is the IEEE quotient x / d
     for finite |x| >= 2^-100 (tools/div_exhaustive.c checks all 2^32 patterns; here every 4,099th)."""
     assert oracle.lib().orc_div_const_mismatches(float(d), 4099) == 0
+
+
+_SIGMAS = [0.1, 0.01, 100.0] + [float(np.float32(2.0) ** e) for e in np.random.default_rng(17).uniform(-20, 20, 6)]
+
+
+@pytest.mark.parametrize("d", _SIGMAS)
+def test_div_rcp_equals_division(oracle, d):
+    """rtmath.h rt_div_rcp (x * RN(1/d) with two remainder corrections: the denoiser's depth weights
+    (dV - d) / sigma) is the IEEE quotient for x = 0, +-inf, NaN and every 2^-30 <= |x| <= 2^30, for
+    divisors in [2^-20, 2^20]: the defaults 0.1, 0.01 (tools/div_exhaustive.c checks all 2^32 patterns
+    for those) and six random ones; here every 4,099th pattern."""
+    assert oracle.lib().orc_div_rcp_mismatches(float(np.float32(d)), 4099) == 0

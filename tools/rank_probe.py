@@ -4,7 +4,9 @@
 The rows other ranks would deliver are filled once with a full-frame render (the denoiser's cost
 depends on them: sky pixels skip the filters), so the denoise sees the frame it would see after
 the gather.  STRIP_DN=1: each rank denoises only its strip (+ halo), with the collective hook a
-no-op (compute only: the exchanges are left out).  Prints ms per frame for each N.  Usage: tools/rank_probe.py [N ...] (default 1 2 4 8)."""
+no-op (compute only: the exchanges are left out).  Prints ms per frame for each N, one fresh process
+per N.  Usage: [W=3840 H=2160] [QUICK=1] [STRIP_DN=1] [STAGES=1] [FRAMES=30] tools/rank_probe.py [N ...]
+(default 1 2 4 8; QUICK: the pipelined frame with denoise only; STAGES: serial stage split too)."""
 import os
 import sys
 import tempfile
@@ -80,7 +82,15 @@ def run(n, frames=int(os.environ.get("FRAMES", "30")), warm=3, W=int(os.environ.
 
 
 if __name__ == "__main__":
-    for n in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
+    ns = [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]
+    if len(ns) > 1:  # one fresh process per N: a second context in one process can land in a slower schedule
+        import subprocess
+        for n in ns:
+            rc = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), str(n)], timeout=300).returncode
+            if rc:
+                sys.exit(rc)
+        sys.exit(0)
+    for n in ns:
         variants = ((True, True), (False, True), (True, False), (False, False))
         for pipe, dn in variants[:1] if os.environ.get("QUICK") else variants:
             print("N=%d rank-0 strip (%sx%s), %s, %s: %.3f ms/frame" % (n, os.environ.get("W", "1920"),

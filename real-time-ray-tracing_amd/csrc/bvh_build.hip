@@ -53,7 +53,8 @@ struct Lds {
     } a;
     uint32_t key1[kBatch];  // sorted keys (the sort ends in buffer 1)
     uint16_t idx1[kBatch];
-    float merged[kBatch][6];  // merged box of each internal node; rows 0..15: the box reductions
+    float merged[kBatch][6];  // merged box of each internal node (rows 0..2 hold the gather's centroids
+                              // until the refit; block_reduce's partials use the sort histogram's area)
     float leaf[kLeafLds ? kBatch : 1][6];  // leaf boxes by original local index (kThr 1024)
 };
 
@@ -346,10 +347,15 @@ RT_DEV void climb_start(const Lds<kThr>& s, const float* leafG, int n, int i, Cl
     c.on = true;
 }
 
-template <int kThr>
+// kDefer: the merged box of every node goes to LDS and refit() stores the nodes afterwards, in
+// order; otherwise each climb step stores its node.  On gfx9 vmcnt counts stores too, so a step's
+// wait for its sibling-box load also waited for the 64-B node store it had just issued (the refit
+// phase of the 958,720-triangle build: 38 k of its 143 k clocks).
+template <int kThr, bool kDefer>
 RT_DEV void climb_step(Lds<kThr>& s, const float* leafG, Node* nodes, const WordCtx& w, Climb& c) {
     const Box m = box_merge(c.l, c.r);
-    store_node(nodes + c.cur, c.l, c.r, c.cl, c.cr, w);
+    if (kDefer) store_box(s.merged[c.cur], m);
+    else store_node(nodes + c.cur, c.l, c.r, c.cl, c.cr, w);
     if (c.cur == 0) {
         c.on = false;
         return;
@@ -363,7 +369,7 @@ RT_DEV void climb_step(Lds<kThr>& s, const float* leafG, Node* nodes, const Word
     if (sib & 0x8000u) {
         sb = leaf_box(s, leafG, sib & 0x7FFFu);
     } else {  // two internal children: the second arrival finishes the parent
-        store_box(s.merged[c.cur], m);
+        if (!kDefer) store_box(s.merged[c.cur], m);
         const uint32_t old = __hip_atomic_fetch_add((U32Alias*)&s.a.info[p][2], 0x10000u, __ATOMIC_ACQ_REL,
                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
         if ((old >> 16) == 0u) {
@@ -380,8 +386,11 @@ RT_DEV void climb_step(Lds<kThr>& s, const float* leafG, Node* nodes, const Word
     c.cur = p;
 }
 
-// The climbs of this thread's internal nodes (kPer of them, one after the other).
-template <int kThr>
+// The climbs of this thread's internal nodes (kPer of them, one after the other).  kDefer (every
+// thread of the workgroup calls): the nodes are stored after the climbs, node i by thread i mod kThr,
+// from the children's boxes — leaf boxes and the merged boxes the climbs left in LDS — so the stores
+// are coalesced and no climb step waits for one.  Without kDefer (the one-wave TLAS) the steps store.
+template <int kThr, bool kDefer>
 RT_DEV void refit(Lds<kThr>& s, const float* leafG, int n, Node* nodes, const WordCtx& w) {
     constexpr int kPer = kBatch / kThr;
     const int t = threadIdx.x;
@@ -397,7 +406,19 @@ RT_DEV void refit(Lds<kThr>& s, const float* leafG, int n, Node* nodes, const Wo
         Climb c;
         climb_start(s, leafG, n, t + j * kThr, c);
         for (int guard = 0; guard < kBatch && c.on; ++guard)  // a valid tree ends at the root in < n steps
-            climb_step(s, leafG, nodes, w, c);
+            climb_step<kThr, kDefer>(s, leafG, nodes, w, c);
+    }
+    if (!kDefer) return;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int i = t + j * kThr;
+        if (i >= n - 1) continue;
+        const uint64_t inf = info_of(s, i);
+        const uint32_t cl = (uint32_t)inf & 0xFFFFu, cr = (uint32_t)(inf >> 16) & 0xFFFFu;
+        const Box l = (cl & 0x8000u) ? leaf_box(s, leafG, cl & 0x7FFFu) : load_box(s.merged[cl]);
+        const Box r = (cr & 0x8000u) ? leaf_box(s, leafG, cr & 0x7FFFu) : load_box(s.merged[cr]);
+        store_node(nodes + i, l, r, cl, cr, w);
     }
 }
 
@@ -463,7 +484,7 @@ RT_DEV void sort_and_build(Lds<kThr>& s, const float* leafG, int n, uint32_t* mo
     __syncthreads();
     BVH_STAMP(4);
 #if !(defined(RTX_BVH_ABL) && RTX_BVH_ABL == 3)
-    refit(s, leafG, n, nodes, w);  // (ablation 3: no refit; timing only)
+    refit<kThr, true>(s, leafG, n, nodes, w);  // (ablation 3: no refit; timing only)
 #endif
 }
 
@@ -508,7 +529,7 @@ RT_DEV void tlas_wave(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
     P.tlasReorder[lane] = s.idx1[lane];
     karras(s, (int)B);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    refit(s, P.tlasAabbs, (int)B, (Node*)P.tlasNodes, tlas_words(B));
+    refit<kThr, false>(s, P.tlasAabbs, (int)B, (Node*)P.tlasNodes, tlas_words(B));
 }
 
 }  // namespace

@@ -329,23 +329,20 @@ RT_HD float exp2_core(float f) {
     return f_fma(p, f, 1.0f);
 }
 
-// p * 2^n for p in [0.7, 1.5], n in [-151, 128], one rounding (into the subnormal range too):
-// p * 2^n1 is exact (2^n1 normal) and the product with f2 (1, 2 or 2^-64) rounds once.  Selects, no
-// branches (the per-tap exp / pow of the denoiser run it in every lane).
+// p * 2^n for p in [0.7, 1.5], n in [-151, 128], one rounding (into the subnormal range too)
 RT_HD float scale2(float p, int n) {
-    const bool hi = n > 127, lo = n < -126;
-    const int n1 = hi ? n - 1 : lo ? n + 64 : n;
-    const float f2 = hi ? 2.0f : lo ? bits_to_float((uint32_t)(-64 + 127) << 23) : 1.0f;
-    return (p * bits_to_float((uint32_t)(n1 + 127) << 23)) * f2;
+    if (n > 127) return p * 2.0f * bits_to_float((uint32_t)(n - 1 + 127) << 23);
+    if (n >= -126) return p * bits_to_float((uint32_t)(n + 127) << 23);
+    return (p * bits_to_float((uint32_t)(n + 64 + 127) << 23)) * bits_to_float((uint32_t)(-64 + 127) << 23);
 }
 
-// 2^(hi + lo), |lo| <= ulp(hi); hi >= 128 gives +inf, hi < -152 gives +0 (selects, no branches)
+// 2^(hi + lo), |lo| <= ulp(hi)
 RT_HD float exp2_pair(float hi, float lo) {
-    const float hc = __builtin_fminf(__builtin_fmaxf(hi, -160.0f), 136.0f);  // keeps the exponent arithmetic in range
-    const float n = __builtin_rintf(hc);
-    const float f = (hc - n) + lo;  // hc - n is exact
-    const float r = scale2(exp2_core(f), (int)n);
-    return hi != hi ? hi : hi >= 128.0f ? bits_to_float(0x7F800000u) : hi < -152.0f ? 0.0f : r;
+    if (hi >= 128.0f) return bits_to_float(0x7F800000u);
+    if (hi < -152.0f) return 0.0f;
+    const float n = __builtin_rintf(hi);
+    const float f = (hi - n) + lo;  // hi - n is exact
+    return scale2(exp2_core(f), (int)n);
 }
 
 // 1 / d for d in [1.70, 2.42] (log2_pair's 2 + r) to ~2^-24 relative: the linear minimax seed
@@ -359,16 +356,18 @@ RT_HD float recip_log_den(float d) {
 
 // log2(x) = hi + lo for finite x > 0 (~2^-44 relative).  Division-free: r / (2 + r) is r times the
 // Newton reciprocal above, corrected once by its exact remainder to within an ulp (so the second
-// remainder, which carries the low part, is exact as well); subnormal x and the mantissa fold take
-// selects.
+// remainder, which carries the low part, is exact as well).
 RT_HD void log2_pair(float x, float& hi, float& lo) {
-    const bool sub = float_to_bits(x) < 0x00800000u;
-    const uint32_t b = float_to_bits(sub ? x * 8388608.0f : x);  // subnormal: scale by 2^23
-    int e = (int)(b >> 23) - (sub ? 150 : 127);
+    uint32_t b = float_to_bits(x);
+    int e = 0;
+    if (b < 0x00800000u) {  // subnormal: scale by 2^23
+        x *= 8388608.0f;
+        b = float_to_bits(x);
+        e = -23;
+    }
+    e += (int)(b >> 23) - 127;
     float m = bits_to_float((b & 0x007FFFFFu) | 0x3F800000u);  // [1, 2)
-    const bool fold = m > 1.41421354f;
-    m = fold ? m * 0.5f : m;
-    e += fold ? 1 : 0;
+    if (m > 1.41421354f) { m *= 0.5f; e += 1; }
     const float r = m - 1.0f;  // exact
     // ln(1 + r) = 2 atanh(s), s = r / (2 + r), s carried as s_hi + s_lo
     const float d = 2.0f + r, dl = r - (d - 2.0f);  // 2 + r exactly as d + dl
@@ -532,11 +531,12 @@ RT_HD float rt_exp2f(float x) {
 }
 
 RT_HD float rt_expf(float x) {
-    // Cody-Waite: x = n ln2 + r, ln2 = 0.693145752 (16 bits) + 1.42860677e-06; the range checks are
-    // selects on the result (x clamped into range for the arithmetic), not branches
-    const float xc = __builtin_fminf(__builtin_fmaxf(x, -104.0f), 89.0f);
-    const float n = __builtin_rintf(xc * 1.44269502162933349609f);
-    float r = rtm::f_fma(-n, 0.693145751953125f, xc);
+    if (x != x) return x;
+    if (x > 89.0f) return rtm::bits_to_float(0x7F800000u);
+    if (x < -104.0f) return 0.0f;
+    // Cody-Waite: x = n ln2 + r, ln2 = 0.693145752 (16 bits) + 1.42860677e-06
+    const float n = __builtin_rintf(x * 1.44269502162933349609f);
+    float r = rtm::f_fma(-n, 0.693145751953125f, x);
     r = rtm::f_fma(-n, 1.428606765330187e-06f, r);
     // e^r, |r| <= 0.35: Taylor to degree 8
     float p = 2.4801587301587302e-05f;
@@ -548,8 +548,7 @@ RT_HD float rt_expf(float x) {
     p = rtm::f_fma(p, r, 0.5f);
     p = rtm::f_fma(p, r, 1.0f);
     p = rtm::f_fma(p, r, 1.0f);
-    const float v = rtm::scale2(p, (int)n);
-    return x != x ? x : x > 89.0f ? rtm::bits_to_float(0x7F800000u) : x < -104.0f ? 0.0f : v;
+    return rtm::scale2(p, (int)n);
 }
 
 RT_HD float rt_log2f(float x) {

@@ -17,8 +17,13 @@ from __future__ import annotations
 
 
 class FramePipeline:
+    PRIORITIES = ("lo", "hi", "0")
+
     def __init__(self, rt, device, pipelined: bool = True, world: int = 1, rank: int = 0, backend: str = "nccl",
-                 strip_denoise: bool = True):
+                 strip_denoise: bool = True, main_priority: str = "hi", post_priority: str = "lo"):
+        """main_priority / post_priority: the torch stream priorities of the renderer's stream and the
+        denoise/post stream ("hi", "lo" or "0", the normal priority); by default the trace chain
+        outranks the denoise stream (A/B of other choices: DESIGN.md §7)."""
         import torch
 
         import rtx
@@ -26,12 +31,14 @@ class FramePipeline:
 
         self.rt, self.device, self.pipelined = rt, device, pipelined
         self.world, self.rank = world, rank
-        if pipelined:  # the trace chain outranks the denoise stream
-            import os
+        for p in (main_priority, post_priority):
+            if p not in self.PRIORITIES:
+                raise ValueError("stream priority must be one of %s, not %r" % (self.PRIORITIES, p))
+        if pipelined:
             lo, hi = torch.cuda.Stream.priority_range()
             pick = {"lo": lo, "hi": hi, "0": 0}
-            self.main = torch.cuda.Stream(device, priority=pick.get(os.environ.get("RTX_MAIN_PRIO", "hi"), hi))
-            self.post = torch.cuda.Stream(device, priority=pick.get(os.environ.get("RTX_POST_PRIO", "lo"), lo))
+            self.main = torch.cuda.Stream(device, priority=pick[main_priority])
+            self.post = torch.cuda.Stream(device, priority=pick[post_priority])
             torch.cuda.set_stream(self.main)
         else:
             self.main, self.post = torch.cuda.current_stream(device), None

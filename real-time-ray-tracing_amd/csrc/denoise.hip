@@ -143,6 +143,10 @@ RT_DEV float depth_ratio(const DenoisePostParams& P, int k, float a, float sigma
 }
 
 // 16-row tile row of this workgroup: launches may cover tile rows [P.ty0, P.ty1) only
+// The tile passes' grids are (tiles across, tile rows), in row-major order.  Dealing each XCD a
+// contiguous eighth of the tiles instead (so a tile's neighbours share its L2) took TemporalFilter
+// 26 -> 54 us and the full-frame a-trous passes 32 -> 105 us (profiles/r05_ab/xcd_tiles/).
+RT_DEV int tile_x(const DenoisePostParams&) { return (int)blockIdx.x; }
 RT_DEV int tile_y(const DenoisePostParams& P) { return (int)blockIdx.y + P.ty0; }
 
 template <typename T>
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uin
     __shared__ uint2 sOut[kNoise ? 256 : 1];
     __shared__ uint16_t sN8[4];
     __shared__ int sCopy;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
+    const int x = tile_x(P) * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     const int W = (int)P.W, H = (int)P.H;
     if (kList && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2 * kListParts)  // the other parity's
         *list_counter(P, P.tileParity ^ 1, (int)threadIdx.x / kListParts, (int)threadIdx.x % kListParts) = 0u;
@@ -272,10 +276,10 @@ __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uin
     }
     if (kNoise) {
         __syncthreads();
-        const float n16 = noise_epilogue(P, sOut, sN8, (int)blockIdx.x, tile_y(P));
+        const float n16 = noise_epilogue(P, sOut, sN8, tile_x(P), tile_y(P));
         if (kList) {
             if (threadIdx.x == 0) {
-                const uint32_t tile = (uint32_t)(tile_y(P) * (int)((P.W + 15) / 16) + (int)blockIdx.x);
+                const uint32_t tile = (uint32_t)(tile_y(P) * (int)((P.W + 15) / 16) + tile_x(P));
                 const bool act7 = !(n16 < P.dn.noise_threshold_local), act5 = !(n16 < P.dn.noise_threshold_large);
                 if (act7) list_append(P, 0, tile);
                 else if (act5) list_append(P, 1, tile);
@@ -416,7 +420,7 @@ __global__ __launch_bounds__(256) void k_noise16(DenoisePostParams P) {
 
 // TileNoiseLevelVisualize (debug pass): outline 16x16 tiles above the noise threshold
 __global__ __launch_bounds__(256) void k_noise_visualize(DenoisePostParams P, uint2* color, int level) {
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
+    const int x = tile_x(P) * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= (int)P.W || y >= (int)P.H) return;
     const int tx = x & 15, ty = y & 15;
     if (!(tx == 0 || tx == 15 || ty == 0 || ty == 15)) return;
@@ -478,11 +482,11 @@ __global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uin
     DN_PRIO();
     __shared__ S7Lds L;
     const int TY = tile_y(P), W16 = ((int)P.W + 15) / 16;
-    const bool gated = kDnGateAll || h2f(P.noise16[TY * W16 + blockIdx.x]) < P.dn.noise_threshold_local;
-    spatial7_tile<kRcp>(P, in, out, L, (int)blockIdx.x, TY, gated, (int)threadIdx.x);
+    const bool gated = kDnGateAll || h2f(P.noise16[TY * W16 + tile_x(P)]) < P.dn.noise_threshold_local;
+    spatial7_tile<kRcp>(P, in, out, L, tile_x(P), TY, gated, (int)threadIdx.x);
     if (kNoise) {
         __syncthreads();
-        noise_epilogue(P, L.Out, L.N8, (int)blockIdx.x, TY);
+        noise_epilogue(P, L.Out, L.N8, tile_x(P), TY);
     }
 }
 
@@ -652,7 +656,7 @@ template <int S, bool kAlbedo, bool kRcp, bool kRedirect>
 __global__ DN5_BOUNDS void k_spatial5(DenoisePostParams P, const uint2* in, uint2* out, const uint2* alt) {
     DN_PRIO();
     const int W = (int)P.W, H = (int)P.H;
-    const int TX = (int)blockIdx.x, TY = tile_y(P);
+    const int TX = tile_x(P), TY = tile_y(P);
     const int x = TX * 16 + (threadIdx.x & 15), y = TY * 16 + (threadIdx.x >> 4);
     const int W16 = (W + 15) / 16;
     const bool active = !kDnGateAll && !(h2f(P.noise16[TY * W16 + TX]) < P.dn.noise_threshold_large);
@@ -907,7 +911,7 @@ __global__ __launch_bounds__(256) void k_temporal2(DenoisePostParams P, const ui
     DN_PRIO();
     __shared__ uint2 sT[kDown ? 256 : 1];
     const int W = (int)P.W, H = (int)P.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
+    const int x = tile_x(P) * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x < W && y < H) {
         const uint2 r = temporal2_pixel(P, in, x, y);
         out[(size_t)y * W + x] = r;
@@ -916,9 +920,9 @@ __global__ __launch_bounds__(256) void k_temporal2(DenoisePostParams P, const ui
     if (kDown) {
         __syncthreads();
         const int t = (int)threadIdx.x, W4 = (W + 3) / 4, H4 = (H + 3) / 4;
-        const int ox = (int)blockIdx.x * 4 + (t & 3), oy = tile_y(P) * 4 + (t >> 2);
+        const int ox = tile_x(P) * 4 + (t & 3), oy = tile_y(P) * 4 + (t >> 2);
         if (t < 16 && ox < W4 && oy < H4)
-            P.c4[oy * W4 + ox] = down4(LdsLevel{sT, W, H, (int)blockIdx.x * 16, tile_y(P) * 16, 16}, ox, oy);
+            P.c4[oy * W4 + ox] = down4(LdsLevel{sT, W, H, tile_x(P) * 16, tile_y(P) * 16, 16}, ox, oy);
     }
 }
 
@@ -1010,13 +1014,15 @@ RT_DEV int bicubic_axis(int x, int Ws, int W, float w[4]) {
     return (int)fx0;
 }
 
+// (k_scale_post's fallback beyond its LDS tile: one row of taps at a time, or the sixteen loads
+// in flight set the kernel's VGPR peak for a path the usual scale factors never take)
 template <class Img>
 RT_DEV uint2 bicubic_scale_px(const Img& im, int W, int H, int x, int y, int Ws, int Hs) {
     float wx[4], wy[4];
     const int t1x = bicubic_axis(x, Ws, W, wx), t1y = bicubic_axis(y, Hs, H, wy);
     F3 o = f3(0.0f);
     float sw = 0.0f;
-#pragma unroll
+#pragma unroll 1
     for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1063,7 +1069,8 @@ RT_DEV F3 tonemap_color(F3 c, int type, float maxWhite, float gamma) {
         c = f3(0.0f) * f3(__builtin_inff());
     }
     const float g = 1.0f / gamma;
-    return clamp3(f3(rt_powf(c.x, g), rt_powf(c.y, g), rt_powf(c.z, g)), f3(0.0f), f3(1.0f));
+    const F3 o = f3(rt_powf(c.x, g), rt_powf(c.y, g), rt_powf(c.z, g));
+    return clamp3(o, f3(0.0f), f3(1.0f));
 }
 
 // ---- BloomGuassian (postprocessing.cuh:348-388): a 16x16 workgroup keys a 16x16 tile
@@ -1121,7 +1128,7 @@ RT_DEV F3 catmull_rom(const View2& im, F2 uv) {
 // Bloom (postprocessing.cuh:390-408), out of place: `in` may be the next frame's history
 __global__ __launch_bounds__(256) void k_bloom_apply(DenoisePostParams P, const uint2* in, uint2* out) {
     const int W = (int)P.W, H = (int)P.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
+    const int x = tile_x(P) * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= W || y >= H) return;
     const int W4 = (W + 3) / 4, H4 = (H + 3) / 4, W16 = (W4 + 3) / 4, H16 = (H4 + 3) / 4;
     const F2 uv = {(float)x / W, (float)y / H};
@@ -1165,7 +1172,7 @@ RT_DEV F3 lf_circle(F2 p, float size, float dist, F2 m) {
 
 __global__ __launch_bounds__(256) void k_lens_flare(DenoisePostParams P, const uint2* in, uint2* out) {
     const int W = (int)P.W, H = (int)P.H;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
+    const int x = tile_x(P) * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= W || y >= H) return;
     const size_t p = (size_t)y * W + x;
     const float sunDepth = h2f(P.depth[(size_t)P.sunUv[1] * W + P.sunUv[0]]);
@@ -1197,30 +1204,41 @@ __global__ __launch_bounds__(256) void k_lens_flare(DenoisePostParams P, const u
 // a 1-pixel apron into LDS, rounded to half exactly as the reference stores ScaledColorBuffer;
 // the sharpened and tone-mapped values are rounded to half in between too, as the reference's
 // separate passes store and reload them.
-constexpr int kScaleLds = 48 * 48;  // render texels staged per workgroup (scale factors up to ~2.5)
+// kLds: render texels staged per workgroup: 24 x 24 covers the 16x16 tile's footprint up to a
+// render / screen ratio of ~1.1 (the usual case, 22 x 22 at 1:1), 48 x 48 up to ~2.5; the host
+// picks the small one when the ratio allows (scale_lds_small), the kernel checks the footprint
+// either way (unstaged reads beyond it).  Occupancy is set by the VGPRs, not the LDS, with the
+// small tile.
+constexpr int kScaleLdsSmall = 24 * 24, kScaleLdsLarge = 48 * 48;
 
 // 256 threads compute the 18x18 scaled apron in two passes (324 = 256 + 68); 384 threads in one pass
 // (the two extra waves leaving after it) measured slower: serial denoise + post 0.274 -> 0.282 ms,
 // pipelined frame 0.869 -> 0.880 (profiles/r04_ab/ablations/scale_post/)
 constexpr int kScaleThreads = 256;
 
+template <int kLds>
 __global__ __launch_bounds__(kScaleThreads) void k_scale_post(DenoisePostParams P, const uint2* render) {
     DN_PRIO();
-    __shared__ uint2 sIn[kScaleLds];
+    __shared__ uint2 sIn[kLds];
     __shared__ uint2 sS[18 * 18];
+    __shared__ uint32_t sSobol[256];  // sobol dims 0..3 (bn_value): CopyToOutput's dither
     const int W = (int)P.W, H = (int)P.H, Ws = (int)P.Ws, Hs = (int)P.Hs;
-    const int X0 = blockIdx.x * 16 - 1, Y0 = tile_y(P) * 16 - 1;
+    const int X0 = tile_x(P) * 16 - 1, Y0 = tile_y(P) * 16 - 1;
+    // the dither's per-pixel bytes and the sobol rows are loaded with the render texels, so the
+    // lookup after the passes reads LDS and registers only
+    const int x = tile_x(P) * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
+    const BnPixel bnp = bn_pixel(P.bluenoise, x, y);
+    bn_stage_sobol(P.bluenoise, sSobol, (int)threadIdx.x, kScaleThreads);
     // render texels the 18x18 output apron reads (t1 is monotone in x and y)
     const int ix0 = clampi(scale_t1(clampi(X0, 0, Ws - 1), Ws, W) - 1, 0, W - 1);
     const int ix1 = clampi(scale_t1(clampi(X0 + 17, 0, Ws - 1), Ws, W) + 2, 0, W - 1);
     const int iy0 = clampi(scale_t1(clampi(Y0, 0, Hs - 1), Hs, H) - 1, 0, H - 1);
     const int iy1 = clampi(scale_t1(clampi(Y0 + 17, 0, Hs - 1), Hs, H) + 2, 0, H - 1);
     const int TW = ix1 - ix0 + 1, TH = iy1 - iy0 + 1;
-    const bool staged = TW * TH <= kScaleLds;
-    if (staged) {
+    const bool staged = TW * TH <= kLds;
+    if (staged)
         for (int i = threadIdx.x; i < TW * TH; i += kScaleThreads) sIn[i] = render[(size_t)(iy0 + i / TW) * W + ix0 + i % TW];
-        __syncthreads();
-    }
+    __syncthreads();
     if (staged) {
         // the x weights and tap columns depend on the apron column only, the y ones on the row
         // only: 36 axis evaluations instead of 2 per texel, same arithmetic (bicubic_axis)
@@ -1266,8 +1284,6 @@ __global__ __launch_bounds__(kScaleThreads) void k_scale_post(DenoisePostParams 
         }
     }
     __syncthreads();
-    if (kScaleThreads > 256 && threadIdx.x >= 256) return;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     if (x >= Ws || y >= Hs) return;
     const size_t p = (size_t)y * Ws + x;
     struct {  // clamped reads of the scaled image, from the LDS tile
@@ -1319,8 +1335,8 @@ __global__ __launch_bounds__(kScaleThreads) void k_scale_post(DenoisePostParams 
     F3 c = rgb_of(cur);
     (void)s;
 #else
-    F3 c = rgb_of(cur) + f3(bluenoise(P.bluenoise, x, y, s, 0) / 256, bluenoise(P.bluenoise, x, y, s, 1) / 256,
-                            bluenoise(P.bluenoise, x, y, s, 2) / 256);
+    F3 c = rgb_of(cur) + f3(bn_value(sSobol, bnp, s, 0) / 256, bn_value(sSobol, bnp, s, 1) / 256,
+                            bn_value(sSobol, bnp, s, 2) / 256);
 #endif
     const float hi = 1.0f - 1.1920928955078125e-07f;
     c = clamp3(c, f3(0.0f), f3(hi));
@@ -1336,6 +1352,11 @@ __global__ __launch_bounds__(256) void k_hdr_out(const uint2* color, float4* hdr
 }
 
 }  // namespace
+
+// k_scale_post's footprint of 18 screen texels along an axis spans at most 17 * r + 5 render
+// texels (r = render / screen: the first tap one before t1, the last two after, one more for the
+// floors' rounding); the small LDS tile holds 24 of them
+static bool scale_lds_small(int render, int screen) { return 17 * render + 5 * screen <= 24 * screen - screen; }
 
 #define LAUNCH_CHECK()                          \
     do {                                        \
@@ -1440,8 +1461,11 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         Q.ty1 = t1;
         if (t1 > t0) {
             DN_MARK(7, 0);
-            hipLaunchKernelGGL(k_scale_post, dim3((Ws + 15) / 16, (unsigned)(t1 - t0)), dim3(kScaleThreads), 0, s, Q,
-                               (const uint2*)cur);
+            const dim3 gs((Ws + 15) / 16, (unsigned)(t1 - t0));
+            if (scale_lds_small(W, Ws) && scale_lds_small(H, Hs))
+                hipLaunchKernelGGL(k_scale_post<kScaleLdsSmall>, gs, dim3(kScaleThreads), 0, s, Q, (const uint2*)cur);
+            else
+                hipLaunchKernelGGL(k_scale_post<kScaleLdsLarge>, gs, dim3(kScaleThreads), 0, s, Q, (const uint2*)cur);
             LAUNCH_CHECK();
             DN_MARK(7, 1);
         }

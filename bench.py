@@ -60,9 +60,14 @@ for p in (ROOT, PKG):
 
 HBM_PEAK_GBS = 8000.0   # /opt/skills/guides/MI355X_MICROARCH.md (spec peak)
 L2_PEAK_GBS = 34500.0   # MI355X_MICROARCH.md, L2 (per XCD) section: aggregate L2 bandwidth
+# vector-instruction issue: a wave's f32 VALU instruction holds its SIMD 4 cycles (8 for the
+# transcendentals; MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'); 256 CUs x 4 SIMDs at the
+# 2.4 GHz peak clock.  A kernel's SQ_INSTS_VALU x 4 / (1024 x 2.4 GHz) is the least time its vector
+# instruction stream takes on the whole chip (a lower bound: transcendentals and DVFS only add).
+VALU_SIMDS, VALU_CYC, CLOCK_GHZ = 1024, 4, 2.4
 DELTA_MS = 16.667       # fixed AutoExposure step (SURVEY §8d determinism settings)
 PMC_FILE = os.path.join(ROOT, "profiles", "r05_pmc_kernels.json")  # tools/prof.sh pmc of the pipelined frames
-PMC_C2C4 = os.path.join(ROOT, "profiles", "r04_pmc_c2c4.json")  # tools/prof_r04_c2c4.sh (configs 2 and 4)
+PMC_C2C4 = os.path.join(ROOT, "profiles", "r05_pmc_c2c4.json")  # KEY=c2c4 tools/prof.sh pmc probe.py c2c4
 TERRAIN_CAM = dict(pos=(8.0, 15.0, -6.0), yaw=0.0, pitch=-0.7)  # ~50 % primary hits (tests' camera)
 
 # algorithmic bytes: per node visit the 64-B node record, per triangle test the
@@ -291,13 +296,57 @@ def kernel_roofline(q, W, rows, S, kernels_ms, pmc, workload_matches):
     return out
 
 
+def valu_issue_us(insts):
+    """least time a kernel's SQ_INSTS_VALU wave-instructions take to issue on the whole chip"""
+    return insts * VALU_CYC / VALU_SIMDS / (CLOCK_GHZ * 1e3)
+
+
+# the denoise kernels' HIP-event names (by position in the chain) -> their PMC names when the frame
+# runs the active-tile-list chain (DESIGN.md §4.2): the list kernels replace the full-frame ones
+PMC_LIST_NAMES = {"k_spatial7": "k_spatial7_list", "k_spatial5<3>": "k_spatial5_list<3>",
+                  "k_spatial5<6>": "k_spatial5_list<6>"}
+
+
+def pmc_entry(pmc, k):
+    ks = pmc.get("kernels", {})
+    return ks.get(PMC_LIST_NAMES.get(k, k)) or ks.get(k)
+
+
 def add_pmc(e, k, pmc, workload_matches):
-    if pmc and workload_matches and k in pmc.get("kernels", {}):
-        pk = pmc["kernels"][k]
+    if pmc and workload_matches and pmc_entry(pmc, k):
+        pk = pmc_entry(pmc, k)
         for f in ("hbm_bytes", "l2_hit_rate", "wait_inst_any_frac", "wait_any_frac", "valu_busy_frac",
                   "valu_per_wave"):
             if f in pk:
                 e[f] = pk[f]
+        insts = pk.get("counters_median", {}).get("SQ_INSTS_VALU")
+        if insts:
+            e["valu_wave_insts"] = int(insts)
+            e["valu_issue_us"] = round(valu_issue_us(insts), 2)
+
+
+def frame_valu_issue(kernels, ms_per_step, pmc, workload_matches):
+    """The frame's vector-instruction issue bound: the VALU wave-instructions of every kernel of a
+    frame (PMC medians per dispatch, one dispatch each per frame) issued at the chip's full rate,
+    against the measured frame time.  Near 1 means the frame is bound by instruction issue, not by
+    memory: what shortens it is fewer instructions (or packed ones), not more overlap."""
+    if not (pmc and workload_matches):
+        return None
+    per = {}
+    for k in kernels:
+        pk = pmc_entry(pmc, k)
+        insts = (pk or {}).get("counters_median", {}).get("SQ_INSTS_VALU")
+        if insts:
+            per[k] = int(insts)
+    if not per:
+        return None
+    tot = sum(per.values())
+    us = valu_issue_us(tot)
+    return {"valu_wave_insts": tot, "issue_ms": round(us / 1e3, 4), "frame_ms": ms_per_step,
+            "frac": round(us / 1e3 / ms_per_step, 4),
+            "by_kernel_us": {k: round(valu_issue_us(v), 2) for k, v in sorted(per.items(), key=lambda kv: -kv[1])},
+            "model": "SQ_INSTS_VALU x %d cycles / (%d SIMDs x %.1f GHz)" % (VALU_CYC, VALU_SIMDS, CLOCK_GHZ),
+            "source": os.path.relpath(PMC_FILE, ROOT)}
 
 
 def denoise_roofline(st, Ws, Hs, kernels_ms, pmc, workload_matches):
@@ -328,16 +377,31 @@ def stream_kernels(shade_on_side):
 
 def pmc_c2c4(kernel, key):
     """HBM bytes per launch and L2 hit rate of a config-2 / config-4 kernel from the committed PMC
-    passes (tools/prof_r04_c2c4.sh -> profiles/r04_pmc_c2c4.json), when its workload matches."""
+    passes (KEY=c2c4 tools/prof.sh <dir> pmc tools/probe.py c2c4 -> profiles/r05_pmc_c2c4.json), when
+    its workload matches: k_trace_primary of the 1920x1080 1-spp launch, and the LBVH build of the
+    958,720-triangle scene (the build launch with the most workgroups of that run)."""
     if not os.path.exists(PMC_C2C4):
         return {}
     with open(PMC_C2C4) as f:
         pm = json.load(f)
-    if pm.get("workload_key", {}).get(kernel) != key or kernel not in pm.get("kernels", {}):
+    if pm.get("workload_key") != "c2c4":
         return {}
-    e = pm["kernels"][kernel]
-    return {k: e[k] for k in ("hbm_bytes", "l2_hit_rate", "valu_busy_frac", "wait_any_frac") if k in e} | {
-        "traffic_source": os.path.relpath(PMC_C2C4, ROOT)}
+    ks = pm.get("kernels", {})
+    if kernel.startswith("k_build_bvh"):
+        builds = [k for k in ks if k.startswith("k_build_bvh@")]
+        if not builds or key != "958720 tris":
+            return {}
+        kernel = max(builds, key=lambda k: int(k.split("@")[1].rstrip("wg")))
+    elif key != "1920x1080x1 primary":
+        return {}
+    e = ks.get(kernel)
+    if not e:
+        return {}
+    out = {k: e[k] for k in ("hbm_bytes", "l2_hit_rate", "valu_busy_frac", "wait_any_frac") if k in e}
+    insts = e.get("counters_median", {}).get("SQ_INSTS_VALU")
+    if insts:
+        out["valu_issue_us"] = round(valu_issue_us(insts), 2)
+    return out | {"pmc_kernel": kernel, "traffic_source": os.path.relpath(PMC_C2C4, ROOT)}
 
 
 def primary_roofline(rt, W, H, ms, frames):
@@ -743,6 +807,7 @@ def main():
                     "HBM; its time is the noise-gated tiles' stencil arithmetic and its waves' wait for issue slots "
                     "beside the next frame's path-trace waves (valu_busy_frac: share of wave time issuing VALU)")),
         "kernels": dict(per, **dn),
+        "valu_issue": frame_valu_issue(list(per) + list(dn), ms_per_step, pmc, matches),
         "denoise_gating": dst,
         "stage": {"kernels": " -> ".join(per), "algorithmic_bytes": stage_bytes, "sum_kernel_ms": round(stage_ms, 5),
                   "achieved_GBs": round(stage_bytes / (stage_ms * 1e-3) / 1e9, 1),

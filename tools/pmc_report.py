@@ -4,8 +4,8 @@
     python tools/pmc_report.py <out.json> <pass_dir>... [--key KEY] [--workload TEXT]
 
 Kernels are named by their symbol with boolean template arguments dropped and integer ones kept
-(k_spatial5<3, false> -> k_spatial5<3>, k_temporal<true> -> k_temporal); k_build_bvh is labelled by
-its workgroup count (k_build_bvh@61wg, @938wg).  Per kernel the median per-dispatch value of every
+(k_spatial5<3, false> -> k_spatial5<3>, k_temporal<true> -> k_temporal; k_scale_post<576> ->
+k_scale_post); k_build_bvh<threads> is labelled by its workgroup count (k_build_bvh@61wg, @938wg).  Per kernel the median per-dispatch value of every
 counter is taken, then (MI355X_MICROARCH.md HBM, L2 and SQ sections):
   hbm_bytes          = (2 * FETCH_SIZE + WRITE_SIZE) * 1024   (FETCH_SIZE, KB, counts half the bytes
                        of wide reads on gfx950, so it is doubled; WRITE_SIZE in KB)
@@ -35,8 +35,9 @@ def short(name, grid, wg):
     n = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
     n = re.sub(r"<(\d+)(, (true|false))+>", r"<\1>", n)
     n = re.sub(r"<(true|false)(, (true|false))*>", "", n)
-    if n == "k_build_bvh" and wg:
-        n += "@%dwg" % (grid // wg)
+    n = re.sub(r"^k_scale_post<\d+>$", "k_scale_post", n)  # its LDS tile size (24 x 24 or 48 x 48)
+    if n.startswith("k_build_bvh") and wg:
+        n = "k_build_bvh@%dwg" % (grid // wg)
     return n
 
 

@@ -19,6 +19,7 @@
 #include "pt_common.h"
 #include "rt_device.h"
 #include "rtmath.h"
+#include "rtmath_pk.h"
 
 using namespace rtd;
 
@@ -44,6 +45,13 @@ constexpr float kRayMaxF = 10e10f;
 #define DN_EXP(a) (a)
 #else
 #define DN_EXP(a) rt_expf(a)
+#endif
+#ifndef RTX_DN_PK
+#define RTX_DN_PK 1
+#endif
+constexpr bool kDnPk = RTX_DN_PK != 0;  // the a-trous list chain's paired tap weights (rtmath_pk.h)
+#ifndef RTX_DN_PKB
+#define RTX_DN_PKB 4  // taps per load batch with paired weights (even)
 #endif
 #ifndef RTX_DN_BATCH
 #define RTX_DN_BATCH 5
@@ -251,14 +259,14 @@ RT_DEV bool list_tile(const DenoisePostParams& P, int list, uint32_t& tile) {
 }
 
 // ------------------------------------------------------------------ TemporalFilter
-template <bool kRcp>
+template <bool kRcp, bool kPk>
 RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, int y);
 
 // kNoise: also the tile noise levels of the output (noise_epilogue); kList: and the tile's place on
 // the active-tile lists (above), with the output of a tile SpatialFilter7x7 leaves unchanged also
 // written to this frame's accumulation buffer (P.accumAlt: P.accum, the previous frame's, is read
 // at reprojected positions by every workgroup); kRcp: the depth weight's division by reciprocal
-template <bool kNoise, bool kList, bool kRcp>
+template <bool kNoise, bool kList, bool kRcp, bool kPk = false>
 __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uint2* in, uint2* out) {
     DN_PRIO();
     __shared__ uint2 sOut[kNoise ? 256 : 1];
@@ -269,7 +277,7 @@ __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uin
     if (kList && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2 * kListParts)  // the other parity's
         *list_counter(P, P.tileParity ^ 1, (int)threadIdx.x / kListParts, (int)threadIdx.x % kListParts) = 0u;
     if (x < W && y < H) {
-        const uint2 res = temporal_pixel<kRcp>(P, in, x, y);
+        const uint2 res = temporal_pixel<kRcp, kPk>(P, in, x, y);
         out[(size_t)y * W + x] = res;
         if (kNoise) sOut[threadIdx.x] = res;
         if (P.histDepthInTemporal) P.histDepth[(size_t)y * W + x] = P.depth[(size_t)y * W + x];
@@ -291,7 +299,7 @@ __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uin
     }
 }
 
-template <bool kRcp>
+template <bool kRcp, bool kPk>
 RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, int y) {
     const int W = (int)P.W, H = (int)P.H;
     const View2 col{in, W, H}, nrm{P.normal, W, H}, acc{P.accum, (int)P.histW, (int)P.histH};
@@ -305,6 +313,7 @@ RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, 
     const uint32_t mV = mask_of(c0);
     if (dV != dV) dV = 0.0f;
     if (isnan3(nV)) nV = f3(0.0f);
+    const bool yOdd = kPk && rtpk::pow_y_odd(P.dn.temporal_denoise_sigma_normal);
     if (!isnan3(cV) && dV < kRayMaxF) {
         F3 nMax = ycocg(cV), nMin = ycocg(cV);
         F3 filt = f3(0.0f);
@@ -319,19 +328,40 @@ RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, 
             dv[j] = dep.at(sx, sy);
             nq[j] = nrm.at(sx, sy);
         }
+        float wv[9];
 #pragma unroll
-        for (int j = 0; j < 9; ++j) {
-            const int xo = j % 3, yo = j / 3;
-            const uint2 q = qv[j];
-            const F3 cc = rgb_of(q);
-            const float d = dv[j];
-            const F3 n = rgb_of(nq[j]);
-            float w = 1.0f;
-            w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.temporal_denoise_sigma_normal);
-            const float dd = depth_ratio<kRcp>(P, 0, dV - d, P.dn.temporal_denoise_sigma_depth);
-            w *= DN_EXP(-0.5f * dd * dd);
-            w *= (mV != mask_of(q)) ? 1.0f / P.dn.temporal_denoise_sigma_material : 1.0f;
-            w *= cG3[xo + yo * 3];
+        for (int j = 0; j < 9; j += (kPk ? 2 : 1)) {
+            if (kPk && j + 1 < 9) {  // taps j, j + 1 as one register pair (rtmath_pk.h)
+                using rtpk::F2;
+                const F3 n0 = rgb_of(nq[j]), n1 = rgb_of(nq[j + 1]);
+                const F2 dt = rtpk::inner3_2(nV.x, F2{n0.x, n1.x}, nV.y, F2{n0.y, n1.y}, nV.z, F2{n0.z, n1.z});
+                const F2 pw = rtpk::pow_pos2(F2{fmaxf(dt.x, 0.0f), fmaxf(dt.y, 0.0f)},
+                                             P.dn.temporal_denoise_sigma_normal, yOdd);
+                const F2 dz = F2{dV - dv[j], dV - dv[j + 1]};
+                const float sd = P.dn.temporal_denoise_sigma_depth;
+                const F2 dd = kRcp ? rtpk::div_rcp2(dz, sd, P.rcpDepth[0]) : F2{dz.x / sd, dz.y / sd};
+                const F2 ew = rtpk::expf2((rtpk::splat(-0.5f) * dd) * dd);
+                const float mw = 1.0f / P.dn.temporal_denoise_sigma_material;
+                F2 w = pw * ew;
+                w = w * F2{mV != mask_of(qv[j]) ? mw : 1.0f, mV != mask_of(qv[j + 1]) ? mw : 1.0f};
+                w = w * F2{cG3[j], cG3[j + 1]};
+                wv[j] = w.x;
+                wv[j + 1] = w.y;
+            } else {
+                const F3 n = rgb_of(nq[j]);
+                float w = 1.0f;
+                w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.temporal_denoise_sigma_normal);
+                const float dd = depth_ratio<kRcp>(P, 0, dV - dv[j], P.dn.temporal_denoise_sigma_depth);
+                w *= DN_EXP(-0.5f * dd * dd);
+                w *= (mV != mask_of(qv[j])) ? 1.0f / P.dn.temporal_denoise_sigma_material : 1.0f;
+                w *= cG3[j];  // (j % 3) + (j / 3) * 3
+                wv[j] = w;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {  // the sums in tap order
+            const F3 cc = rgb_of(qv[j]);
+            const float w = wv[j];
             filt = filt + cc * w;
             wsum += w;
             const F3 nc = ycocg(cc);
@@ -435,7 +465,7 @@ __global__ __launch_bounds__(256) void k_noise_visualize(DenoisePostParams P, ui
 
 // ------------------------------------------------------------------ SpatialFilter7x7
 // 16x16 tile + 3-pixel apron staged in LDS (22 x 22 entries of colour, normal, depth).
-template <int kParity, bool kRcp>
+template <int kParity, bool kRcp, bool kPk = false>
 RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD, int tx,
                             int ty);
 
@@ -449,7 +479,7 @@ struct S7Lds {
 
 // one 16x16 tile (BX, TY) of SpatialFilter7x7 into `out`: the apron staged (when filtered), the
 // pixel filtered or copied (gated), the result also kept in L.Out for a noise epilogue
-template <bool kRcp>
+template <bool kRcp, bool kPk = false>
 RT_DEV void spatial7_tile(const DenoisePostParams& P, const uint2* in, uint2* out, S7Lds& L, int BX, int TY,
                           bool gated, int lid) {
     const int W = (int)P.W, H = (int)P.H;
@@ -470,8 +500,8 @@ RT_DEV void spatial7_tile(const DenoisePostParams& P, const uint2* in, uint2* ou
         const size_t p = (size_t)y * W + x;
         // the tap set alternates with the frame parity: both sets compiled with constant offsets
         const uint2 res = gated ? in[p]
-                          : (P.frameNum % 2 == 0 ? spatial7_pixel<0, kRcp>(P, L.C, L.N, L.D, tx, ty)
-                                                 : spatial7_pixel<1, kRcp>(P, L.C, L.N, L.D, tx, ty));
+                          : (P.frameNum % 2 == 0 ? spatial7_pixel<0, kRcp, kPk>(P, L.C, L.N, L.D, tx, ty)
+                                                 : spatial7_pixel<1, kRcp, kPk>(P, L.C, L.N, L.D, tx, ty));
         out[p] = res;
         L.Out[lid] = res;
     }
@@ -492,7 +522,7 @@ __global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uin
 
 // SpatialFilter7x7 over active-tile list 0 only (tile rows outside [ty0, ty1) are skipped), with the
 // noise epilogue, which puts tiles above the large threshold on list 1
-template <bool kRcp>
+template <bool kRcp, bool kPk = false>
 __global__ __launch_bounds__(256) void k_spatial7_list(DenoisePostParams P, const uint2* in, uint2* out) {
     DN_PRIO();
     __shared__ S7Lds L;
@@ -501,13 +531,44 @@ __global__ __launch_bounds__(256) void k_spatial7_list(DenoisePostParams P, cons
     if (!list_tile(P, 0, tile)) return;
     const int BX = (int)(tile % (uint32_t)W16), TY = (int)(tile / (uint32_t)W16);
     if (TY < P.ty0 || TY >= P.ty1) return;
-    spatial7_tile<kRcp>(P, in, out, L, BX, TY, false, (int)threadIdx.x);
+    spatial7_tile<kRcp, kPk>(P, in, out, L, BX, TY, false, (int)threadIdx.x);
     __syncthreads();
     const float n16 = noise_epilogue(P, L.Out, L.N8, BX, TY);
     if (threadIdx.x == 0 && !(n16 < P.dn.noise_threshold_large)) list_append(P, 1, tile);
 }
 
-template <int kParity, bool kRcp>
+// the weight of one SpatialFilter7x7 tap (tap d, n already sanitised)
+template <bool kRcp>
+RT_DEV float spatial7_weight(const DenoisePostParams& P, F3 nV, float dV, uint32_t mV, uint32_t mq, float d, F3 n,
+                             int g) {
+    float w = 1.0f;
+    w *= DN_POW(fmaxf(dot(nV, n), 0.0001f), P.dn.local_denoise_sigma_normal);
+    const float dd = depth_ratio<kRcp>(P, 1, dV - d, P.dn.local_denoise_sigma_depth);
+    w *= DN_EXP(-0.5f * dd * dd);
+    w *= (mV != mq) ? 1.0f / P.dn.local_denoise_sigma_material : 1.0f;
+    w *= cG7[g];
+    return w;
+}
+
+// two taps' weights as one register pair (spatial5_weight2; the clamped dot is >= 0.0001, so the
+// pair pow's zero case never applies)
+template <bool kRcp>
+RT_DEV rtpk::F2 spatial7_weight2(const DenoisePostParams& P, F3 nV, float dV, uint32_t mV, uint32_t mq0, uint32_t mq1,
+                                 float d0, float d1, F3 n0, F3 n1, int g0, int g1) {
+    using rtpk::F2;
+    const F2 dt = rtpk::inner3_2(nV.x, F2{n0.x, n1.x}, nV.y, F2{n0.y, n1.y}, nV.z, F2{n0.z, n1.z});
+    const F2 pw = rtpk::pow_pos2(F2{fmaxf(dt.x, 0.0001f), fmaxf(dt.y, 0.0001f)}, P.dn.local_denoise_sigma_normal, false);
+    const F2 dz = F2{dV - d0, dV - d1};
+    const float sd = P.dn.local_denoise_sigma_depth;
+    const F2 dd = kRcp ? rtpk::div_rcp2(dz, sd, P.rcpDepth[1]) : F2{dz.x / sd, dz.y / sd};
+    const F2 ew = rtpk::expf2((rtpk::splat(-0.5f) * dd) * dd);
+    const float mw = 1.0f / P.dn.local_denoise_sigma_material;
+    F2 w = pw * ew;
+    w = w * F2{mV != mq0 ? mw : 1.0f, mV != mq1 ? mw : 1.0f};
+    return w * F2{cG7[g0], cG7[g1]};
+}
+
+template <int kParity, bool kRcp, bool kPk>
 RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD, int tx,
                             int ty) {
     const int ci = (tx + 3) + (ty + 3) * 22;
@@ -535,25 +596,34 @@ RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const u
                 dv[m] = sD[li];
                 nq[m] = sN[li];
             }
+            F3 cc[6], n[6];
+            float d[6], w[6];
 #pragma unroll
             for (int m = 0; m < 6; ++m) {
-                const int j = kParity + 2 * (i0 + m);
-                const int xo = j % 7, yo = j / 7;
-                const uint2 q = qv[m];
-                F3 cc = rgb_of(q);
-                float d = dv[m];
-                F3 n = rgb_of(nq[m]);
-                if (isnan3(cc)) cc = f3(0.0f);
-                if (d != d) d = 0.0f;
-                if (isnan3(n)) n = f3(0.0f);
-                float w = 1.0f;
-                w *= DN_POW(fmaxf(dot(nV, n), 0.0001f), P.dn.local_denoise_sigma_normal);
-                const float dd = depth_ratio<kRcp>(P, 1, dV - d, P.dn.local_denoise_sigma_depth);
-                w *= DN_EXP(-0.5f * dd * dd);
-                w *= (mV != mask_of(q)) ? 1.0f / P.dn.local_denoise_sigma_material : 1.0f;
-                w *= cG7[xo + yo * 7];
-                sum = sum + cc * w;
-                sw += w;
+                cc[m] = rgb_of(qv[m]);
+                d[m] = dv[m];
+                n[m] = rgb_of(nq[m]);
+                if (isnan3(cc[m])) cc[m] = f3(0.0f);
+                if (d[m] != d[m]) d[m] = 0.0f;
+                if (isnan3(n[m])) n[m] = f3(0.0f);
+            }
+#pragma unroll
+            for (int m = 0; m < 6; m += (kPk ? 2 : 1)) {
+                const int j = kParity + 2 * (i0 + m), g = j % 7 + (j / 7) * 7;
+                if (kPk) {
+                    const int j1 = j + 2, g1 = j1 % 7 + (j1 / 7) * 7;
+                    const rtpk::F2 w2 = spatial7_weight2<kRcp>(P, nV, dV, mV, mask_of(qv[m]), mask_of(qv[m + 1]), d[m],
+                                                               d[m + 1], n[m], n[m + 1], g, g1);
+                    w[m] = w2.x;
+                    w[m + 1] = w2.y;
+                } else {
+                    w[m] = spatial7_weight<kRcp>(P, nV, dV, mV, mask_of(qv[m]), d[m], n[m], g);
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < 6; ++m) {  // the sums in tap order
+                sum = sum + cc[m] * w[m];
+                sw += w[m];
             }
         }
         if (isnan3(sum)) sum = f3(0.0f);
@@ -579,12 +649,48 @@ RT_DEV uint32_t active_neighbourhood(const DenoisePostParams& P, int TX, int TY)
     return (uint32_t)__ballot(a);
 }
 
+// One tap's weight and weighted colour of SpatialFilterGlobal5x5 (the scalar form)
+template <bool kRcp>
+RT_DEV float spatial5_weight(const DenoisePostParams& P, F3 nV, float dV, uint32_t mV, uint2 q, float d, uint2 nq,
+                             int k) {
+    const F3 n = rgb_of(nq);
+    float w = 1.0f;
+    w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.large_denoise_sigma_normal);
+    const float dd = depth_ratio<kRcp>(P, 2, dV - d, P.dn.large_denoise_sigma_depth);
+    w *= DN_EXP(-0.5f * dd * dd);
+    w *= (mV != mask_of(q)) ? 1.0f / P.dn.large_denoise_sigma_material : 1.0f;
+    w *= cG5[k];
+    return w;
+}
+
+// The weights of taps k and k + 1 as one register pair (rtmath_pk.h: the same operations per
+// element, the polynomial and compensated-dot chains issued once for both); pow's special cases
+// need large_denoise_sigma_normal finite and > 0 (rtpk::pow_pos_ok, checked by the launcher)
+template <bool kRcp>
+RT_DEV rtpk::F2 spatial5_weight2(const DenoisePostParams& P, F3 nV, float dV, uint32_t mV, uint2 q0, uint2 q1, float d0,
+                                 float d1, uint2 nq0, uint2 nq1, int k, bool yOdd) {
+    using rtpk::F2;
+    const F3 n0 = rgb_of(nq0), n1 = rgb_of(nq1);
+    const F2 dt = rtpk::inner3_2(nV.x, F2{n0.x, n1.x}, nV.y, F2{n0.y, n1.y}, nV.z, F2{n0.z, n1.z});
+    const F2 pw = rtpk::pow_pos2(F2{fmaxf(dt.x, 0.0f), fmaxf(dt.y, 0.0f)}, P.dn.large_denoise_sigma_normal, yOdd);
+    const F2 dz = F2{dV - d0, dV - d1};
+    const float sd = P.dn.large_denoise_sigma_depth;
+    const F2 dd = kRcp ? rtpk::div_rcp2(dz, sd, P.rcpDepth[2]) : F2{dz.x / sd, dz.y / sd};
+    const F2 ew = rtpk::expf2((rtpk::splat(-0.5f) * dd) * dd);
+    const float mw = 1.0f / P.dn.large_denoise_sigma_material;
+    F2 w = pw * ew;
+    w = w * F2{mV != mask_of(q0) ? mw : 1.0f, mV != mask_of(q1) ? mw : 1.0f};
+    return w * F2{cG5[k], cG5[k + 1]};
+}
+
 // One pixel of SpatialFilterGlobal5x5<S> in a filtered tile (TX, TY).  kRedirect: `in` holds only
 // the list-1 tiles, so a tap whose (clamped) texel lies in a tile off the list (its bit clear in
-// `act`) reads `alt`, the accumulation buffer those tiles would have been copied from.
-template <int S, bool kRcp, bool kRedirect>
+// `act`) reads `alt`, the accumulation buffer those tiles would have been copied from.  kPk: tap
+// weights two at a time (spatial5_weight2), batches of six taps.
+template <int S, bool kRcp, bool kRedirect, bool kPk = false>
 RT_DEV uint2 spatial5_pixel(const DenoisePostParams& P, const uint2* in, const uint2* alt, uint32_t act, int x, int y,
                             int TX, int TY) {
+    constexpr int kB = kPk ? RTX_DN_PKB : kDnBatch;
     const int W = (int)P.W, H = (int)P.H;
     const size_t p = (size_t)y * W + x;
     const uint2 c0 = in[p];
@@ -596,18 +702,19 @@ RT_DEV uint2 spatial5_pixel(const DenoisePostParams& P, const uint2* in, const u
     if (isnan3(cV)) cV = f3(0.0f);
     if (dV != dV) dV = 0.0f;
     if (isnan3(nV)) nV = f3(0.0f);
+    const bool yOdd = kPk && rtpk::pow_y_odd(P.dn.large_denoise_sigma_normal);
     if (dV < 10e9f) {
         F3 sum = f3(0.0f);
         float sw = 0.0f;
-        // taps in batches of kDnBatch: a batch's loads are issued together, then its weights
-        // computed (the branches of rt_powf otherwise keep the compiler from hoisting the next
-        // tap's loads, one memory round trip per tap)
+        // taps in batches of kB: a batch's loads are issued together, then its weights computed
+        // (the branches of rt_powf otherwise keep the compiler from hoisting the next tap's loads,
+        // one memory round trip per tap)
 #pragma unroll
-        for (int k0 = 0; k0 < 25; k0 += kDnBatch) {
-            uint2 qv[kDnBatch], nq[kDnBatch];
-            float dv[kDnBatch];
+        for (int k0 = 0; k0 < 25; k0 += kB) {
+            uint2 qv[kB], nq[kB];
+            float dv[kB];
 #pragma unroll
-            for (int m = 0; m < kDnBatch; ++m) {
+            for (int m = 0; m < kB; ++m) {
                 const int k = k0 + m < 25 ? k0 + m : 24;
                 const int cx = clampi(x + (k % 5 - 2) * S, 0, W - 1), cy = clampi(y + (k / 5 - 2) * S, 0, H - 1);
                 const size_t q = (size_t)cy * W + cx;
@@ -620,21 +727,25 @@ RT_DEV uint2 spatial5_pixel(const DenoisePostParams& P, const uint2* in, const u
                 dv[m] = h2f(P.depth[q]);
                 nq[m] = P.normal[q];
             }
+            float wv[kB];
 #pragma unroll
-            for (int m = 0; m < kDnBatch; ++m) {
+            for (int m = 0; m < kB; ++m) {
                 const int k = k0 + m;
                 if (k >= 25) break;
-                const int i = k % 5, j = k / 5;
-                const uint2 q = qv[m];
-                F3 cc = rgb_of(q);
-                const float d = dv[m];
-                const F3 n = rgb_of(nq[m]);
-                float w = 1.0f;
-                w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.large_denoise_sigma_normal);
-                const float dd = depth_ratio<kRcp>(P, 2, dV - d, P.dn.large_denoise_sigma_depth);
-                w *= DN_EXP(-0.5f * dd * dd);
-                w *= (mV != mask_of(q)) ? 1.0f / P.dn.large_denoise_sigma_material : 1.0f;
-                w *= cG5[i + j * 5];
+                if (kPk && m % 2 == 0 && k + 1 < 25 && m + 1 < kB) {
+                    const rtpk::F2 w2 = spatial5_weight2<kRcp>(P, nV, dV, mV, qv[m], qv[m + 1], dv[m], dv[m + 1],
+                                                               nq[m], nq[m + 1], k, yOdd);
+                    wv[m] = w2.x;
+                    wv[m + 1] = w2.y;
+                } else if (!kPk || m % 2 == 0) {
+                    wv[m] = spatial5_weight<kRcp>(P, nV, dV, mV, qv[m], dv[m], nq[m], k);
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < kB; ++m) {  // the sums in tap order
+                if (k0 + m >= 25) break;
+                F3 cc = rgb_of(qv[m]);
+                float w = wv[m];
                 if (isnan3(cc)) { cc = f3(0.0f); w = 0.0f; }
                 sum = sum + cc * w;
                 sw += w;
@@ -652,7 +763,7 @@ RT_DEV uint2 spatial5_pixel(const DenoisePostParams& P, const uint2* in, const u
 // every tile of the launch's rows: tiles below the large threshold pass their input through (from
 // `alt` when kRedirect: `in` holds only the list-1 tiles); kAlbedo: ApplyAlbedo (denoising.cu:160-171)
 // fused into the store of the last wide pass
-template <int S, bool kAlbedo, bool kRcp, bool kRedirect>
+template <int S, bool kAlbedo, bool kRcp, bool kRedirect, bool kPk = false>
 __global__ DN5_BOUNDS void k_spatial5(DenoisePostParams P, const uint2* in, uint2* out, const uint2* alt) {
     DN_PRIO();
     const int W = (int)P.W, H = (int)P.H;
@@ -664,14 +775,14 @@ __global__ DN5_BOUNDS void k_spatial5(DenoisePostParams P, const uint2* in, uint
     if (kRedirect && active) act = active_neighbourhood(P, TX, TY);  // before any lane leaves
     if (x >= W || y >= H) return;
     const size_t p = (size_t)y * W + x;
-    uint2 res = active ? spatial5_pixel<S, kRcp, kRedirect>(P, in, alt, act, x, y, TX, TY) : (kRedirect ? alt : in)[p];
+    uint2 res = active ? spatial5_pixel<S, kRcp, kRedirect, kPk>(P, in, alt, act, x, y, TX, TY) : (kRedirect ? alt : in)[p];
     if (kAlbedo) res = pack_color(rgb_of(res) * rgb_of(P.albedo[p]), 0x3C00u);  // w = half(1.0)
     out[p] = res;
 }
 
 // SpatialFilterGlobal5x5<S> over active-tile list 1 only (tile rows outside [ty0, ty1) are skipped):
 // `out` is written in those tiles only
-template <int S, bool kRcp, bool kRedirect>
+template <int S, bool kRcp, bool kRedirect, bool kPk = false>
 __global__ DN5_BOUNDS void k_spatial5_list(DenoisePostParams P, const uint2* in, uint2* out, const uint2* alt) {
     DN_PRIO();
     const int W = (int)P.W, H = (int)P.H, W16 = (W + 15) / 16;
@@ -681,7 +792,7 @@ __global__ DN5_BOUNDS void k_spatial5_list(DenoisePostParams P, const uint2* in,
     if (TY < P.ty0 || TY >= P.ty1) return;
     const uint32_t act = kRedirect ? active_neighbourhood(P, TX, TY) : 0u;
     const int x = TX * 16 + (threadIdx.x & 15), y = TY * 16 + (threadIdx.x >> 4);
-    if (x < W && y < H) out[(size_t)y * W + x] = spatial5_pixel<S, kRcp, kRedirect>(P, in, alt, act, x, y, TX, TY);
+    if (x < W && y < H) out[(size_t)y * W + x] = spatial5_pixel<S, kRcp, kRedirect, kPk>(P, in, alt, act, x, y, TX, TY);
 }
 
 // ------------------------------------------------------------------ ApplyAlbedo (in place, pointwise)
@@ -1069,7 +1180,17 @@ RT_DEV F3 tonemap_color(F3 c, int type, float maxWhite, float gamma) {
         c = f3(0.0f) * f3(__builtin_inff());
     }
     const float g = 1.0f / gamma;
-    const F3 o = f3(rt_powf(c.x, g), rt_powf(c.y, g), rt_powf(c.z, g));
+    F3 o;
+    if (kDnPk && rtpk::pow_pos_ok(g)) {  // red and green as a pair (rtmath_pk.h), x >= 0 finite
+        const float inf = __builtin_inff();
+        const bool ok0 = c.x >= 0.0f && c.x < inf, ok1 = c.y >= 0.0f && c.y < inf;
+        rtpk::F2 r = rtpk::pow_pos2(rtpk::F2{ok0 ? c.x : 1.0f, ok1 ? c.y : 1.0f}, g, rtpk::pow_y_odd(g));
+        if (!ok0) r.x = rt_powf(c.x, g);  // negative, infinite or NaN: rt_powf's special cases
+        if (!ok1) r.y = rt_powf(c.y, g);
+        o = f3(r.x, r.y, rt_powf(c.z, g));
+    } else {
+        o = f3(rt_powf(c.x, g), rt_powf(c.y, g), rt_powf(c.z, g));
+    }
     return clamp3(o, f3(0.0f), f3(1.0f));
 }
 
@@ -1353,6 +1474,17 @@ __global__ __launch_bounds__(256) void k_hdr_out(const uint2* color, float4* hdr
 
 }  // namespace
 
+// the list chain's first two a-trous passes: depth-weight reciprocal x paired tap weights
+template <int S, bool kRedirect>
+static void launch_s5_list(bool rcp, bool pk, dim3 g, hipStream_t s, const DenoisePostParams& Q, const uint2* in,
+                           uint2* out, const uint2* alt) {
+    const dim3 b(256);
+    if (rcp && pk) hipLaunchKernelGGL((k_spatial5_list<S, true, kRedirect, true>), g, b, 0, s, Q, in, out, alt);
+    else if (rcp) hipLaunchKernelGGL((k_spatial5_list<S, true, kRedirect, false>), g, b, 0, s, Q, in, out, alt);
+    else if (pk) hipLaunchKernelGGL((k_spatial5_list<S, false, kRedirect, true>), g, b, 0, s, Q, in, out, alt);
+    else hipLaunchKernelGGL((k_spatial5_list<S, false, kRedirect, false>), g, b, 0, s, Q, in, out, alt);
+}
+
 // k_scale_post's footprint of 18 screen texels along an axis spans at most 17 * r + 5 render
 // texels (r = render / screen: the first tap one before t1, the last two after, one more for the
 // floors' rounding); the small LDS tile holds 24 of them
@@ -1507,6 +1639,12 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
     uint2* const accOut = useList ? P->accumAlt : P->accum;
     P->listUsed = useList ? 1 : 0;
     const bool rcpT = (P->rcpDepthOk & 1) != 0, rcp7 = (P->rcpDepthOk & 2) != 0, rcp5 = (P->rcpDepthOk & 4) != 0;
+    const float sn5 = P->dn.large_denoise_sigma_normal;
+    const bool pk5 = kDnPk && sn5 > 0.0f && sn5 < __builtin_inff();  // rtpk::pow_pos_ok
+    const float sn7 = P->dn.local_denoise_sigma_normal;
+    const bool pk7 = kDnPk && sn7 > 0.0f && sn7 < __builtin_inff();
+    const float snT = P->dn.temporal_denoise_sigma_normal;
+    const bool pkT = kDnPk && snT > 0.0f && snT < __builtin_inff();
     const dim3 gList((unsigned)(kListParts * (P->tileCap / kListParts + 1)));  // one workgroup per list slot
     bool noise1 = false, histDepthDone = false;
     if (P->temporal && P->frameNum != 1) {
@@ -1518,7 +1656,9 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
             Q.histDepthInTemporal = histDepthDone = P->temporal2 && !P->stripLocal && !P->visualize;
             DN_MARK(0, 0);
             if (useList) {
-                if (rcpT) hipLaunchKernelGGL((k_temporal<true, true, true>), g, b256, 0, s, Q, (const uint2*)cur, dst);
+                if (rcpT && pkT) hipLaunchKernelGGL((k_temporal<true, true, true, true>), g, b256, 0, s, Q, (const uint2*)cur, dst);
+                else if (rcpT) hipLaunchKernelGGL((k_temporal<true, true, true>), g, b256, 0, s, Q, (const uint2*)cur, dst);
+                else if (pkT) hipLaunchKernelGGL((k_temporal<true, true, false, true>), g, b256, 0, s, Q, (const uint2*)cur, dst);
                 else hipLaunchKernelGGL((k_temporal<true, true, false>), g, b256, 0, s, Q, (const uint2*)cur, dst);
             } else if (noise1) {
                 if (rcpT) hipLaunchKernelGGL((k_temporal<true, false, true>), g, b256, 0, s, Q, (const uint2*)cur, dst);
@@ -1540,8 +1680,10 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         if (tiles(3, Q, g)) {
             DN_MARK(1, 0);
             if (useList) {  // list 0 only; TemporalFilter wrote the other tiles into the accumulation buffer
-                if (rcp7) hipLaunchKernelGGL(k_spatial7_list<true>, gList, b256, 0, s, Q, (const uint2*)cur, dst);
-                else hipLaunchKernelGGL(k_spatial7_list<false>, gList, b256, 0, s, Q, (const uint2*)cur, dst);
+                if (rcp7 && pk7) hipLaunchKernelGGL((k_spatial7_list<true, true>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
+                else if (rcp7) hipLaunchKernelGGL((k_spatial7_list<true, false>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
+                else if (pk7) hipLaunchKernelGGL((k_spatial7_list<false, true>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
+                else hipLaunchKernelGGL((k_spatial7_list<false, false>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
             } else if (noise2) {
                 if (rcp7) hipLaunchKernelGGL((k_spatial7<true, true>), g, b256, 0, s, Q, (const uint2*)cur, dst);
                 else hipLaunchKernelGGL((k_spatial7<true, false>), g, b256, 0, s, Q, (const uint2*)cur, dst);
@@ -1571,8 +1713,7 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         if (tiles(3, Q, g)) {
             DN_MARK(2, 0);
             if (useList) {
-                if (rcp5) hipLaunchKernelGGL((k_spatial5_list<3, true, false>), gList, b256, 0, s, Q, (const uint2*)cur, a, alt);
-                else hipLaunchKernelGGL((k_spatial5_list<3, false, false>), gList, b256, 0, s, Q, (const uint2*)cur, a, alt);
+                launch_s5_list<3, false>(rcp5, pk5, gList, s, Q, (const uint2*)cur, a, alt);
             } else {
                 if (rcp5) hipLaunchKernelGGL((k_spatial5<3, false, true, false>), g, b256, 0, s, Q, (const uint2*)cur, a, alt);
                 else hipLaunchKernelGGL((k_spatial5<3, false, false, false>), g, b256, 0, s, Q, (const uint2*)cur, a, alt);
@@ -1584,8 +1725,7 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         if (tiles(2, Q, g)) {
             DN_MARK(3, 0);
             if (useList) {
-                if (rcp5) hipLaunchKernelGGL((k_spatial5_list<6, true, true>), gList, b256, 0, s, Q, (const uint2*)a, b, alt);
-                else hipLaunchKernelGGL((k_spatial5_list<6, false, true>), gList, b256, 0, s, Q, (const uint2*)a, b, alt);
+                launch_s5_list<6, true>(rcp5, pk5, gList, s, Q, (const uint2*)a, b, alt);
             } else {
                 if (rcp5) hipLaunchKernelGGL((k_spatial5<6, false, true, false>), g, b256, 0, s, Q, (const uint2*)a, b, alt);
                 else hipLaunchKernelGGL((k_spatial5<6, false, false, false>), g, b256, 0, s, Q, (const uint2*)a, b, alt);
@@ -1596,7 +1736,9 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         if (tiles(1, Q, g)) {
             DN_MARK(4, 0);
             if (useList) {
-                if (rcp5) hipLaunchKernelGGL((k_spatial5<12, true, true, true>), g, b256, 0, s, Q, (const uint2*)b, a, alt);
+                if (rcp5 && pk5) hipLaunchKernelGGL((k_spatial5<12, true, true, true, true>), g, b256, 0, s, Q, (const uint2*)b, a, alt);
+                else if (rcp5) hipLaunchKernelGGL((k_spatial5<12, true, true, true>), g, b256, 0, s, Q, (const uint2*)b, a, alt);
+                else if (pk5) hipLaunchKernelGGL((k_spatial5<12, true, false, true, true>), g, b256, 0, s, Q, (const uint2*)b, a, alt);
                 else hipLaunchKernelGGL((k_spatial5<12, true, false, true>), g, b256, 0, s, Q, (const uint2*)b, a, alt);
             } else {
                 if (rcp5) hipLaunchKernelGGL((k_spatial5<12, true, true, false>), g, b256, 0, s, Q, (const uint2*)b, a, alt);

@@ -483,9 +483,7 @@ RT_DEV void sort_and_build(Lds<kThr>& s, const float* leafG, int n, uint32_t* mo
     karras(s, n);
     __syncthreads();
     BVH_STAMP(4);
-#if !(defined(RTX_BVH_ABL) && RTX_BVH_ABL == 3)
-    refit<kThr, true>(s, leafG, n, nodes, w);  // (ablation 3: no refit; timing only)
-#endif
+    refit<kThr, true>(s, leafG, n, nodes, w);
 }
 
 // the TLAS's child words: internal nodes after the B*1024 BLAS slots, leaves at their BLAS roots
@@ -572,10 +570,6 @@ RT_DEV void tlas_builder(Lds<kThr>& s, const BvhBuildParams& P, uint32_t B) {
     constexpr int kPer = kBatch / kThr;
     const int t = threadIdx.x;
     tlas_wait(P, B);
-#if defined(RTX_BVH_ABL) && RTX_BVH_ABL == 1
-    if (t == 0) tlas_rearm(P, B);
-    return;  // timing ablation: no TLAS
-#endif
     if (B <= kTlasWaveMax) {  // wave 0 alone
         if (t < 64) tlas_wave(s, P, B);
 #ifdef RTX_BVH_STAMPS

@@ -35,38 +35,18 @@ namespace {
 
 constexpr float kRayMaxF = 10e10f;
 
-// ablation switches for profiling builds only (tools/abl_build.sh); the product build defines none
-#ifdef RTX_ABL_DN_NOPOW
-#define DN_POW(a, b) (a)
-#else
 #define DN_POW(a, b) rt_powf(a, b)
-#endif
-#ifdef RTX_ABL_DN_NOEXP
-#define DN_EXP(a) (a)
-#else
 #define DN_EXP(a) rt_expf(a)
-#endif
+// compile-time switches of A/B builds (tools/abl_build.sh "-DRTX_DN_PK=0" ...); the defaults are the product
 #ifndef RTX_DN_PK
 #define RTX_DN_PK 1
 #endif
-constexpr bool kDnPk = RTX_DN_PK != 0;  // the a-trous list chain's paired tap weights (rtmath_pk.h)
+constexpr bool kDnPk = RTX_DN_PK != 0;  // paired tap weights (rtmath_pk.h)
 #ifndef RTX_DN_PKB
 #define RTX_DN_PKB 4  // taps per load batch with paired weights (even)
 #endif
-#ifndef RTX_DN_BATCH
-#define RTX_DN_BATCH 5
-#endif
-constexpr int kDnBatch = RTX_DN_BATCH;  // SpatialFilterGlobal5x5 taps per load batch
-#if defined(RTX_DN5_WAVES) && RTX_DN5_WAVES > 0
-#define DN5_BOUNDS __launch_bounds__(256, RTX_DN5_WAVES)
-#else
+constexpr int kDnBatch = 5;  // SpatialFilterGlobal5x5 taps per load batch (unpaired)
 #define DN5_BOUNDS __launch_bounds__(256)
-#endif
-#ifdef RTX_ABL_DN_GATEALL
-constexpr bool kDnGateAll = true;
-#else
-constexpr bool kDnGateAll = false;
-#endif
 
 // gaussian.cuh:12-43 (double literals converted to float, as the reference's float arrays)
 __constant__ float cG3[9] = RT_GAUSS3_INIT;
@@ -512,7 +492,7 @@ __global__ __launch_bounds__(256) void k_spatial7(DenoisePostParams P, const uin
     DN_PRIO();
     __shared__ S7Lds L;
     const int TY = tile_y(P), W16 = ((int)P.W + 15) / 16;
-    const bool gated = kDnGateAll || h2f(P.noise16[TY * W16 + tile_x(P)]) < P.dn.noise_threshold_local;
+    const bool gated = h2f(P.noise16[TY * W16 + tile_x(P)]) < P.dn.noise_threshold_local;
     spatial7_tile<kRcp>(P, in, out, L, tile_x(P), TY, gated, (int)threadIdx.x);
     if (kNoise) {
         __syncthreads();
@@ -770,7 +750,7 @@ __global__ DN5_BOUNDS void k_spatial5(DenoisePostParams P, const uint2* in, uint
     const int TX = tile_x(P), TY = tile_y(P);
     const int x = TX * 16 + (threadIdx.x & 15), y = TY * 16 + (threadIdx.x >> 4);
     const int W16 = (W + 15) / 16;
-    const bool active = !kDnGateAll && !(h2f(P.noise16[TY * W16 + TX]) < P.dn.noise_threshold_large);
+    const bool active = !(h2f(P.noise16[TY * W16 + TX]) < P.dn.noise_threshold_large);
     uint32_t act = 0u;
     if (kRedirect && active) act = active_neighbourhood(P, TX, TY);  // before any lane leaves
     if (x >= W || y >= H) return;
@@ -1415,11 +1395,7 @@ __global__ __launch_bounds__(kScaleThreads) void k_scale_post(DenoisePostParams 
         }
     } im{sS, X0, Y0, Ws, Hs};
     uint2 cur = im.at(x, y);
-#if defined(RTX_SP_ABL) && RTX_SP_ABL == 4  // timing ablation only: no sharpen
-    if (false) {
-#else
     if (P.sharpen) {
-#endif
         F3 c[3][3];
 #pragma unroll
         for (int i = 0; i < 3; ++i)
@@ -1443,22 +1419,15 @@ __global__ __launch_bounds__(kScaleThreads) void k_scale_post(DenoisePostParams 
         o = o / (f3(1.0f) + f3(4.0f) * w);
         cur = pack_color(o, 0x3C00u);
     }
-#if !(defined(RTX_SP_ABL) && RTX_SP_ABL == 2)  // timing ablation only: no tone map
     if (P.tonemap) {
         const F3 c = tonemap_color(rgb_of(cur) * P.exposure[0], P.toneMappingType, P.maxWhite, P.gamma);
         cur = pack_color(c, 0x3C00u);
     }
-#endif
     P.scaledB[p] = cur;
     // CopyToOutput (kernel.cu:26-59): blue-noise dither (bn/256; the -1/512 is integer 0)
     const int s = P.frameNum;
-#if defined(RTX_SP_ABL) && RTX_SP_ABL == 3  // timing ablation only: no dither
-    F3 c = rgb_of(cur);
-    (void)s;
-#else
     F3 c = rgb_of(cur) + f3(bn_value(sSobol, bnp, s, 0) / 256, bn_value(sSobol, bnp, s, 1) / 256,
                             bn_value(sSobol, bnp, s, 2) / 256);
-#endif
     const float hi = 1.0f - 1.1920928955078125e-07f;
     c = clamp3(c, f3(0.0f), f3(hi));
     P.rgba[(size_t)y * P.rgbaPitch + x] = (uint32_t)(uint8_t)(c.x * 256) | ((uint32_t)(uint8_t)(c.y * 256) << 8) |
@@ -1635,7 +1604,7 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
     // it also writes tiles of this frame's, so the list chain writes the other buffer of a pair
     // (accumAlt; the host swaps them) — not with a caller-bound buffer, nor a strip-local denoise
     const bool useList = P->tileList && P->accumAlt && !P->stripLocal && P->temporal && P->frameNum != 1 &&
-                         P->localSpatial && P->wideSpatial && !P->visualize && !kDnGateAll;
+                         P->localSpatial && P->wideSpatial && !P->visualize;
     uint2* const accOut = useList ? P->accumAlt : P->accum;
     P->listUsed = useList ? 1 : 0;
     const bool rcpT = (P->rcpDepthOk & 1) != 0, rcp7 = (P->rcpDepthOk & 2) != 0, rcp5 = (P->rcpDepthOk & 4) != 0;
@@ -1721,7 +1690,6 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
             LAUNCH_CHECK();
             DN_MARK(2, 1);
         }
-#if !(defined(RTX_DN_ABL) && RTX_DN_ABL == 1)  // timing ablation only: two a-trous passes fewer
         if (tiles(2, Q, g)) {
             DN_MARK(3, 0);
             if (useList) {
@@ -1747,7 +1715,6 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
             LAUNCH_CHECK();
             DN_MARK(4, 1);
         }
-#endif
         cur = a;
         spare = b;
     } else {  // out of place when cur is the accumulation buffer (the next frame's history)

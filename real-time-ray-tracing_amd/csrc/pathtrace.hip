@@ -436,13 +436,8 @@ inline bool one_round(uint32_t spp) { return spp >= 1 && ((int)spp + cam_sample_
 //
 // kOneRound: every sample wave runs one round (spp <= 4 except 3: the launcher checks), so the
 // round loop and its carried state compile away.
-#ifdef RTX_CAM_WPE  // ablation builds only: forced waves per SIMD
-#define RTX_CAM_ATTR __attribute__((amdgpu_waves_per_eu(RTX_CAM_WPE, RTX_CAM_WPE)))
-#else
-#define RTX_CAM_ATTR
-#endif
 template <bool kOneRound>
-__global__ __launch_bounds__(256, kOneRound ? 6 : 4) RTX_CAM_ATTR void k_pt_camera(PathTraceParams P) {
+__global__ __launch_bounds__(256, kOneRound ? 6 : 4) void k_pt_camera(PathTraceParams P) {
     // stack entries in LDS (the rest in registers): 26 KB per workgroup, 6 workgroups per CU
     // (measured: 16 entries 4 per CU 0.948 ms/frame, 12 entries 5 per CU 0.918, 10 entries 6 per CU
     // 0.900; the default scene's rays hold at most 11 entries)
@@ -485,11 +480,7 @@ __global__ __launch_bounds__(256, kOneRound ? 6 : 4) RTX_CAM_ATTR void k_pt_came
             generate_ray_jittered(P.cam, x, y, F2{rnd(c, 0, 0), rnd(c, 0, 1)}, F2{rnd(c, 0, 2), rnd(c, 0, 3)}, org,
                                   dir, uv);
             TravState st;
-#if defined(RTX_CAM_ABL) && RTX_CAM_ABL == 1  // timing ablation only: no traversal (every ray culled)
-            if (true) {
-#else
             if (root_surely_missed(sc, org, dir)) {  // most sky rays: settled without the ray-box helper
-#endif
                 trav_root_miss(st, sc.root);
                 ++camCull;
             } else {
@@ -523,11 +514,7 @@ __global__ __launch_bounds__(256, kOneRound ? 6 : 4) RTX_CAM_ATTR void k_pt_came
                 v.rs.albedo = f3(1.0f);
                 v.beta0 = f3(1.0f);
                 v.beta1 = f3(1.0f);
-#if defined(RTX_CAM_ABL) && RTX_CAM_ABL == 2  // timing ablation only: no sky colour
-                const F3 Ls = dir;
-#else
                 const F3 Ls = finish(c, v);
-#endif
                 out = make_float4(Ls.x, Ls.y, Ls.z, 0.0f);
             }
         }
@@ -805,11 +792,7 @@ RT_DEV void store_path_L(const PathCtx& c, const PathVars& v, uint32_t p, uint32
 
 // Resumes the samples of queue kStep (3 or 4) once k_trace_queue has written their hits.
 template <int kStep, bool kMF>
-#ifndef RTX_CTX_PRIO  // A/B: wave priority (s_setprio) of the context stream's tracers and resume kernels
-#define RTX_CTX_PRIO 0
-#endif
 __global__ __launch_bounds__(256, kMF ? 2 : 3) void k_pt_resume(PathTraceParams P) {
-    if (RTX_CTX_PRIO > 0) __builtin_amdgcn_s_setprio(RTX_CTX_PRIO);
     __shared__ uint32_t sob[256];
     __shared__ unsigned long long wgRays[4];
     // step 4 ends the path before any diffuse interaction: no light sampling there
@@ -972,9 +955,6 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
         }
         // ---- phase 2: resume this wave's entries, trace and finish their I4 rays
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the hit records this wave wrote
-#if defined(RTX_CHAIN_ABL) && RTX_CHAIN_ABL == 1
-        nRanges = 0;  // timing ablation: no phase 2
-#endif
         PathCtx c{P, f3(P.sunDir[0], P.sunDir[1], P.sunDir[2]), sob, BnPixel{0u, 0u}, 0, 0u, 0u, 0u, 0u};
         c.skyTree = P.skyTree;  // the light-CDF heaps from L2: LDS holds the traversal stacks
         c.sunTree = P.sunTree;
@@ -997,9 +977,6 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
                 trav_init(s4, sc.root);
                 TravRec rec4;
                 const bool mine = act;
-#if defined(RTX_CHAIN_ABL) && RTX_CHAIN_ABL == 2
-                act = false;  // timing ablation: I4 rays not traced
-#endif
                 if (nq4 < 16u) {  // few rays: plain per-lane loop (no ballots, no leaf batching)
 #pragma unroll 1
                     while (act)

@@ -29,13 +29,9 @@ constexpr uint32_t kTrace3Short = 1u << 20;  // queue-3 length below which trace
 #define RTX_LEAF_BATCH 1
 #endif
 constexpr bool kLeafBatch = RTX_LEAF_BATCH != 0;  // ablation: -DRTX_LEAF_BATCH=0
-#ifndef RTX_CTX_PRIO  // A/B: wave priority (s_setprio) of the context stream's tracers and resume kernels
-#define RTX_CTX_PRIO 0
-#endif
 
 template <int kStep>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) {
-    if (RTX_CTX_PRIO > 0) __builtin_amdgcn_s_setprio(RTX_CTX_PRIO);
     __shared__ uint2 stk[17 * kTraceBlock];  // 16 entries + the dead slot trav_step stores above the top
     const int tid = threadIdx.x;
     const int lane = (int)__lane_id();

@@ -152,6 +152,8 @@ extern "C" float orc_rtmath(int fn, float x, float y) {
         case 9: return rt_logf(x);
         case 10: return rt_log2f(x);
         case 11: return rt_powf(x, y);
+        case 12: return rt_log2f_div(x);
+        case 13: return rt_powf_div(x, y);
         default: return 0.0f;
     }
 }

@@ -42,8 +42,10 @@
 #define rt_exp2f exp2f
 #define rt_logf logf
 #define rt_log2f log2f
+#define rt_log2f_div log2f
 #define rt_log10f log10f
 #define rt_powf powf
+#define rt_powf_div powf
 #define ORC_EXPD(x) exp(x)
 #else
 #define ORC_EXPD(x) rtm::expd(x)

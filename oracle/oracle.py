@@ -191,7 +191,8 @@ def primary_rays(width: int, height: int, frame_num: int = 1, cam: CameraIn | No
     return rays, cone
 
 
-RTMATH = dict(sin=0, cos=1, tan=2, atan=3, atan2=4, acos=5, asin=6, exp=7, exp2=8, log=9, log2=10, pow=11)
+RTMATH = dict(sin=0, cos=1, tan=2, atan=3, atan2=4, acos=5, asin=6, exp=7, exp2=8, log=9, log2=10, pow=11,
+              log2_div=12, pow_div=13)  # *_div: the path tracer's log2 variant (rtmath.h log2_pair_t)
 
 
 def rtmath(fn: str, x: float, y: float = 0.0) -> float:

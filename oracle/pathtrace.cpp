@@ -405,7 +405,7 @@ static void diffuse(Ctx& c, int bounce, RayState& rs, F3& beta, const float r[4]
     {
         const float uvScale = 0.5f;
         float len = sqrtf(1024.0f * 1024.0f + 1024.0f * 1024.0f);
-        float lod = rt_log2f(rs.rayConeWidth * uvScale * len);
+        float lod = rt_log2f_div(rs.rayConeWidth * uvScale * len);  // the path tracer's log2 variant (rtmath.h log2_pair_t)
         F3 aX, aY, aZ, nX, nY, nZ;
         const uint16_t* T0 = c.f->texAlbedoAo;
         const uint16_t* T1 = c.f->texNormalRough;
@@ -413,7 +413,7 @@ static void diffuse(Ctx& c, int bounce, RayState& rs, F3& beta, const float r[4]
             uv.x *= uvScale;
             uv.y *= uvScale;
             F4 t0 = sample_lod(T0, uv, lod);
-            alb = f3(rt_powf(t0.x, 2.2f), rt_powf(t0.y, 2.2f), rt_powf(t0.z, 2.2f));
+            alb = f3(rt_powf_div(t0.x, 2.2f), rt_powf_div(t0.y, 2.2f), rt_powf_div(t0.z, 2.2f));
             F4 t1 = sample_lod(T1, uv, lod);
             F3 n = f3(t1.x - 0.5f, t1.y - 0.5f, t1.z - 0.5f);
             F3 w = alt ? wAlt : wDefault;

@@ -154,7 +154,7 @@ RT_DEV void tri_plane(const PathTraceParams& P, F2 uv, float lod, F3 normal, F3 
     // scheduling fences: the gamma chain and the normal-map fetches would otherwise interleave,
     // and the live texels of both maps set the register peak of the shading kernels
     __builtin_amdgcn_sched_barrier(0);
-    alb = f3(rt_powf(t0.x, 2.2f), rt_powf(t0.y, 2.2f), rt_powf(t0.z, 2.2f));
+    alb = f3(rt_powf_div(t0.x, 2.2f), rt_powf_div(t0.y, 2.2f), rt_powf_div(t0.z, 2.2f));  // rtmath.h log2_pair_t
     __builtin_amdgcn_sched_barrier(0);
     const F4 t1 = sample_lod(P.texNormal, uv, lod);
     const F3 n = f3(t1.x - 0.5f, t1.y - 0.5f, t1.z - 0.5f);
@@ -178,7 +178,7 @@ RT_DEV void diffuse(PathCtx& c, int bounce, RayState& rs, F3& beta) {
     const F3 surfaceNormal = rs.normal;
     F3 albedo;
     {
-        const float lod = rt_log2f(rs.rayConeWidth * 0.5f * __builtin_sqrtf(1024.0f * 1024.0f + 1024.0f * 1024.0f));
+        const float lod = rt_log2f_div(rs.rayConeWidth * 0.5f * __builtin_sqrtf(1024.0f * 1024.0f + 1024.0f * 1024.0f));
         const float wx = surfaceNormal.x * surfaceNormal.x, wy = surfaceNormal.y * surfaceNormal.y,
                     wz = surfaceNormal.z * surfaceNormal.z;
         F3 accA = f3(0.0f), accN = f3(0.0f);

@@ -354,10 +354,15 @@ RT_HD float recip_log_den(float d) {
     return f_fma(y, f_fma(-d, y, 1.0f), y);
 }
 
-// log2(x) = hi + lo for finite x > 0 (~2^-44 relative).  Division-free: r / (2 + r) is r times the
-// Newton reciprocal above, corrected once by its exact remainder to within an ulp (so the second
-// remainder, which carries the low part, is exact as well).
-RT_HD void log2_pair(float x, float& hi, float& lo) {
+// log2(x) = hi + lo for finite x > 0 (~2^-44 relative).  Division-free (kDiv false): r / (2 + r)
+// is r times the Newton reciprocal above, corrected once by its exact remainder to within an ulp (so
+// the second remainder, which carries the low part, is exact as well).  kDiv: the two correctly
+// rounded divisions instead — the path tracer's variant (rt_powf_div / rt_log2f_div): the
+// reciprocal's extra registers pushed the fused bounce chain, which holds 168 VGPRs, into scratch.
+// The two variants can differ in the last bit; each call site uses the same one on the GPU and in
+// the oracle.
+template <bool kDiv = false>
+RT_HD void log2_pair_t(float x, float& hi, float& lo) {
     uint32_t b = float_to_bits(x);
     int e = 0;
     if (b < 0x00800000u) {  // subnormal: scale by 2^23
@@ -371,10 +376,16 @@ RT_HD void log2_pair(float x, float& hi, float& lo) {
     const float r = m - 1.0f;  // exact
     // ln(1 + r) = 2 atanh(s), s = r / (2 + r), s carried as s_hi + s_lo
     const float d = 2.0f + r, dl = r - (d - 2.0f);  // 2 + r exactly as d + dl
-    const float y = recip_log_den(d);
-    const float s0 = r * y;
-    const float s = f_fma(f_fma(-s0, d, r), y, s0);      // r / d within an ulp
-    const float sl = (f_fma(-s, d, r) - s * dl) * y;    // the exact remainder over d: r / (2 + r) - s
+    float s, sl;
+    if (kDiv) {
+        s = r / d;
+        sl = (f_fma(-s, d, r) - s * dl) / d;
+    } else {
+        const float y = recip_log_den(d);
+        const float s0 = r * y;
+        s = f_fma(f_fma(-s0, d, r), y, s0);    // r / d within an ulp
+        sl = (f_fma(-s, d, r) - s * dl) * y;  // the exact remainder over d: r / (2 + r) - s
+    }
     const float s2 = s * s;
     float q = 1.0f / 13.0f;
     q = f_fma(q, s2, 1.0f / 11.0f);
@@ -397,6 +408,7 @@ RT_HD void log2_pair(float x, float& hi, float& lo) {
     lo = lo - (t - hi);
     hi = t;
 }
+RT_HD void log2_pair(float x, float& hi, float& lo) { log2_pair_t<false>(x, hi, lo); }
 
 // ---- float cores of sin / cos / atan / atan2 (the path tracer's per-sample trig: the aperture
 // disk, cosine-weighted and light directions, the sky lookup's longitude).  Float arithmetic with
@@ -551,15 +563,18 @@ RT_HD float rt_expf(float x) {
     return rtm::scale2(p, (int)n);
 }
 
-RT_HD float rt_log2f(float x) {
+template <bool kDiv = false>
+RT_HD float rt_log2f_t(float x) {
     if (x != x) return x;
     if (x < 0.0f) return rtm::bits_to_float(0x7FC00000u);
     if (x == 0.0f) return rtm::bits_to_float(0xFF800000u);
     if (x == rtm::bits_to_float(0x7F800000u)) return x;
     float h, l;
-    rtm::log2_pair(x, h, l);
+    rtm::log2_pair_t<kDiv>(x, h, l);
     return h + l;
 }
+RT_HD float rt_log2f(float x) { return rt_log2f_t<false>(x); }
+RT_HD float rt_log2f_div(float x) { return rt_log2f_t<true>(x); }
 
 RT_HD float rt_logf(float x) {
     if (x != x) return x;
@@ -620,15 +635,17 @@ RT_HD float rt_acosf(float x) {
     return (float)rtm::atan2f_core(__builtin_sqrt((1.0 - d) * (1.0 + d)), d);
 }
 
-// powf with the C99 special cases that matter on the path (x >= 0 in practice)
-RT_HD float rt_powf(float xf, float yf) {
+// powf with the C99 special cases that matter on the path (x >= 0 in practice); kDiv: log2_pair_t's
+// division variant (rt_powf_div, the path tracer's)
+template <bool kDiv = false>
+RT_HD float rt_powf_t(float xf, float yf) {
     // common case first (textures' ^2.2, the tone mapper's gamma): x positive and finite, y not
     // NaN.  None of the special cases below applies to it, so this is the same computation as
     // the tail of the general path, without its double-precision classification.
     if (xf > 0.0f && xf < rtm::bits_to_float(0x7F800000u) && yf == yf) {
         if (xf == 1.0f) return 1.0f;  // exact (the denoiser's equal normals: a whole wave skips the log)
         float lh, ll;
-        rtm::log2_pair(xf, lh, ll);
+        rtm::log2_pair_t<kDiv>(xf, lh, ll);
         const float th = yf * lh;
         const float tl = rtm::f_fma(yf, lh, -th) + yf * ll;
         return rtm::exp2_pair(th, tl);
@@ -662,12 +679,14 @@ RT_HD float rt_powf(float xf, float yf) {
     if (x == rtm::d_inf()) return (float)(sign * (y > 0 ? rtm::d_inf() : 0.0));
     // exp2(y log2 x) with log2 x as a float pair and the product's rounding error kept
     float lh, ll;
-    rtm::log2_pair((float)x, lh, ll);
+    rtm::log2_pair_t<kDiv>((float)x, lh, ll);
     const float th = yf * lh;
     const float tl = rtm::f_fma(yf, lh, -th) + yf * ll;
     const float r = rtm::exp2_pair(th, tl);
     return sign < 0.0 ? -r : r;
 }
+RT_HD float rt_powf(float xf, float yf) { return rt_powf_t<false>(xf, yf); }
+RT_HD float rt_powf_div(float xf, float yf) { return rt_powf_t<true>(xf, yf); }
 
 // IEEE float -> binary16, round to nearest even (matches __float2half_rn / v_cvt_f16_f32)
 //

@@ -8,7 +8,7 @@ FNS = {
     "sin": (np.sin, (-50, 50)), "cos": (np.cos, (-50, 50)), "tan": (np.tan, (-1.5, 1.5)),
     "atan": (np.arctan, (-100, 100)), "acos": (np.arccos, (-1, 1)), "asin": (np.arcsin, (-1, 1)),
     "exp": (np.exp, (-80, 80)), "exp2": (np.exp2, (-120, 120)), "log": (np.log, (1e-30, 1e30)),
-    "log2": (np.log2, (1e-30, 1e30)),
+    "log2": (np.log2, (1e-30, 1e30)), "log2_div": (np.log2, (1e-30, 1e30)),
 }
 
 
@@ -23,7 +23,7 @@ def ulp_err(got, ref):
 def test_rtmath_faithful(oracle, name):
     f, (lo, hi) = FNS[name]
     rng = np.random.default_rng(7)
-    if name in ("log", "log2"):
+    if name in ("log", "log2", "log2_div"):
         xs = np.float32(10.0) ** rng.uniform(-30, 30, 3000).astype(np.float32)
     else:
         xs = rng.uniform(lo, hi, 3000).astype(np.float32)
@@ -39,6 +39,7 @@ def test_rtmath_pow_atan2(oracle):
     for _ in range(3000):
         x, y = np.float32(rng.uniform(0, 20)), np.float32(rng.uniform(-8, 8))
         worst = max(worst, ulp_err(oracle.rtmath("pow", float(x), float(y)), np.float64(x) ** np.float64(y)))
+        worst = max(worst, ulp_err(oracle.rtmath("pow_div", float(x), float(y)), np.float64(x) ** np.float64(y)))
         a, b = np.float32(rng.uniform(-5, 5)), np.float32(rng.uniform(-5, 5))
         worst = max(worst, ulp_err(oracle.rtmath("atan2", float(a), float(b)), np.arctan2(np.float64(a), np.float64(b))))
     assert worst <= 1

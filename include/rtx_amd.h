@@ -352,6 +352,13 @@ int rt_sync(rt_context* ctx);
  * milliseconds between the first launch and the end of the last. */
 int rt_time_stage(rt_context* ctx, int stage, int iters, float* total_ms);
 
+/* Test entry (no reference counterpart): the denoiser's packed-pair transcendentals (rtmath_pk.h)
+ * beside their scalar rtmath.h forms, over a caller-owned device array x of n floats (element i
+ * is paired with i ^ 1).  fn 0: pow(x, y) (x finite >= 0, y finite > 0), 1: expf(x), 2: x / y
+ * through c = RN(1 / y) (rt_div_rcp).  out_pk / out_scalar (device, n floats each) receive the two
+ * results, which must agree bit for bit.  Null stream, synchronising; RT_ERR_ARG on bad arguments. */
+int rt_debug_pk_math(int fn, const float* x, float y, float c, float* out_pk, float* out_scalar, size_t n);
+
 /* HIP-event split of the path-trace stage (stage 2 above): runs `iters` path traces with an
  * event recorded between consecutive kernels and writes the average milliseconds of each kernel
  * (n >= 7: camera, shade, trace bounce queue, resume, trace shadow queue, resume, resolve).

@@ -158,6 +158,14 @@ extern "C" float orc_rtmath(int fn, float x, float y) {
     }
 }
 
+// rtmath.h over arrays with one second argument (the denoiser's uniform sigmas): 0 rt_powf(x, y),
+// 1 rt_expf(x), 2 rt_div_rcp(x, y, c) — the checker of the GPU's packed-pair forms
+// (tests/test_gpu_pk_math.py)
+extern "C" void orc_rtmath_n(int fn, const float* x, float y, float c, float* out, size_t n) {
+    for (size_t i = 0; i < n; ++i)
+        out[i] = fn == 0 ? rt_powf(x[i], y) : fn == 1 ? rt_expf(x[i]) : rt_div_rcp(x[i], y, c);
+}
+
 // the half conversions of the G-buffers and denoise buffers (rtmath.h rt_f2h / rt_h2f, host
 // integer restatements), over arrays: tests/test_gpu_half.py checks the GPU's hardware conversions
 // against them

@@ -94,6 +94,8 @@ def lib() -> C.CDLL:
         L.orc_div_rcp_mismatches.restype = C.c_long
         L.orc_unorm16_mismatches.argtypes = []
         L.orc_unorm16_mismatches.restype = C.c_int
+        L.orc_rtmath_n.argtypes = [C.c_int, C.c_void_p, C.c_float, C.c_float, C.c_void_p, C.c_size_t]
+        L.orc_rtmath_n.restype = None
         L.orc_f2h_n.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.orc_f2h_n.restype = None
         L.orc_h2f_n.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
@@ -197,6 +199,14 @@ RTMATH = dict(sin=0, cos=1, tan=2, atan=3, atan2=4, acos=5, asin=6, exp=7, exp2=
 
 def rtmath(fn: str, x: float, y: float = 0.0) -> float:
     return lib().orc_rtmath(RTMATH[fn], x, y)
+
+
+def rtmath_n(fn: int, x: np.ndarray, y: float = 0.0, c: float = 0.0) -> np.ndarray:
+    """rtmath.h over a float32 array (0 pow(x, y), 1 expf(x), 2 rt_div_rcp(x, y, c))."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    lib().orc_rtmath_n(fn, x.ctypes.data, y, c, out.ctypes.data, x.size)
+    return out
 
 
 def f2h(f: np.ndarray) -> np.ndarray:

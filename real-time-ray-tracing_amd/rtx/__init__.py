@@ -134,6 +134,7 @@ SIGNATURES = {
     "rt_trace_primary": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "rt_sync": (C.c_int, [C.c_void_p]),
     "rt_time_stage": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float)]),
+    "rt_debug_pk_math": (C.c_int, [C.c_int, C.c_void_p, C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_size_t]),
     "rt_time_path_trace_kernels": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_float), C.c_int]),
     "rt_time_frame_kernels": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float), C.c_int]),
     "rt_trace_rays": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(C.c_float)]),

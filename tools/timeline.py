@@ -27,6 +27,22 @@ def pipelined(rows, a, nf):
         busy[r["Queue_Id"]] += e - s
         print("%8.1f %8.1f %7.1f q%s %s" % (s, e, e - s, r["Queue_Id"], short(r["Kernel_Name"])[:30]))
     print("frame period: %.1f us" % ((int(rows[end]["Start_Timestamp"]) - t0) / 1000 / nf))
+    # the chip's idle time: moments with no kernel of any queue running (host-bound gaps)
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows[start:end])
+    idle, cur_e, one = 0, iv[0][1], 0
+    for s_, e_ in iv[1:]:
+        if s_ > cur_e:
+            idle += s_ - cur_e
+        cur_e = max(cur_e, e_)
+    # time with exactly one kernel running (no overlap) vs two or more
+    ev = sorted([(s_, 1) for s_, _ in iv] + [(e_, -1) for _, e_ in iv])
+    depth, last, alone = 0, ev[0][0], 0
+    for t_, d_ in ev:
+        if depth == 1:
+            alone += t_ - last
+        depth += d_
+        last = t_
+    print("no kernel running: %.1f us per frame; one kernel alone: %.1f us per frame" % (idle / 1000 / nf, alone / 1000 / nf))
     print("kernel time per frame by queue: " + ", ".join("q%s %.1f us" % (q, v / nf) for q, v in sorted(busy.items())))
 
 

@@ -419,7 +419,8 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, TravR
     uint32_t next = nodeNext ^ ((nodeNext ^ cur ^ (kLeafBit | kBlasBit)) & (uint32_t)((int)cur >> 31));
     const bool pop = isTri || (isNode && !i1 && !i2);
     bool done = kLds == 16 && pop && tp < 0;
-    int top = (pop && kLds == 16) ? tp - 1 : ((push && !pop) ? tp + 1 : tp);
+    // (a push needs both children hit at a node, so it never coincides with a pop)
+    int top = (pop && kLds == 16) ? tp - 1 : (push ? tp + 1 : tp);
     next = (pop && kLds == 16) ? (uint32_t)e : next;
     // kLds 16: the popped entry is e, and the loop pops on past entries farther than the closest
     // hit; otherwise the loop makes every pop (a +inf start enters it)

@@ -961,12 +961,17 @@ RT_DEV uint2 temporal2_pixel(const DenoisePostParams& P, const uint2* in, int x,
     for (int j = 0; j < 9; ++j) {
         const int xo = j % 3, yo = j / 3;
         const bool same = (int)mask_of(qs[j]) == mV;
+        // a tap of another material enters the bounds as NaN, which fmaxf / fminf (IEEE maxNum /
+        // minNum, v_max_f32 / v_min_f32) pass over: the reference's `same ? fmax(b, c) : b` with one
+        // select per channel instead of one per bound and channel (the bounds are never NaN)
         const F3 cc = ycocg(rgb_of(qs[j]));
-        nMax = same ? fmax3(nMax, cc) : nMax;
-        nMin = same ? fmin3(nMin, cc) : nMin;
+        const float qn = __builtin_nanf("");
+        const F3 cs = same ? cc : f3(qn);
+        nMax = fmax3(nMax, cs);
+        nMin = fmin3(nMin, cs);
         if (abs(xo - 1) + abs(yo - 1) <= 1) {
-            nMax2 = same ? fmax3(nMax2, cc) : nMax2;
-            nMin2 = same ? fmin3(nMin2, cc) : nMin2;
+            nMax2 = fmax3(nMax2, cs);
+            nMin2 = fmin3(nMin2, cs);
         }
     }
     nMax = (nMax + nMax2) / 2.0f;

@@ -1134,6 +1134,12 @@ RT_DEV uint2 bicubic_scale_px(const Img& im, int W, int H, int x, int y, int Ws,
 RT_DEV float luminance(F3 v) { return dot(v, f3(0.2126f, 0.7152f, 0.0722f)); }  // linearMath.h:746-749
 
 RT_DEV F3 mat3_mul(const float* m, F3 v) {  // Mat3 * Float3 (linearMath.h:533-538), rows via InnerProduct
+    if (kDnPk) {  // rows 0 and 1 as one register pair (rtmath_pk.h inner3_2g)
+        using rtpk::F2;
+        const F2 r01 = rtpk::inner3_2g(F2{m[0], m[3]}, rtpk::splat(v.x), F2{m[1], m[4]}, rtpk::splat(v.y),
+                                       F2{m[2], m[5]}, rtpk::splat(v.z));
+        return f3(r01.x, r01.y, inner3(m[6], v.x, m[7], v.y, m[8], v.z));
+    }
     return f3(inner3(m[0], v.x, m[1], v.y, m[2], v.z), inner3(m[3], v.x, m[4], v.y, m[5], v.z),
               inner3(m[6], v.x, m[7], v.y, m[8], v.z));
 }

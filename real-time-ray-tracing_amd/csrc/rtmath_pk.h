@@ -156,10 +156,8 @@ __device__ inline F2 expf2(F2 x) {
               x.y != x.y ? x.y : x.y > 89.0f ? inf : x.y < -104.0f ? 0.0f : s.y};
 }
 
-// inner3(a, b, c, d, e, f) with a, c, e shared by both elements (the centre normal) — rt_device.h's
-// compensated dot product, element for element
-__device__ inline F2 inner3_2(float a, F2 b, float c, F2 d, float e, F2 f) {
-    const F2 A = splat(a), C = splat(c), E = splat(e);
+// inner3(a, b, c, d, e, f) — rt_device.h's compensated dot product, element for element
+__device__ inline F2 inner3_2g(F2 A, F2 b, F2 C, F2 d, F2 E, F2 f) {
     const F2 ef = E * f, efe = fma2(E, f, -ef);
     const F2 cd = C * d, cde = fma2(C, d, -cd);
     const F2 s2 = cd + ef, dl2 = s2 - cd, s2e = (cd - (s2 - dl2)) + (ef - dl2);
@@ -168,6 +166,10 @@ __device__ inline F2 inner3_2(float a, F2 b, float c, F2 d, float e, F2 f) {
     const F2 s1 = ab + tpv, dl1 = s1 - ab, s1e = (ab - (s1 - dl1)) + (tpv - dl1);
     const F2 rv = s1, re = abe + (tpe + s1e);
     return rv + re;
+}
+// with a, c, e shared by both elements (the centre normal)
+__device__ inline F2 inner3_2(float a, F2 b, float c, F2 d, float e, F2 f) {
+    return inner3_2g(splat(a), b, splat(c), d, splat(e), f);
 }
 
 // rt_div_rcp(a, b, c) (c = RN(1 / b), b in its range: rt_div_rcp_ok)

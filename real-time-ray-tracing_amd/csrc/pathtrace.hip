@@ -268,20 +268,38 @@ RT_DEV float ray_cone_width(const PathTraceParams& P, int ix, int iy) {
     return af - an;
 }
 
+// step 0's G-buffer values: depth, material mask and the motion vector
+// (HistoryCamera::WorldToScreenSpace, kernel.cuh:144-151)
+RT_DEV void gbuffer_step0(const PathCtx& c, PathVars& v) {
+    const RayState& rs = v.rs;
+    v.outDepth = rs.depth;
+    v.mask = (uint32_t)rs.matId & 0xFFFFu;
+    F2 mv = {0.0f, 0.0f};
+    if (rs.hit) {
+        const PathTraceParams& P = c.P;
+        const F3 d = rs.pos - load3(P.hist.pos);
+        const F3 q = f3(dot(load3(P.hist.left), d), dot(load3(P.hist.up), d), dot(load3(P.hist.dir), d));
+        const F2 s = {q.x / q.z, q.y / q.z};
+        const F2 ndc = {s.x / P.tanHalfFov[0], s.y / P.tanHalfFov[1]};
+        mv = F2{(0.5f - ndc.x * 0.5f) - v.sampleUv.x, (0.5f - ndc.y * 0.5f) - v.sampleUv.y};
+    }
+    v.mv = F2{mv.x + 0.5f, mv.y + 0.5f};
+}
+
 // Steps k0..4 of the reference's straight-line sequence (pathtrace.cuh:61-101)
 //   I G0 I G1 I G2 D0 [normal] I G3 D1 I
 // as one loop so traversal, glossy and diffuse each have a single call site.  With `hit`
 // set, step k0's intersection result is *hit (a deferred ray that came back from the queue
-// tracer).  An intersection at a step >= kDeferFrom is not traced here: the step is returned
-// and the caller queues the ray.  Returns 5 when the path is complete.
+// tracer), applied before the loop so that the record is dead by the first interaction.  An
+// intersection at a step >= kDeferFrom is not traced here: the step is returned and the caller
+// queues the ray.  Returns 5 when the path is complete.
 template <int kDeferFrom, bool kMF>
 RT_DEV int run_path(PathCtx& c, PathVars& v, int k0, const HitInfo* hit, const SceneView& sc, uint2* stk) {
     RayState& rs = v.rs;
+    if (hit) apply_hit(c.P, rs, *hit);
 #pragma unroll 1
     for (int k = k0; k < 5; ++k) {
-        if (k == k0 && hit) {
-            apply_hit(c.P, rs, *hit);
-        } else if (needs_trace(rs)) {
+        if ((k != k0 || !hit) && needs_trace(rs)) {
             if (k >= kDeferFrom) return k;
             ++c.rays;
             HitInfo h;
@@ -290,20 +308,7 @@ RT_DEV int run_path(PathCtx& c, PathVars& v, int k0, const HitInfo* hit, const S
             c.tests += h.tests;
             apply_hit(c.P, rs, h);
         }
-        if (k == 0) {
-            v.outDepth = rs.depth;
-            v.mask = (uint32_t)rs.matId & 0xFFFFu;
-            F2 mv = {0.0f, 0.0f};
-            if (rs.hit) {  // HistoryCamera::WorldToScreenSpace (kernel.cuh:144-151)
-                const PathTraceParams& P = c.P;
-                const F3 d = rs.pos - load3(P.hist.pos);
-                const F3 q = f3(dot(load3(P.hist.left), d), dot(load3(P.hist.up), d), dot(load3(P.hist.dir), d));
-                const F2 s = {q.x / q.z, q.y / q.z};
-                const F2 ndc = {s.x / P.tanHalfFov[0], s.y / P.tanHalfFov[1]};
-                mv = F2{(0.5f - ndc.x * 0.5f) - v.sampleUv.x, (0.5f - ndc.y * 0.5f) - v.sampleUv.y};
-            }
-            v.mv = F2{mv.x + 0.5f, mv.y + 0.5f};
-        }
+        if (k == 0) gbuffer_step0(c, v);
         if (k == 4) break;
         glossy(c, rs, k);
         if (k >= 2) {
@@ -319,6 +324,25 @@ RT_DEV int run_path(PathCtx& c, PathVars& v, int k0, const HitInfo* hit, const S
         }
     }
     return 5;
+}
+
+// run_path<1, kMF>(c, v, 0, &hit, ..) for a material table without mirror or glass, in straight
+// line.  glossy() then returns at once for every state (an emissive or sky hit sets hitLight or
+// isOccluded, a lambertian or microfacet one isDiffuse), so step 1 never traces, step 2 is D0, and
+// step 3 traces exactly when D0 produced a ray (D0 either returns before touching the state, which
+// D1 then does too, or sets isOccluded, or sets a direction with isHitProcessed).  Without the
+// step loop the camera hit record, the loop state and glossy's operands are not live across D0:
+// k_pt_shade0 fits 3 waves per SIMD.
+template <bool kMF>
+RT_DEV int run_shade0_diffuse(PathCtx& c, PathVars& v, const HitInfo& hit) {
+    RayState& rs = v.rs;
+    apply_hit(c.P, rs, hit);
+    gbuffer_step0(c, v);
+    F3 beta = f3(1.0f);
+    diffuse<kMF>(c, 0, rs, beta);
+    v.beta1 = beta;
+    v.outNormal = rs.fakeNormal;
+    return needs_trace(rs) ? 3 : 5;
 }
 
 // end of PathTrace (pathtrace.cuh:103-128): the sample's demodulated colour
@@ -588,9 +612,12 @@ __global__ __launch_bounds__(256, kOneRound ? 6 : 4) void k_pt_camera(PathTraceP
 // colours the resolve kernel needs — exactly as the sequential loop of PathTrace's caller does.
 //
 // kOneRound as in k_pt_camera: with one round per sample wave the fold state around the sample loop
-// is not carried across rounds (229 instead of 256 VGPRs; one GPU 0.970 -> 0.945 ms/frame).
+// is not carried across rounds (one GPU 0.970 -> 0.945 ms/frame in round 3).  Without mirror or
+// glass the sample runs run_shade0_diffuse, so the one-round kernel fits 168 VGPRs without
+// scratch: 3 waves per SIMD instead of 2 (229 VGPRs through the step loop; serial 0.212 ->
+// 0.190 ms, synchronous draw 1.089 -> 1.069 ms, profiles/r05_ab/shade0_straight/).
 template <bool kGlossy, bool kMF, bool kOneRound>
-__global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
+__global__ __launch_bounds__(256, (kGlossy || !kOneRound) ? 2 : 3) void k_pt_shade0(PathTraceParams P) {
     __shared__ uint2 stk[kGlossy ? 17 * 256 : 1];  // 16 entries + trav_step's dead slot
     __shared__ uint32_t sob[256];
     __shared__ float4 foldL[4][64];  // this round's samples: finished colour xyz, w = 1 when deferred
@@ -648,7 +675,8 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
                 HitInfo h;
                 finalize_hit(sc, v.rs.orig, v.rs.dir, hr.x, (int)__float_as_uint(hr.y), hr.z, hr.w, P.ws.hit0Err[q],
                              h);
-                kd = run_path<kGlossy ? 3 : 1, kMF>(c, v, 0, &h, sc, stk + (kGlossy ? tid : 0));
+                if constexpr (kGlossy) kd = run_path<3, kMF>(c, v, 0, &h, sc, stk + tid);
+                else kd = run_shade0_diffuse<kMF>(c, v, h);
                 if (kd < 3) {  // cannot happen without mirror/glass materials: flag it, finish the sample
                     atomicAdd(&P.ws.counters[kCntError], 1u);
                     kd = 5;
@@ -746,10 +774,24 @@ __global__ __launch_bounds__(256, 2) void k_pt_shade0(PathTraceParams P) {
     add_rays(P, wgRays, raysWg, wS);
 }
 
+// run_path<0, kMF>(c, v, kStep, &hit, ..) in straight line where no glossy interaction can run:
+// step 4 (it ends the path) for any table, step 3 without mirror or glass (as run_shade0_diffuse:
+// G3 returns at once, so step 3 is D1 and step 4 traces exactly when D1 produced a ray)
+template <int kStep, bool kMF>
+RT_DEV int resume_diffuse(PathCtx& c, PathVars& v, const HitInfo& hit) {
+    apply_hit(c.P, v.rs, hit);
+    if (kStep == 4) return 5;
+    F3 beta = f3(1.0f);
+    diffuse<kMF>(c, 1, v.rs, beta);
+    v.beta0 = beta;
+    return needs_trace(v.rs) ? 4 : 5;
+}
+
 // Entry i of queue kStep (3 or 4): reloads the sample's state, applies the hit the tracer found
 // (t, triangle index bits, u, v; errorT) and runs the rest of its sequence.  Returns 4 when the
-// I4 ray must be traced (kStep == 3 only), else 5 (the sample is complete).
-template <int kStep, bool kMF>
+// I4 ray must be traced (kStep == 3 only), else 5 (the sample is complete).  kGlossy: the material
+// table holds mirror or glass.
+template <int kStep, bool kMF, bool kGlossy>
 RT_DEV int resume_entry(PathCtx& c, const PtQueue& q, const SceneView& sc, uint32_t i, float4 hr, float herr,
                         PathVars& v, uint32_t& p, uint32_t& s) {
     const PathTraceParams& P = c.P;
@@ -779,7 +821,8 @@ RT_DEV int resume_entry(PathCtx& c, const PtQueue& q, const SceneView& sc, uint3
     rs.matType = MAT_SKY;
     HitInfo h;
     finalize_hit(sc, rs.orig, rs.dir, hr.x, (int)__float_as_uint(hr.y), hr.z, hr.w, herr, h);
-    return run_path<0, kMF>(c, v, kStep, &h, sc, nullptr);
+    if constexpr (kGlossy && kStep == 3) return run_path<0, kMF>(c, v, kStep, &h, sc, nullptr);
+    else return resume_diffuse<kStep, kMF>(c, v, h);
 }
 
 // a completed sample of a queue entry: its radiance goes to the late-resolve slot
@@ -791,8 +834,8 @@ RT_DEV void store_path_L(const PathCtx& c, const PathVars& v, uint32_t p, uint32
 }
 
 // Resumes the samples of queue kStep (3 or 4) once k_trace_queue has written their hits.
-template <int kStep, bool kMF>
-__global__ __launch_bounds__(256, kMF ? 2 : 3) void k_pt_resume(PathTraceParams P) {
+template <int kStep, bool kMF, bool kGlossy>
+__global__ __launch_bounds__(256, kStep == 3 ? 3 : 4) void k_pt_resume(PathTraceParams P) {
     __shared__ uint32_t sob[256];
     __shared__ unsigned long long wgRays[4];
     // step 4 ends the path before any diffuse interaction: no light sampling there
@@ -819,7 +862,7 @@ __global__ __launch_bounds__(256, kMF ? 2 : 3) void k_pt_resume(PathTraceParams 
         PathVars v;
         int kd = 5;
         uint32_t p = 0, s = 0;
-        if (active) kd = resume_entry<kStep, kMF>(c, q, sc, i, P.ws.hitRec[i], P.ws.hitErr[i], v, p, s);
+        if (active) kd = resume_entry<kStep, kMF, kGlossy>(c, q, sc, i, P.ws.hitRec[i], P.ws.hitErr[i], v, p, s);
         const uint32_t slot = wave_append(kd == 4, &P.ws.counters[kCntQ4]);
         if (active) {
             if (kd < 5) {  // kStep == 3 only: the I4 ray
@@ -994,7 +1037,7 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
                     PathVars v;
                     uint32_t p = 0, smp = 0;
                     c.rays = 0;
-                    (void)resume_entry<4, false>(c, P.ws.q4, sc, slot,
+                    (void)resume_entry<4, false, false>(c, P.ws.q4, sc, slot,
                                                  make_float4(s4.t, __uint_as_float((uint32_t)s4.hitIdx), s4.hitU, s4.hitV),
                                                  s4.hitErrT, v, p, smp);
                     store_path_L(c, v, p, smp);
@@ -1017,7 +1060,7 @@ __global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
             uint32_t p = 0, smp = 0;
             c.rays = 0;
             c.diffuse = 0;
-            if (act) kd = resume_entry<3, false>(c, q, sc, i, P.ws.hitRec[i], P.ws.hitErr[i], v, p, smp);
+            if (act) kd = resume_entry<3, false, false>(c, q, sc, i, P.ws.hitRec[i], P.ws.hitErr[i], v, p, smp);
             const bool i4 = kd == 4;
             const uint32_t slot = wave_append(i4, &P.ws.counters[kCntQ4]);
             const unsigned long long m4 = __ballot(i4);
@@ -1166,12 +1209,13 @@ hipError_t launch_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t*
     } else {
         if ((e = rtk_launch_trace_queue(p, 3, stream)) != hipSuccess || (e = end()) != hipSuccess) return e;
         if ((e = begin()) != hipSuccess) return e;
-        if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_resume<3, true>), pg, pb, 0, stream, *p);
-        else hipLaunchKernelGGL((k_pt_resume<3, false>), pg, pb, 0, stream, *p);
+        if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_resume<3, true, false>), pg, pb, 0, stream, *p);
+        else if (p->ws.glossy) hipLaunchKernelGGL((k_pt_resume<3, false, true>), pg, pb, 0, stream, *p);
+        else hipLaunchKernelGGL((k_pt_resume<3, false, false>), pg, pb, 0, stream, *p);
         if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
         if ((e = rtk_launch_trace_queue(p, 4, stream)) != hipSuccess || (e = end()) != hipSuccess) return e;
         if ((e = begin()) != hipSuccess) return e;
-        hipLaunchKernelGGL((k_pt_resume<4, false>), pg, pb, 0, stream, *p);  // step 4 shades nothing
+        hipLaunchKernelGGL((k_pt_resume<4, false, false>), pg, pb, 0, stream, *p);  // step 4 shades nothing
         if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_pt_resolve, dim3(p->ws.persistBlocks), dim3(256), 0, stream, *p);

@@ -199,13 +199,25 @@ RT_DEV void radix_sort(Lds<kThr>& s) {
         }
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
-            uint64_t m = ~0ull;
+            // lanes whose digit equals this lane's: the AND over the six bits of (bit ? ballot : ~ballot),
+            // with ~ballot = ballot ^ ~0 — per bit one sign-extended inverted bit s (0 where the bit is
+            // set, ~0 where clear), the ballot of s == 0, and m &= ballot ^ s as one v_bitop3 per half
+            // (LUT 0x60: src0 & (src1 ^ src2))
+            const uint32_t nd = ~d[j];
+            uint32_t mlo = 0u, mhi = 0u;
 #pragma unroll
             for (int b = 0; b < 6; ++b) {
-                const bool bit = (d[j] >> b) & 1u;
-                const uint64_t bal = __ballot(bit);
-                m &= bit ? bal : ~bal;
+                const uint32_t sb = (uint32_t)((int32_t)(nd << (31 - b)) >> 31);
+                const uint64_t bal = __ballot(sb == 0u);
+                if (b == 0) {
+                    mlo = (uint32_t)bal ^ sb;
+                    mhi = (uint32_t)(bal >> 32) ^ sb;
+                } else {
+                    mlo = __builtin_amdgcn_bitop3_b32(mlo, (uint32_t)bal, sb, 0x60);
+                    mhi = __builtin_amdgcn_bitop3_b32(mhi, (uint32_t)(bal >> 32), sb, 0x60);
+                }
             }
+            const uint64_t m = ((uint64_t)mhi << 32) | mlo;
             rank[j] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             if (rank[j] == 0) hist[d[j] * 16 + w + j * kW] = (uint16_t)__popcll(m);
         }
@@ -236,14 +248,20 @@ RT_DEV void radix_sort(Lds<kThr>& s) {
     }
 }
 
+// delta(i, j) of the reference (buildBVH.cuh:8-20): the common prefix length of key i (m0) and key j,
+// 32 for equal keys, 0 for j outside [0, n).  Branch-free: the read is clamped into the array and
+// the out-of-range result selected afterwards.
 RT_DEV int lcp(const uint32_t* key, int n, uint32_t m0, int j) {
-    if (j < 0 || j >= n) return 0;
-    const uint32_t x = m0 ^ key[j];
-    return x == 0u ? 32 : __builtin_clz(x);
+    const int jc = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
+    const uint32_t x = m0 ^ key[jc];
+    const int c = x == 0u ? 32 : __builtin_clz(x);
+    return (uint32_t)j < (uint32_t)n ? c : 0;
 }
 
 // Karras 2012 topology over key1[0..n) (buildBVH.cuh:60-134) of internal node i, into the info
-// words; also clears node i's arrival count for the refit.
+// words; also clears node i's arrival count for the refit.  The probes i + k * d (d = +-1) are
+// 24-bit multiplies (v_mul_i32_i24, full rate; |k| < 2048) and the split search's ceil(l / div),
+// div = 2, 4, 8 ..., a shift: the reference's arithmetic on these operand ranges.
 template <int kThr>
 RT_DEV void karras_node(Lds<kThr>& s, int n, int i) {
     const uint32_t* key = s.key1;
@@ -253,20 +271,20 @@ RT_DEV void karras_node(Lds<kThr>& s, int n, int i) {
     const int d = (dr - dl) >= 0 ? 1 : -1;
     const int deltaMin = lcp(key, n, m0, i - d);
     int lmax = 2;
-    while (lcp(key, n, m0, i + lmax * d) > deltaMin) lmax *= 2;
+    while (lcp(key, n, m0, i + __mul24(lmax, d)) > deltaMin) lmax *= 2;
     int l = 0;
-    for (int t = lmax / 2; t >= 1; t /= 2)
-        if (lcp(key, n, m0, i + (l + t) * d) > deltaMin) l += t;
-    const int j = i + l * d;
+    for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (lcp(key, n, m0, i + __mul24(l + t, d)) > deltaMin) l += t;
+    const int j = i + __mul24(l, d);
     const int deltaNode = lcp(key, n, m0, j);
-    int sp = 0, div = 2;
+    int sp = 0, sh = 1;  // div = 2^sh
     while (true) {  // the reference's extra t == 1 probes are no-ops (SURVEY §0 #8b)
-        const int t = (l + div - 1) / div;
-        if (lcp(key, n, m0, i + (sp + t) * d) > deltaNode) sp += t;
+        const int t = (l + (1 << sh) - 1) >> sh;  // (l + div - 1) / div, l >= 0
+        if (lcp(key, n, m0, i + __mul24(sp + t, d)) > deltaNode) sp += t;
         if (t <= 1) break;
-        div *= 2;
+        ++sh;
     }
-    const int gamma = i + sp * d + (d < 0 ? d : 0);
+    const int gamma = i + __mul24(sp, d) + (d < 0 ? d : 0);
     const int lo = i < j ? i : j, hi = i < j ? j : i;
     if (lo == gamma) {
         s.a.info[i][0] = (uint16_t)(0x8000u | s.idx1[gamma]);
@@ -480,9 +498,15 @@ RT_DEV void sort_and_build(Lds<kThr>& s, const float* leafG, int n, uint32_t* mo
         mortonOut[e] = s.key1[e];
         reorderOut[e] = s.idx1[e];
     }
+#if defined(RTX_BVH_PHASES) && RTX_BVH_PHASES >= 2
+    return;
+#endif
     karras(s, n);
     __syncthreads();
     BVH_STAMP(4);
+#if defined(RTX_BVH_PHASES) && RTX_BVH_PHASES >= 1
+    return;
+#endif
     refit<kThr, true>(s, leafG, n, nodes, w);
 }
 
@@ -703,6 +727,10 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
     Node* const nodes = (Node*)P.nodes;
     const WordCtx blasWords{kBlasBit, start, kLeafBit | kBlasBit, B * (uint32_t)kBatch + B + start, 1u};
     BVH_STAMP(2);
+#if defined(RTX_BVH_PHASES) && RTX_BVH_PHASES >= 3
+    if (!pubNow && t == 0) publish_root(P, b, scene);
+    return;
+#endif
     sort_and_build(s, leafG, (int)cnt, P.morton + start, P.reorder + start, nodes + start, blasWords,
                    pubNow ? nullptr : &P, b);
     __syncthreads();

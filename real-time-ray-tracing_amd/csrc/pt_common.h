@@ -72,14 +72,12 @@ RT_DEV void bn_stage_sobol(const uint8_t* tables, uint32_t* sobolRows, int tid, 
 RT_DEV F2 concentric_disk(F2 u) {
     const F2 o = {2.0f * u.x - 1.0f, 2.0f * u.y - 1.0f};
     if (fabsf(o.x) < 1e-10f && fabsf(o.y) < 1e-10f) return F2{0.0f, 0.0f};
-    float theta, r;
-    if (fabsf(o.x) > fabsf(o.y)) {
-        r = o.x;
-        theta = kPiOver4 * (o.y / o.x);
-    } else {
-        r = o.y;
-        theta = kPiOver2 - kPiOver4 * (o.x / o.y);
-    }
+    // the two branches as selects around one division (a wave's lanes take both; each lane's
+    // operations are the branch's own)
+    const bool xMajor = fabsf(o.x) > fabsf(o.y);
+    const float r = xMajor ? o.x : o.y;
+    const float q = (xMajor ? o.y : o.x) / r;
+    const float theta = xMajor ? kPiOver4 * q : kPiOver2 - kPiOver4 * q;
     float sn, cs;
     rt_sincosf(theta, &sn, &cs);
     return F2{cs * r, sn * r};

@@ -498,15 +498,9 @@ RT_DEV void sort_and_build(Lds<kThr>& s, const float* leafG, int n, uint32_t* mo
         mortonOut[e] = s.key1[e];
         reorderOut[e] = s.idx1[e];
     }
-#if defined(RTX_BVH_PHASES) && RTX_BVH_PHASES >= 2
-    return;
-#endif
     karras(s, n);
     __syncthreads();
     BVH_STAMP(4);
-#if defined(RTX_BVH_PHASES) && RTX_BVH_PHASES >= 1
-    return;
-#endif
     refit<kThr, true>(s, leafG, n, nodes, w);
 }
 
@@ -727,10 +721,6 @@ __global__ __launch_bounds__(kThr, 8) void k_build_bvh(BvhBuildParams P) {
     Node* const nodes = (Node*)P.nodes;
     const WordCtx blasWords{kBlasBit, start, kLeafBit | kBlasBit, B * (uint32_t)kBatch + B + start, 1u};
     BVH_STAMP(2);
-#if defined(RTX_BVH_PHASES) && RTX_BVH_PHASES >= 3
-    if (!pubNow && t == 0) publish_root(P, b, scene);
-    return;
-#endif
     sort_and_build(s, leafG, (int)cnt, P.morton + start, P.reorder + start, nodes + start, blasWords,
                    pubNow ? nullptr : &P, b);
     __syncthreads();

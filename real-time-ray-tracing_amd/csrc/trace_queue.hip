@@ -33,6 +33,15 @@ constexpr bool kLeafBatch = RTX_LEAF_BATCH != 0;  // ablation: -DRTX_LEAF_BATCH=
 template <int kStep>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) {
     __shared__ uint2 stk[17 * kTraceBlock];  // 16 entries + the dead slot trav_step stores above the top
+    // The tracers' waves issue at the denoise kernels' priority (DN_PRIO), above the next frame's
+    // camera waves: in a pipelined frame the context stream binds (bench.py binding_stream), and its
+    // queue tracers' time is their longest rays' dependent iterations, which stretch when the SIMD
+    // arbiter serves the camera waves first.  Measured (tools/ab.sh, three repeats): frame
+    // 0.803-0.811 -> 0.782-0.792 ms, trace<3> 0.287 -> 0.244 ms, trace<4> 0.203 -> 0.166 ms, terrain
+    // 3.20-3.24 -> 3.16-3.21 ms; trace<4> alone at 3: 0.785-0.790; both at 2: 0.799-0.802; the resume
+    // kernels at 3 on top: no better (profiles/r05_ab/queue_prio/).  (Round 4, with the shade kernel
+    // at 2 waves per SIMD and the post stream binding, the same measured slower.)
+    __builtin_amdgcn_s_setprio(3);
     const int tid = threadIdx.x;
     const int lane = (int)__lane_id();
     const PtQueue& q = kStep == 3 ? P.ws.q3 : P.ws.q4;

@@ -280,13 +280,15 @@ int rt_set_stream(rt_context* ctx, void* stream);
  * stream, after everything enqueued on the context stream so far (path trace, G-buffer
  * gathers), and the path tracer alternates between two G-buffer sets, so the trace of frame
  * f+1 overlaps the denoise of frame f; the LBVH build and camera rays of the next frame run on
- * an internal third stream beside the current frame's trace kernels (two LBVH sets, three
- * G-buffer sets).  Results are identical to the serial order.  Host reads (rt_get_buffer,
- * rt_download, rt_sync, rt_draw's copies) wait for all streams.  NULL turns it off.
+ * an internal third stream beside the current frame's trace kernels (two LBVH sets,
+ * RT_GBUFFER_SETS G-buffer sets).  Results are identical to the serial order.  Host reads
+ * (rt_get_buffer, rt_download, rt_sync, rt_draw's copies) wait for all streams.  NULL turns it off.
  * rt_info.gbufferSet names the set the last path trace wrote; bind the other sets' buffers
- * with name | RT_BUF_SET1 / RT_BUF_SET2. */
+ * with name | RT_BUF_SET1 / RT_BUF_SET2 / RT_BUF_SET3. */
+#define RT_GBUFFER_SETS 4
 #define RT_BUF_SET1 0x100
 #define RT_BUF_SET2 0x200
+#define RT_BUF_SET3 0x300
 int rt_set_post_stream(rt_context* ctx, void* stream);
 
 /* Multi-GPU gathers off the trace chain (no reference counterpart): each later rt_denoise_post

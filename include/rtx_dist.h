@@ -85,7 +85,7 @@ int rtd_exchange_histogram(rtd_strips* s, int32_t* histogram, void* stream);
 int rtd_exchange_rows(rtd_strips* s, void* accum, void* history, void* rgba, void* stream);
 
 /* Allocate (hipMalloc) and bind (rt_bind_buffer) the full-frame buffers the exchanges move — the
- * G-buffers of all three G-buffer sets, accumulation, both history buffers, histogram, RGBA8 — and
+ * G-buffers of all RT_GBUFFER_SETS G-buffer sets, accumulation, both history buffers, histogram, RGBA8 — and
  * install rtd_hook for RT_HOOK_GBUFFERS, RT_HOOK_HISTOGRAM and RT_HOOK_ROWS (rt_set_hook_stages).
  * ctx must be an inited context of this rank's strip (stripCount = world, stripIndex = rank).
  * On failure the buffers bound before the failing step stay bound to ctx and are owned by s: the

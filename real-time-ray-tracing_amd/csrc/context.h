@@ -42,8 +42,11 @@ struct BvhBufs {
     uint32_t* counter = nullptr;
 };
 
-#ifndef RTX_GB_SETS  // A/B builds only (tools/abl_build.sh): 2..4; rtx_dist.h hosts assume 3
-#define RTX_GB_SETS 3
+// G-buffer sets in flight with frame pipelining: with four, frame f+4's camera rays wait for the
+// denoise of f instead of f+3's for f's; 3 -> 4 measured 0.787 -> 0.771 ms per pipelined 1080p
+// frame (tools/ab.sh, three repeats, profiles/r05_ab/gbuffer_sets/)
+#ifndef RTX_GB_SETS  // A/B builds only (tools/abl_build.sh): 2..4 with RT_GBUFFER_SETS set alike
+#define RTX_GB_SETS RT_GBUFFER_SETS
 #endif
 constexpr int kGbSets = RTX_GB_SETS;  // G-buffer / camera-output sets in flight with frame pipelining
 

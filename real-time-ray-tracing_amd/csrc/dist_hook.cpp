@@ -21,7 +21,7 @@ namespace {
 constexpr int kGb = 5;
 constexpr int kGbName[kGb] = {RT_BUF_RENDER_COLOR, RT_BUF_NORMAL, RT_BUF_ALBEDO, RT_BUF_DEPTH, RT_BUF_MOTION};
 constexpr size_t kGbBpp[kGb] = {8, 8, 8, 2, 4};
-constexpr int kSets = 3;  // G-buffer sets of a pipelined context (rt_set_post_stream)
+constexpr int kSets = RT_GBUFFER_SETS;  // G-buffer sets of a pipelined context (rt_set_post_stream)
 
 struct Range { uint32_t lo, hi; };
 

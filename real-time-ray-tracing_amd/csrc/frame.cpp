@@ -1182,7 +1182,7 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
 int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
     if (!ctx || !device_ptr) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_bind_buffer before rt_init"; return RT_ERR_STATE; }
-    const int set = (name >> 8) & 3;  // RT_BUF_SET1 / RT_BUF_SET2
+    const int set = (name >> 8) & 3;  // RT_BUF_SET1 / RT_BUF_SET2 / RT_BUF_SET3
     name &= 0xFF;
     if (set >= kGbSets) { ctx->err = "rt_bind_buffer: no such G-buffer set"; return RT_ERR_ARG; }
     const size_t need = rt_alloc_bytes(ctx, name);  // later frames may be larger than the current one

@@ -152,8 +152,8 @@ SIGNATURES = {
 }
 IMAGE_PPM_RGBA8, IMAGE_PFM_HDR = 0, 1
 DRAW_ASYNC = 1  # rt_draw_device flag
-BUF_SET1, BUF_SET2 = 0x100, 0x200  # rt_bind_buffer: further G-buffer sets (frame pipelining)
-GBUFFER_SETS = 3  # G-buffer sets a pipelined context cycles through (rt_set_post_stream)
+BUF_SET1, BUF_SET2, BUF_SET3 = 0x100, 0x200, 0x300  # rt_bind_buffer: further G-buffer sets (frame pipelining)
+GBUFFER_SETS = 4  # G-buffer sets a pipelined context cycles through (rt_set_post_stream; RT_GBUFFER_SETS)
 
 _lib = None
 
@@ -356,7 +356,7 @@ class RayTracer:
         self._check(self.lib.rt_set_hook_stages(self.h, mask), "rt_set_hook_stages")
 
     def bind_buffer(self, name: str, device_ptr: int, nbytes: int, gbuffer_set: int = 0):
-        what = BUF[name] | (int(gbuffer_set) << 8)  # RT_BUF_SET1 / RT_BUF_SET2
+        what = BUF[name] | (int(gbuffer_set) << 8)  # RT_BUF_SET1 / RT_BUF_SET2 / RT_BUF_SET3
         self._check(self.lib.rt_bind_buffer(self.h, what, device_ptr, nbytes), "rt_bind_buffer")
 
     def buffer_bytes(self, name: str) -> int:

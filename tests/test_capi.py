@@ -27,6 +27,15 @@ def test_dist_header_symbols_exported_and_bound(rtx):
     assert set(syms) == set(DIST_SIGNATURES)
 
 
+def test_gbuffer_set_constants_match_the_header(rtx):
+    """RT_GBUFFER_SETS / RT_BUF_SET1..3 (frame pipelining) and their Python mirrors agree."""
+    text = open(HEADER).read()
+    consts = {k: int(v, 0) for k, v in re.findall(r"#define\s+(RT_GBUFFER_SETS|RT_BUF_SET\d)\s+(\w+)", text)}
+    assert consts["RT_GBUFFER_SETS"] == rtx.GBUFFER_SETS
+    for k in range(1, rtx.GBUFFER_SETS):
+        assert consts["RT_BUF_SET%d" % k] == k << 8 == getattr(rtx, "BUF_SET%d" % k)
+
+
 def test_header_declares_the_renderer_api():
     syms = declared_symbols()
     for s in ("rt_create", "rt_init", "rt_draw", "rt_destroy", "rt_build_bvh", "rt_trace_primary",

@@ -1,13 +1,14 @@
 """Frame pipelining (rt_set_post_stream): the denoise/post chain of frame f on a second
-stream, overlapping the trace of frame f+1 into the other G-buffer set.  Every output after
-a 6-frame moving-camera sequence, and the RGBA8 image of every frame, must be identical to
-the serial order (and to each other frame-by-frame)."""
+stream, overlapping the trace of frame f+1 into the next G-buffer set.  Every output after a
+9-frame moving-camera sequence (each of the RT_GBUFFER_SETS = 4 sets reused at least once), and
+the RGBA8 image of every frame, must be identical to the serial order (and to each other
+frame-by-frame)."""
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-W, H, FRAMES = 320, 180, 6
+W, H, FRAMES = 320, 180, 9
 
 
 def post_stream():

@@ -118,7 +118,7 @@ def worker_sets(rank, world, port, result_dir):
 
 
 def test_strip_allgather_pipelined_sets(tmp_path):
-    """Frame pipelining binds three G-buffer sets; gather(set k) assembles set k only."""
+    """StripGather over three bound G-buffer sets (any count works): gather(set k) assembles set k only."""
     import torch.multiprocessing as mp
 
     world = 2

@@ -22,7 +22,8 @@ CPP_OBJS := $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.cpp.o,$(CPP_SRCS))
 ORC_SRCS := $(wildcard oracle/*.cpp)
 ORC_HDRS := $(wildcard oracle/*.h) $(CSRC)/rtmath.h $(CSRC)/soil_textures.h
 
-all: $(LIBDIR)/librtx.so $(LIBDIR)/librtx_rccl.so oracle/_build/liboracle.so oracle/_build/liboracle_libm.so
+all: $(LIBDIR)/librtx.so $(LIBDIR)/librtx_rccl.so oracle/_build/liboracle.so oracle/_build/liboracle_libm.so \
+     oracle/_build/liboracle_libm_fma.so
 
 $(OBJDIR)/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -48,6 +49,24 @@ oracle/_build/liboracle.so: $(ORC_SRCS) $(ORC_HDRS) $(CSRC)/soil_textures.cpp
 oracle/_build/liboracle_libm.so: $(ORC_SRCS) $(ORC_HDRS) $(CSRC)/soil_textures.cpp
 	@mkdir -p oracle/_build
 	$(CXX) $(CXXFLAGS) -DORC_LIBM -shared -o $@ $(ORC_SRCS) $(CSRC)/soil_textures.cpp -lpthread
+
+# ... and with nvcc's default contraction (the reference builds with CMake's nvcc defaults,
+# CMakeLists.txt:42, no --fmad=false): every a*b+c the compiler finds becomes one fused multiply-add,
+# in the restatement of the reference's device code.  The procedural scene and the soil textures
+# are host code in the reference (terrain.cpp) and inputs here, so they stay uncontracted.
+ORC_FMA_DEV  := $(filter-out oracle/scene.cpp,$(ORC_SRCS))
+ORC_FMA_OBJS := $(patsubst oracle/%.cpp,oracle/_build/fma/%.o,$(ORC_FMA_DEV))
+oracle/_build/fma/%.o: oracle/%.cpp $(ORC_HDRS)
+	@mkdir -p oracle/_build/fma
+	$(CXX) $(filter-out -ffp-contract=off,$(CXXFLAGS)) -ffp-contract=fast -mfma -DORC_LIBM -c $< -o $@
+oracle/_build/fma/scene.o: oracle/scene.cpp $(ORC_HDRS)
+	@mkdir -p oracle/_build/fma
+	$(CXX) $(CXXFLAGS) -DORC_LIBM -c $< -o $@
+oracle/_build/fma/soil_textures.o: $(CSRC)/soil_textures.cpp $(ORC_HDRS)
+	@mkdir -p oracle/_build/fma
+	$(CXX) $(CXXFLAGS) -DORC_LIBM -c $< -o $@
+oracle/_build/liboracle_libm_fma.so: $(ORC_FMA_OBJS) oracle/_build/fma/scene.o oracle/_build/fma/soil_textures.o
+	$(CXX) -shared -o $@ $^ -lpthread
 
 clean:
 	rm -rf $(LIBDIR) oracle/_build

@@ -26,7 +26,12 @@ extern "C" {
 #define RT_ERR_NO_DEVICE (-5)   /* no gfx950 device visible */
 #define RT_ERR_DEVICE (-6)      /* a kernel reported a failure (rt_last_error has the text): the LBVH's
                                    TLAS workgroup timed out waiting for a batch; the frames since the
-                                   last check may be wrong, the renderer re-armed itself */
+                                   last check may be wrong, the renderer re-armed itself.  Reported
+                                   once, by the call that finds it: rt_sync, rt_build_bvh, the draws
+                                   and the reads (rt_get_buffer, rt_download, rt_get_ray_count,
+                                   rt_save_image ...).  Setters (rt_set_*stream, rt_bind_buffer,
+                                   rt_set_collective_hook, rt_upload_texture) never return it: they
+                                   do their work and leave the report to the next such call */
 
 typedef struct rt_context rt_context;
 
@@ -35,7 +40,12 @@ typedef struct rt_context rt_context;
 /* RayTracer::RayTracer(screenWidth, screenHeight), kernel.cuh:435-441, plus LoadConfig
  * (configLoader.cpp:5-27).  config_toml may be NULL (defaults) or a path to a TOML file with
  * the reference's [resolution] / [file] / [optimziation] tables; extensions: [scene]
- * chunkDim (VoxelsGenerator::kChunkDim, terrain.h:42), [render] spp, [render] device. */
+ * chunkDim (VoxelsGenerator::kChunkDim, terrain.h:42), [render] spp, [render] device.
+ * [tuning] (scheduling A/B aids; the defaults are the measured best): arena (bool),
+ * streams ("cumask" | "prio"), tracePerCu / trace4PerCu (0: automatic), chain ("serial" | "off" |
+ * "always"), shadeOnSide (bool), overlapAfter / cameraAfter (-1: automatic).  [debug] (fault
+ * injection, tests): bvhSkipPublish, bvhSkipPublishBuilds, bvhWaitMs.  The library reads no
+ * environment variables. */
 int rt_create(int screen_width, int screen_height, const char* config_toml, rt_context** out);
 
 /* RayTracer::init, init.cu:53-410: builds the procedural default scene, allocates every device
@@ -59,7 +69,7 @@ int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out);
  * caller-owned DEVICE memory (row pitch in bytes, 0 = width * 4; 4-byte aligned).  flags 0: returns
  * when the frame is complete, as the reference's draw does (it ends with a device sync).
  * RT_DRAW_ASYNC: returns once the frame is enqueued; frames are pipelined (the denoise/post of
- * frame f overlaps the trace of f+1 on an internal stream (low priority under RTX_STREAMS=prio) unless rt_set_post_stream
+ * frame f overlaps the trace of f+1 on an internal stream (low priority under [tuning] streams = "prio") unless rt_set_post_stream
  * named one) and each frame's target must stay valid until rt_sync (or a later synchronous
  * call) has returned.  rt_download(RT_ARR_RGBA8) reads the last frame's target. */
 #define RT_DRAW_ASYNC 1

@@ -17,6 +17,9 @@ LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 # the same restatement with host-libm transcendentals (ocommon.h ORC_LIBM): the parity-metric
 # reference that shares no transcendental code with the product
 LIBM_PATH = os.path.join(HERE, "_build", "liboracle_libm.so")
+# ... and with nvcc-style a*b+c contraction into fused multiply-adds (Makefile liboracle_libm_fma.so)
+LIBM_FMA_PATH = os.path.join(HERE, "_build", "liboracle_libm_fma.so")
+_PATHS = {"libm": LIBM_PATH, "libm_fma": LIBM_FMA_PATH}
 DATA_DIR = os.path.join(os.path.dirname(HERE), "real-time-ray-tracing_amd", "data")
 
 NODE_DTYPE = np.dtype([("lmin", "<f4", 3), ("lmax", "<f4", 3), ("rmin", "<f4", 3), ("rmax", "<f4", 3),
@@ -55,10 +58,13 @@ _variant = "rtmath"
 
 
 @contextlib.contextmanager
-def libm():
-    """Run the oracle calls inside the block on the host-libm build (liboracle_libm.so)."""
+def libm(variant: str = "libm"):
+    """Run the oracle calls inside the block on the host-libm build (liboracle_libm.so), or with
+    variant "libm_fma" on that build with a*b+c contracted to fused multiply-adds."""
     global _variant
-    old, _variant = _variant, "libm"
+    if variant not in _PATHS:
+        raise ValueError(variant)
+    old, _variant = _variant, variant
     try:
         yield
     finally:
@@ -66,7 +72,7 @@ def libm():
 
 
 def lib() -> C.CDLL:
-    path = LIBM_PATH if _variant == "libm" else LIB_PATH
+    path = _PATHS.get(_variant, LIB_PATH)
     if path not in _libs:
         if not os.path.exists(path):
             raise RuntimeError("oracle not built: %s (run make)" % path)

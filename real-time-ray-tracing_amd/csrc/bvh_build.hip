@@ -566,15 +566,24 @@ constexpr uint32_t kTlasWaveMax = 64;
 // RT_ERR_DEVICE and answer by re-arming the counters.  The counter is re-armed here by subtracting
 // B, not by storing 0: a late publisher's count then still lands, and the counter is back at 0 when
 // the launch ends whatever the timing.
+//
+// The count is compared signed: after a timeout the counter sits below zero (wrapped) until the
+// host re-arms it, and a build already queued behind the faulty one must not read that wrapped
+// count as complete — it waits, times out and reports in turn (its sequence number goes to the
+// second status word), instead of reading leaf boxes its batches are still publishing.
+RT_DEV bool tlas_short(uint32_t seen, uint32_t B) { return (int32_t)(seen - B) < 0; }
 RT_DEV void tlas_wait(const BvhBuildParams& P, uint32_t B) {
     if (threadIdx.x == 0) {
         uint32_t seen = xwg_load(P.counter);
-        if (seen < B) {
+        if (tlas_short(seen, B)) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while ((seen = xwg_load(P.counter)) < B && __builtin_amdgcn_s_memrealtime() - t0 < P.waitTicks)
+            while (tlas_short(seen = xwg_load(P.counter), B) && __builtin_amdgcn_s_memrealtime() - t0 < P.waitTicks)
                 __builtin_amdgcn_s_sleep(2);
         }
-        if (seen < B) report_status(P.status, kStatusTlasTimeout, B - seen);
+        if (tlas_short(seen, B)) {
+            report_status(P.status, kStatusTlasTimeoutBuild, P.buildSeq);
+            report_status(P.status, kStatusTlasTimeout, B - seen);
+        }
         xwg_acquire();
     }
     __syncthreads();  // the boxes are read below with agent-coherent loads only

@@ -5,7 +5,8 @@
 
 // words of rt_context::status, the pinned host block kernels report failures into (rt_device.h
 // report_status; checked by sync_streams and rt_build_bvh)
-constexpr int kStatusTlasTimeout = 0;  // the TLAS workgroup gave up waiting: the number of missing batches
+constexpr int kStatusTlasTimeout = 0;       // the TLAS workgroup gave up waiting: the number of missing batches
+constexpr int kStatusTlasTimeoutBuild = 1;  // ... and the sequence number of the (last) build that did
 
 struct BvhBuildParams {
     const float* vertices;     // [nv][3]
@@ -33,6 +34,7 @@ struct BvhBuildParams {
     uint32_t* status;          // pinned host words of device failure reports (rt_device.h report_status)
     uint64_t waitTicks;        // the TLAS workgroup's wait bound in s_memrealtime ticks
     uint32_t skipPublish;      // fault injection: this batch does not publish (0xFFFFFFFF: none)
+    uint32_t buildSeq;         // this build's sequence number in the context (reported with a timeout)
 };
 
 struct TraceCamera {

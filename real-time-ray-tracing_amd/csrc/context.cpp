@@ -111,10 +111,6 @@ bool load_triangle_bin(const std::string& path, rtscene::SceneMesh& m, std::stri
 
 namespace {
 constexpr size_t kArenaChunk = 256ull << 20, kArenaMaxBuffer = 64ull << 20, kArenaAlign = 2ull << 20;
-bool arena_enabled() {
-    static const bool on = getenv("RTX_NO_ARENA") == nullptr;  // A/B aid
-    return on;
-}
 int raw_alloc(rt_context* ctx, void** p, size_t bytes) {
     void* q = nullptr;
     hipError_t e = hipMalloc(&q, bytes);
@@ -134,18 +130,15 @@ int raw_alloc(rt_context* ctx, void** p, size_t bytes) {
 // had created its pools, rt_draw_device(RT_DRAW_ASYNC) ran 1.42 ms/frame instead of 1.10, two of
 // its streams having landed on one queue.  A stream created with a CU mask gets a hardware queue
 // of its own, so the renderer's streams use a full mask; they then carry no priority, which
-// measured no difference.  RTX_STREAMS=prio: plain streams with priorities.
+// measured no difference.  [tuning] streams = "prio": plain streams with priorities.
 // hipExtStreamCreateWithCUMask makes blocking streams (hipStreamDefault): work on the null stream
 // (a framework's default-stream kernels, synchronous hipMemcpy / hipMemset) and the renderer's
 // streams wait for each other.  The renderer itself issues synchronous copies only outside
 // frames (rt_init, rt_bind_buffer, host reads, the ray-counter reset); a host that keeps default-
-// stream work in flight beside pipelined frames should set RTX_STREAMS=prio (non-blocking streams).
+// stream work in flight beside pipelined frames should set [tuning] streams = "prio" (non-blocking
+// streams).
 int rt_create_stream(rt_context* ctx, hipStream_t* s, bool high) {
-    static const bool prio = [] {
-        const char* v = getenv("RTX_STREAMS");
-        return v && strcmp(v, "prio") == 0;
-    }();
-    if (!prio) {
+    if (!ctx->tune.prioStreams) {
         uint32_t mask[32];  // 1024 CUs' worth of bits; bits past the device's CU count are ignored
         for (uint32_t& m : mask) m = 0xFFFFFFFFu;
         HIP_TRY(ctx, hipExtStreamCreateWithCUMask(s, 32, mask));
@@ -164,7 +157,7 @@ int rt_create_stream(rt_context* ctx, hipStream_t* s, bool high) {
 // used queue planes get allocations of their own.
 int rt_dalloc_bytes(rt_context* ctx, void** p, size_t bytes) {
     if (bytes < 16) bytes = 16;
-    if (!arena_enabled() || bytes > kArenaMaxBuffer) return raw_alloc(ctx, p, bytes);
+    if (!ctx->tune.arena || bytes > kArenaMaxBuffer) return raw_alloc(ctx, p, bytes);
     size_t at = (ctx->arenaUsed + kArenaAlign - 1) / kArenaAlign * kArenaAlign;
     if (!ctx->arenaPtr || at + bytes > ctx->arenaCap) {
         void* chunk = nullptr;
@@ -330,7 +323,20 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
     ctx->stripIndex = rttoml::find_or_int(doc, "render", "stripIndex", 0);
     ctx->materialOverride = rttoml::find_or_int(doc, "render", "materialOverride", -1);
     ctx->bvhSkipPublish = (uint32_t)rttoml::find_or_int(doc, "debug", "bvhSkipPublish", -1);
+    ctx->bvhSkipBuilds = rttoml::find_or_int(doc, "debug", "bvhSkipPublishBuilds", -1);
     ctx->bvhWaitMs = rttoml::find_or_float(doc, "debug", "bvhWaitMs", 1000.0f);
+    {
+        rt_context::Tuning& t = ctx->tune;
+        t.arena = rttoml::find_or_bool(doc, "tuning", "arena", true);
+        t.prioStreams = rttoml::find_or_string(doc, "tuning", "streams", "cumask") == "prio";
+        t.tracePerCu = rttoml::find_or_int(doc, "tuning", "tracePerCu", 0);
+        t.trace4PerCu = rttoml::find_or_int(doc, "tuning", "trace4PerCu", 0);
+        const std::string chain = rttoml::find_or_string(doc, "tuning", "chain", "serial");
+        t.chain = chain == "off" ? 0 : chain == "always" ? 2 : 1;
+        t.shadeOnSide = rttoml::find_or_bool(doc, "tuning", "shadeOnSide", true);
+        t.overlapAfter = rttoml::find_or_int(doc, "tuning", "overlapAfter", -1);
+        t.cameraAfter = rttoml::find_or_int(doc, "tuning", "cameraAfter", -1);
+    }
     if (ctx->screenW <= 0 || ctx->screenH <= 0 || ctx->screenW > 16384 || ctx->screenH > 16384 || ctx->spp < 1 ||
         ctx->spp > 64 || ctx->chunkDim < 1 || ctx->chunkDim > 8 ||
         (ctx->bvhThreads != 0 && ctx->bvhThreads != 512 && ctx->bvhThreads != 1024)) {
@@ -409,7 +415,7 @@ int rt_init(rt_context* ctx) {
     HIP_TRY(ctx, hipHostMalloc((void**)&ctx->status, 64, hipHostMallocDefault));
     memset(ctx->status, 0, 64);
 
-    // the context stream (the trace chain, a frame's critical path); with RTX_STREAMS=prio it is
+    // the context stream (the trace chain, a frame's critical path); with [tuning] streams = "prio" it is
     // created at the highest priority and the side / internal post streams at the lowest, otherwise
     // all are CU-masked streams without priority (rt_create_stream)
     if (int rc = rt_create_stream(ctx, &ctx->ownStream, true)) return rc;
@@ -485,7 +491,7 @@ int rt_init(rt_context* ctx) {
 
 void rt_destroy(rt_context* ctx) {
     if (!ctx) return;
-    if (ctx->inited) (void)sync_streams(ctx);  // also when the context stream is the null stream
+    if (ctx->inited) (void)sync_streams(ctx, false);  // also when the context stream is the null stream
     for (hipEvent_t e : {ctx->overlapEv, ctx->cameraGate, ctx->buildDone[0], ctx->buildDone[1], ctx->bvhFree[0], ctx->bvhFree[1]})
         if (e) (void)hipEventDestroy(e);
     for (int k = 0; k < kGbSets; ++k)
@@ -629,7 +635,9 @@ int rt_build_bvh(rt_context* ctx) {
     p.cus = (uint32_t)ctx->cuCount;
     p.status = ctx->status;
     p.waitTicks = (uint64_t)((double)ctx->bvhWaitMs * (double)ctx->wallTicksPerMs);
-    p.skipPublish = ctx->bvhSkipPublish;
+    p.skipPublish = ctx->bvhSkipBuilds != 0 ? ctx->bvhSkipPublish : 0xFFFFFFFFu;
+    if (ctx->bvhSkipBuilds > 0) --ctx->bvhSkipBuilds;
+    p.buildSeq = ++ctx->buildSeq;
     HIP_TRY(ctx, rtk_launch_build_bvh(&p, stream));
     if (ctx->postStream) {
         HIP_TRY(ctx, hipEventRecord(ctx->buildDone[ctx->bvhSet], stream));
@@ -774,7 +782,7 @@ int rt_time_frame_kernels(rt_context* ctx, int first_frame, int iters, float* ke
 int rt_frame_marks_begin(rt_context* ctx, int frames, uint32_t kernel_mask) {
     if (!ctx || frames < 0 || frames > 100000 || (kernel_mask & ~((1u << kFrameKernels) - 1u)) != 0) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_frame_marks_begin before rt_init"; return RT_ERR_STATE; }
-    if (int rc = sync_streams(ctx)) return rc;  // the events of earlier frames are complete
+    if (int rc = sync_streams(ctx, false)) return rc;  // the events of earlier frames are complete
     ctx->dnMarks = nullptr;
     const size_t need = (size_t)frames * 2 * kFrameKernels;
     while (ctx->markPool.size() < need) {

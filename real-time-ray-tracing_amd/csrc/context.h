@@ -188,7 +188,22 @@ struct rt_context {
     // [debug] fault injection (tests): a batch whose TLAS leaf box is never published, and the TLAS
     // workgroup's wait bound (rt_device.h report_status)
     uint32_t bvhSkipPublish = 0xFFFFFFFFu;
+    int bvhSkipBuilds = -1;  // [debug] bvhSkipPublishBuilds: the fault applies to this many builds (-1: all)
     float bvhWaitMs = 1000.0f;
+    uint32_t buildSeq = 0;   // LBVH builds issued so far (a timeout report names the build)
+    // [tuning] scheduling knobs (A/B aids, config only; the defaults are the measured best,
+    // DESIGN.md §7): the device-buffer arena, plain prioritised streams instead of CU-masked ones,
+    // the queue tracers' workgroups per CU (0: automatic), the bounce-chain choice (0 off, 1 serial
+    // frames with a short queue 3, 2 always), the shade kernel on the side stream, and the
+    // pipelined frame's issue points (-1: automatic)
+    struct Tuning {
+        bool arena = true;
+        bool prioStreams = false;
+        int tracePerCu = 0, trace4PerCu = 0;
+        int chain = 1;
+        bool shadeOnSide = true;
+        int overlapAfter = -1, cameraAfter = -1;
+    } tune;
 
     std::string err;
     bool inited = false;
@@ -301,7 +316,7 @@ int dalloc(rt_context* ctx, T** p, size_t bytes) {
 int rt_create_stream(rt_context* ctx, hipStream_t* s, bool high);  // context.cpp: renderer streams
 extern "C" int ensure_bvh_pair(rt_context* ctx);  // frame.cpp: second LBVH set, side stream, build events
 int rt_frame_init(rt_context* ctx);  // frame.cpp: sky tables, textures, G-buffers
-int sync_streams(rt_context* ctx);   // frame.cpp: context, post and side streams
+int sync_streams(rt_context* ctx, bool report = true);  // frame.cpp: context, post and side streams (report: RT_ERR_DEVICE)
 void poll_q3(rt_context* ctx);       // frame.cpp: the last serial frame's queue-3 length, if stored
 int check_device_status(rt_context* ctx);  // frame.cpp: kernel failure reports (RT_ERR_DEVICE)
 bool strip_local_denoise(const rt_context* ctx, uint32_t& a, uint32_t& b);  // frame.cpp: next denoise's rows

@@ -117,7 +117,7 @@ int update_sky(rt_context* ctx) {
     fr.sunDir[0] = sunDir.x; fr.sunDir[1] = sunDir.y; fr.sunDir[2] = sunDir.z;
     if (fr.skyValid && !sp.needRegenerate && sky_params_equal(sp, fr.lastSky)) return RT_OK;
     if (ctx->postStream) {  // frame pipelining: nothing may read the sky while it is rewritten
-        const int rc = sync_streams(ctx);
+        const int rc = sync_streams(ctx, false);
         if (rc != RT_OK) return rc;
     }
     sp.sunScalar = sp.sunScalar > 0.00001f ? sp.sunScalar : 0.00001f;
@@ -303,8 +303,11 @@ hipError_t overlap_hook(void* arg, int kernel) {
 }
 }  // namespace
 
-// wait for the context stream and, when set, the post stream
-int sync_streams(rt_context* ctx) {
+// wait for the context stream and, when set, the post stream.  `report`: return a kernel's failure
+// report (RT_ERR_DEVICE) — rt_sync, the draws, the reads and rt_build_bvh do; the setters that only
+// need the streams idle (stream / hook / buffer / texture changes) pass false and do their work, the
+// report then waiting for the next reporting call.
+int sync_streams(rt_context* ctx, bool report) {
     if (ctx->postStream) {
         const int rc = issue_pending_post(ctx);
         if (rc != RT_OK) return rc;
@@ -313,7 +316,7 @@ int sync_streams(rt_context* ctx) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->postStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->postStream));
     poll_q3(ctx);
-    return check_device_status(ctx);
+    return report ? check_device_status(ctx) : RT_OK;
 }
 
 // The last serial frame's queue-3 length (rt_path_trace's chain choice), if k_pt_resolve has
@@ -335,13 +338,16 @@ void poll_q3(rt_context* ctx) {
 int check_device_status(rt_context* ctx) {
     const uint32_t missing = __atomic_load_n(&ctx->status[kStatusTlasTimeout], __ATOMIC_ACQUIRE);
     if (!missing) return RT_OK;
+    const uint32_t build = __atomic_load_n(&ctx->status[kStatusTlasTimeoutBuild], __ATOMIC_ACQUIRE);
     if (ctx->sideStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->sideStream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     for (const BvhBufs& b : ctx->bvh)
         if (b.counter) HIP_TRY(ctx, hipMemset(b.counter, 0, 64));
     __atomic_store_n(&ctx->status[kStatusTlasTimeout], 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&ctx->status[kStatusTlasTimeoutBuild], 0u, __ATOMIC_RELEASE);
     ctx->err = "LBVH build: the TLAS workgroup timed out waiting for " + std::to_string(missing) +
-               " batch publication(s); the TLAS of that build (and the frames traced on it) may be wrong";
+               " batch publication(s) (last in build " + std::to_string(build) +
+               "); the TLAS of that build (and the frames traced on it) may be wrong";
     return RT_ERR_DEVICE;
 }
 
@@ -467,18 +473,16 @@ int rt_frame_init(rt_context* ctx) {
         // more rays than lanes, lanes refill as rays finish, and the CUs keep room for the
         // denoise and next-frame waves beside the traversal tail (measured: DESIGN.md §7)
         int tracePerCu = perCu >= 3 ? 3 : (perCu > 0 ? perCu : 1), trace4PerCu = 1;
-        if (const char* a = getenv("RTX_TRACE_PER_CU"))  // tuning aids
-            if (atoi(a) > 0 && atoi(a) <= perCu) tracePerCu = atoi(a);
-        if (const char* a = getenv("RTX_TRACE4_PER_CU"))
-            if (atoi(a) > 0 && atoi(a) <= perCu) trace4PerCu = atoi(a);
+        const rt_context::Tuning& tn = ctx->tune;  // [tuning] tracePerCu / trace4PerCu (A/B aids)
+        if (tn.tracePerCu > 0 && tn.tracePerCu <= perCu) tracePerCu = tn.tracePerCu;
+        if (tn.trace4PerCu > 0 && tn.trace4PerCu <= perCu) trace4PerCu = tn.trace4PerCu;
         ws.traceBlocks = (uint32_t)(cus * tracePerCu);
         // one GPU: a short queue 3 (below kTrace3Short rays, the default view's 323 k) is traced by
         // 2 workgroups per CU, which leaves the next frame's camera waves more room (1.091 -> 1.081
         // ms/frame, four repeats); a long one (the terrain view) keeps all of them (2 per CU there:
         // 4.14 -> 4.44 ms); strip ranks keep 3 (at 2 ranks 0.710 vs 0.727 ms, equal at 4 and 8)
         ws.trace3ShortBlocks = ctx->stripCount == 1 ? (uint32_t)(cus * 2) : 0u;
-        ws.chain = 1;  // RTX_CHAIN=off|serial|always: A/B aid (default serial)
-        if (const char* a = getenv("RTX_CHAIN")) ws.chain = strcmp(a, "off") == 0 ? 0 : strcmp(a, "always") == 0 ? 2 : 1;
+        ws.chain = (uint32_t)tn.chain;  // [tuning] chain = "off" | "serial" | "always" (default serial)
         ws.trace4Blocks = (uint32_t)(cus * trace4PerCu);
     }
     ALLOC(fr.colorB, P * 8);
@@ -576,7 +580,7 @@ int rt_upload_texture(rt_context* ctx, int which, const uint16_t* texels, int wi
         return RT_ERR_ARG;
     }
     if (ctx->inited) {  // frames in flight may be sampling the old chain
-        const int rc = sync_streams(ctx);
+        const int rc = sync_streams(ctx, false);
         if (rc != RT_OK) return rc;
     }
     HIP_TRY(ctx, hipMemcpyAsync(chain, texels, (size_t)width * height * channels * 2, hipMemcpyHostToDevice, ctx->stream));
@@ -726,14 +730,17 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     }
     // rt_frame_marks_begin: this path trace's kernels are bracketed by events (caller's timed frames)
     hipEvent_t* const savedMarks = ctx->ptMarks;
-    if (!ctx->ptMarks && ctx->markNext < ctx->markFrames)
-        ctx->ptMarks = ctx->markRing.data() + (size_t)(ctx->markNext++) * 2 * kFrameKernels;
+    const bool ringSlot = !ctx->ptMarks && ctx->markNext < ctx->markFrames;
+    if (ringSlot) ctx->ptMarks = ctx->markRing.data() + (size_t)(ctx->markNext++) * 2 * kFrameKernels;
     ctx->dnMarks = ctx->ptMarks ? ctx->ptMarks + 2 * kPtKernels : nullptr;  // for this frame's rt_denoise_post
     struct MarksReset {  // every return path leaves ptMarks as it found it
         rt_context* c;
         hipEvent_t* m;
         ~MarksReset() { c->ptMarks = m; }
     } marksReset{ctx, savedMarks};
+    if (ringSlot)  // the slot's denoise pairs, recorded once here: a frame no rt_denoise_post follows
+        for (int k = 2 * kPtKernels; k < 2 * kFrameKernels; ++k)  // reads 0 ms for them
+            if (ctx->ptMarks[k]) HIP_TRY(ctx, hipEventRecord(ctx->ptMarks[k], cs));
     HIP_TRY(ctx, rtk_launch_pt_camera(&p, cs, ctx->ptMarks));
     // the shade kernel follows on the side stream, so it runs beside the previous frame's queue
     // tracers instead of after them (its bounce queues are this set's own, camQ3[g] ..)
@@ -747,17 +754,20 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->camDone[g], 0));
     }
     PtLaunchHook hook{overlap_hook, ctx};
-    if (!side && !fr.q3Pending) {  // serial frames: queue 3's length for the next frame's chain choice
+    const bool askQ3 = !side && !fr.q3Pending;  // serial frames: queue 3's length for the next chain choice
+    if (askQ3) {
         if (!fr.q3Host) {
             HIP_TRY(ctx, hipHostMalloc((void**)&fr.q3Host, sizeof(unsigned long long), hipHostMallocDefault));
             *fr.q3Host = 0ull;
         }
         p.ws.q3HostOut = fr.q3Host;  // stored by k_pt_resolve (no copy on the stream)
         p.ws.q3Tag = ++fr.q3Tag;
-        fr.q3Pending = true;
     }
     if (shadeSide) HIP_TRY(ctx, rtk_launch_pt_rest_after_shade(&p, ctx->stream, ctx->ptMarks, &hook));
     else HIP_TRY(ctx, rtk_launch_pt_rest(&p, ctx->stream, ctx->ptMarks, ctx->postStream ? &hook : nullptr));
+    // pending only once the launches that store it are enqueued: a failed launch leaves the next
+    // serial frame to ask again instead of freezing the chain choice
+    if (askQ3) fr.q3Pending = true;
     if (ctx->postPending && (rc = issue_pending_post(ctx)) != RT_OK) return rc;
     if (ctx->postStream) {
         HIP_TRY(ctx, hipEventRecord(ctx->restDone[g], ctx->stream));
@@ -1046,7 +1056,7 @@ int rt_draw_device(rt_context* ctx, void* rgba8_device, size_t pitch_bytes, int 
 int rt_set_stream(rt_context* ctx, void* stream) {
     if (!ctx) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_set_stream before rt_init"; return RT_ERR_STATE; }
-    int rc = sync_streams(ctx);
+    int rc = sync_streams(ctx, false);
     if (rc != RT_OK) return rc;
     ctx->stream = stream == RT_OWN_STREAM ? ctx->ownStream : (hipStream_t)stream;  // NULL: the null stream
     return RT_OK;
@@ -1055,7 +1065,7 @@ int rt_set_stream(rt_context* ctx, void* stream) {
 int rt_set_collective_hook(rt_context* ctx, rt_collective_fn fn, void* arg) {
     if (!ctx) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_set_collective_hook before rt_init"; return RT_ERR_STATE; }
-    int rc = sync_streams(ctx);
+    int rc = sync_streams(ctx, false);
     if (rc != RT_OK) return rc;
     ctx->hook = fn;
     ctx->hookArg = arg;
@@ -1078,7 +1088,7 @@ int rt_set_hook_stages(rt_context* ctx, uint32_t stage_mask) {
 int rt_set_gather_stream(rt_context* ctx, void* stream) {
     if (!ctx) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_set_gather_stream before rt_init"; return RT_ERR_STATE; }
-    int rc = sync_streams(ctx);
+    int rc = sync_streams(ctx, false);
     if (rc != RT_OK) return rc;
     for (int k = 0; k < kGbSets; ++k)
         if (!ctx->gatherDone[k]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->gatherDone[k], hipEventDisableTiming));
@@ -1126,7 +1136,7 @@ int ensure_bvh_pair(rt_context* ctx) {
 int rt_set_post_stream(rt_context* ctx, void* stream) {
     if (!ctx) return RT_ERR_ARG;
     if (!ctx->inited) { ctx->err = "rt_set_post_stream before rt_init"; return RT_ERR_STATE; }
-    int rc = sync_streams(ctx);
+    int rc = sync_streams(ctx, false);
     if (rc != RT_OK) return rc;
     FrameResources& fr = ctx->fr;
     for (int k = 0; k < kGbSets; ++k) fr.setInFlight[k] = false;
@@ -1146,11 +1156,10 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
         ALLOC(fr.gMotion[k], P * 4);
         if ((rc = alloc_ws_slot(ctx, k, false)) != RT_OK) return rc;
     }
-    // the shade kernel runs on the side stream, with bounce queues per set (RTX_SHADE_SIDE=0|1
-    // overrides: A/B aid); measured: one GPU 1.025 -> 0.970 ms/frame, one rank's
-    // share at 2 / 4 / 8 ranks 0.648 -> 0.650 / 0.495 -> 0.482 / 0.453 -> 0.411 ms
-    ctx->shadeOnSide = true;
-    if (const char* a = getenv("RTX_SHADE_SIDE")) ctx->shadeOnSide = atoi(a) != 0;
+    // the shade kernel runs on the side stream, with bounce queues per set ([tuning] shadeOnSide:
+    // A/B aid); measured: one GPU 1.025 -> 0.970 ms/frame, one rank's share at
+    // 2 / 4 / 8 ranks 0.648 -> 0.650 / 0.495 -> 0.482 / 0.453 -> 0.411 ms
+    ctx->shadeOnSide = ctx->tune.shadeOnSide;
     for (int k = 1; ctx->shadeOnSide && k < kGbSets; ++k)
         if ((rc = alloc_ws_slot(ctx, k, true)) != RT_OK) return rc;
 #undef ALLOC
@@ -1173,8 +1182,8 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
     // queue-3 traversal), after this frame's trace<3> on two GPUs and its resume<3> on four, where
     // a rank's tails are shorter, and after its shade on eight (measured per N: DESIGN.md §7)
     ctx->cameraAfter = ctx->stripCount == 1 ? 0 : ctx->stripCount == 2 ? 2 : ctx->stripCount < 8 ? 3 : 1;
-    if (const char* a = getenv("RTX_OVERLAP_AFTER")) ctx->overlapAfter = atoi(a);  // tuning aids
-    if (const char* a = getenv("RTX_CAMERA_AFTER")) ctx->cameraAfter = atoi(a);
+    if (ctx->tune.overlapAfter >= 0) ctx->overlapAfter = ctx->tune.overlapAfter;  // [tuning] A/B aids
+    if (ctx->tune.cameraAfter >= 0) ctx->cameraAfter = ctx->tune.cameraAfter;
     ctx->postStream = (hipStream_t)stream;
     return RT_OK;
 }
@@ -1188,7 +1197,7 @@ int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
     const size_t need = rt_alloc_bytes(ctx, name);  // later frames may be larger than the current one
     if (need == 0 || bytes < need) { ctx->err = "rt_bind_buffer: unknown buffer or too small"; return RT_ERR_ARG; }
     if (((uintptr_t)device_ptr & 15u) != 0) { ctx->err = "rt_bind_buffer: pointer must be 16-byte aligned"; return RT_ERR_ARG; }
-    int rc = sync_streams(ctx);
+    int rc = sync_streams(ctx, false);
     if (rc != RT_OK) return rc;
     FrameResources& fr = ctx->fr;
     switch (name) {

@@ -835,7 +835,7 @@ RT_DEV void store_path_L(const PathCtx& c, const PathVars& v, uint32_t p, uint32
 
 // Resumes the samples of queue kStep (3 or 4) once k_trace_queue has written their hits.
 template <int kStep, bool kMF, bool kGlossy>
-__global__ __launch_bounds__(256, kStep == 3 ? 3 : 4) void k_pt_resume(PathTraceParams P) {
+__global__ __launch_bounds__(256, kStep == 3 ? (kGlossy ? 2 : 3) : 4) void k_pt_resume(PathTraceParams P) {
     __shared__ uint32_t sob[256];
     __shared__ unsigned long long wgRays[4];
     // step 4 ends the path before any diffuse interaction: no light sampling there

@@ -189,8 +189,12 @@ class RtError(RuntimeError):
 
 def write_config(path: str, width: int, height: int, dynamic: bool = False, chunk_dim: int = 1, spp: int = 1,
                  extra: str = "", max_size=(3840, 2160), camera_file: str | None = None, min_size=(640, 480),
-                 target_fps: float = 60.0, mesh_file: str | None = None) -> str:
-    """Write a config.toml with the reference's three tables (resources/config.toml) + extensions."""
+                 target_fps: float = 60.0, mesh_file: str | None = None, tuning: dict | None = None) -> str:
+    """Write a config.toml with the reference's three tables (resources/config.toml) + extensions.
+
+    `tuning`: the [tuning] table (scheduling A/B aids, include/rtx_amd.h).  When None, the
+    RTX_TUNING environment variable ("key=value,key=value", e.g. "chain=off,tracePerCu=2") fills
+    it: the A/B tools (tools/ab.sh) set it per variant.  The library itself reads no environment."""
     with open(path, "w") as f:
         f.write("[resolution]\nwidth = %d\nheight = %d\n\n" % (width, height))
         if camera_file:
@@ -206,7 +210,33 @@ def write_config(path: str, width: int, height: int, dynamic: bool = False, chun
             f.write('meshFile = "%s"\n' % mesh_file)
         f.write("\n[render]\nspp = %d\n" % spp)
         f.write(extra)
+        if tuning is None:
+            tuning = tuning_from_env()
+        if tuning:
+            f.write("\n[tuning]\n")
+            for k, v in tuning.items():
+                f.write("%s = %s\n" % (k, _toml_value(v)))
     return path
+
+
+def _toml_value(v) -> str:
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (int, float)):
+        return repr(v)
+    s = str(v)
+    if s in ("true", "false") or s.lstrip("-").isdigit():
+        return s
+    return '"%s"' % s
+
+
+def tuning_from_env() -> dict:
+    """RTX_TUNING="key=value,..." as a [tuning] table (A/B tools only)."""
+    out = {}
+    for item in filter(None, (x.strip() for x in os.environ.get("RTX_TUNING", "").split(","))):
+        k, _, v = item.partition("=")
+        out[k.strip()] = v.strip()
+    return out
 
 
 class RayTracer:

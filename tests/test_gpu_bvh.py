@@ -98,6 +98,34 @@ def test_tlas_wait_timeout_is_reported(rtx, tmp_path, chunk_dim, threads):
     rt.cleanup()
 
 
+@pytest.mark.parametrize("chunk_dim,threads", [(1, 1024), (2, 512)])
+def test_build_queued_behind_timeout_reports(rtx, tmp_path, chunk_dim, threads):
+    """A healthy build queued behind a faulty one on the same LBVH set, with no sync between them
+    (ADVICE r5): the faulty build leaves the launch counter one below zero until the host re-arms
+    it, so the second build's batches bring it only to B - 1.  tlas_wait compares signed: the
+    second build waits, times out and reports too (the report names build 2), instead of taking
+    the wrapped count as complete.  After the re-arm a build equals a fault-free context's."""
+    base = "bvhThreads = %d\n" % threads
+    extra = base + "\n[debug]\nbvhSkipPublish = 1\nbvhSkipPublishBuilds = 1\nbvhWaitMs = 20\n"
+    cfg = rtx.write_config(str(tmp_path / "fault.toml"), 64, 64, chunk_dim=chunk_dim, extra=extra)
+    rt = rtx.RayTracer(64, 64, cfg).init()
+    rt.build_bvh()  # build 1: batch 1 never publishes
+    rt.build_bvh()  # build 2: healthy, queued while build 1 still waits
+    with pytest.raises(rtx.RtError, match=r"RT_ERR_DEVICE .*for 1 batch publication\(s\) \(last in build 2\)"):
+        rt.sync()
+    rt.build_bvh()  # build 3, after the re-arm
+    rt.sync()
+    tlas, nodes = rt.download("TLAS_NODES").copy(), rt.download("NODES").copy()
+    rt.cleanup()
+    ok = rtx.RayTracer(64, 64, rtx.write_config(str(tmp_path / "ok.toml"), 64, 64, chunk_dim=chunk_dim,
+                                                 extra=base)).init()
+    ok.build_bvh()
+    ok.sync()
+    assert np.array_equal(ok.download("TLAS_NODES"), tlas)
+    assert np.array_equal(ok.download("NODES"), nodes)
+    ok.cleanup()
+
+
 def test_tlas_no_fault_no_report(rtx, tmp_path):
     """Healthy builds back to back with the bounded wait: no report, the TLAS equals the first one."""
     rt = build_gpu(rtx, tmp_path, 1, threads=1024)

@@ -19,8 +19,9 @@ def post_stream():
     return torch.cuda.Stream(device=0)
 
 
-def run(rtx, tmp_path, pipelined, per_frame):
-    cfg = rtx.write_config(str(tmp_path / ("p%d%d.toml" % (pipelined, per_frame))), W, H, spp=2)
+def run(rtx, tmp_path, pipelined, per_frame, tuning=None):
+    cfg = rtx.write_config(str(tmp_path / ("p%d%d.toml" % (pipelined, per_frame))), W, H, spp=2,
+                           tuning=tuning or {})
     rt = rtx.RayTracer(W, H, cfg).init()
     rt.set_delta_time(16.667)
     post = post_stream() if pipelined else None
@@ -58,13 +59,12 @@ def test_pipelined_frames_match_serial(rtx, tmp_path):
 
 
 @pytest.mark.parametrize("chain", ["always", "off"])
-def test_pipelined_chain_modes_match_serial(rtx, tmp_path, monkeypatch, chain):
+def test_pipelined_chain_modes_match_serial(rtx, tmp_path, chain):
     """The bounce chain as one launch (k_pt_chain: what serial frames run) and as four kernels
-    (what pipelined frames run), each pipelined, against serial frames (k_pt_chain): identical
-    outputs."""
+    (what pipelined frames run), each pipelined ([tuning] chain), against serial frames
+    (k_pt_chain): identical outputs."""
     ref, _, _ = run(rtx, tmp_path, False, False)
-    monkeypatch.setenv("RTX_CHAIN", chain)
-    got, _, _ = run(rtx, tmp_path, True, False)
+    got, _, _ = run(rtx, tmp_path, True, False, tuning={"chain": chain})
     for k in ref:
         assert np.array_equal(ref[k], got[k]), k
 

@@ -3,7 +3,8 @@
 # process under its own time limit; the chain stops at the first failure.
 #   tools/ab.sh <outdir> <repeats> "<variant>|<variant>|..." python3 tools/probe.py frames
 # A variant is a space-separated list of VAR=value settings applied to that run, e.g.
-#   "RTX_LIB=real-time-ray-tracing_amd/abl_x/librtx.so" | "" (the in-tree build) | "RTX_CHAIN=off"
+#   "RTX_LIB=real-time-ray-tracing_amd/abl_x/librtx.so" | "" (the in-tree build) | "RTX_TUNING=chain=off"
+# (RTX_TUNING becomes the config's [tuning] table in rtx.write_config; the library reads no environment)
 # Every run's last stdout line goes to <outdir>/ab.jsonl with its variant and repeat.
 set -u
 OUT=$1; REPS=$2; VARIANTS=$3; shift 3

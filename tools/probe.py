@@ -9,7 +9,7 @@ passes (tools/prof.sh).  DESIGN.md §4-§9 cite the subcommands.
   probe.py serial  [--view ...] [--n 10]                                      serial frames, each
                    stage synchronised (per-kernel profiles without overlap)
   probe.py stages  [--view ...]                                               serial per-kernel and
-                   per-stage times (rt_time_path_trace_kernels, rt_time_stage 0 / 2 / 3 / 4; RTX_CHAIN=off
+                   per-stage times (rt_time_path_trace_kernels, rt_time_stage 0 / 2 / 3 / 4; RTX_TUNING=chain=off
                    for the four bounce kernels instead of the fused chain)
   probe.py denoise [--view ...] [--n 20]                                      serial frames, then the
                    noise gating (active tiles) and the serial denoise + post ms

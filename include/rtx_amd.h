@@ -43,7 +43,8 @@ typedef struct rt_context rt_context;
  * chunkDim (VoxelsGenerator::kChunkDim, terrain.h:42), [render] spp, [render] device.
  * [tuning] (scheduling A/B aids; the defaults are the measured best): arena (bool),
  * streams ("cumask" | "prio"), tracePerCu / trace4PerCu (0: automatic), chain ("serial" | "off" |
- * "always"), shadeOnSide (bool), overlapAfter / cameraAfter (-1: automatic).  [debug] (fault
+ * "always"), shadeOnSide (bool), shadeBlocksPerCu (synchronous frames; 0: the kernel's residency),
+ * overlapAfter / cameraAfter (-1: automatic).  [debug] (fault
  * injection, tests): bvhSkipPublish, bvhSkipPublishBuilds, bvhWaitMs.  The library reads no
  * environment variables. */
 int rt_create(int screen_width, int screen_height, const char* config_toml, rt_context** out);

@@ -334,6 +334,7 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
         const std::string chain = rttoml::find_or_string(doc, "tuning", "chain", "serial");
         t.chain = chain == "off" ? 0 : chain == "always" ? 2 : 1;
         t.shadeOnSide = rttoml::find_or_bool(doc, "tuning", "shadeOnSide", true);
+        t.shadeBlocksPerCu = rttoml::find_or_int(doc, "tuning", "shadeBlocksPerCu", 0);
         t.overlapAfter = rttoml::find_or_int(doc, "tuning", "overlapAfter", -1);
         t.cameraAfter = rttoml::find_or_int(doc, "tuning", "cameraAfter", -1);
     }

@@ -202,6 +202,7 @@ struct rt_context {
         int tracePerCu = 0, trace4PerCu = 0;
         int chain = 1;
         bool shadeOnSide = true;
+        int shadeBlocksPerCu = 0;  // k_pt_shade0's grid per CU (0: its residency)
         int overlapAfter = -1, cameraAfter = -1;
     } tune;
 

@@ -468,6 +468,8 @@ int rt_frame_init(rt_context* ctx) {
         if (cus <= 0) cus = 256;
         // grid of the persistent shade / resume kernels: 5 workgroups per CU (measured)
         ws.persistBlocks = (uint32_t)(cus * 5);
+        ws.cus = (uint32_t)cus;
+        ws.shadeBlocksPerCu = (uint32_t)(ctx->tune.shadeBlocksPerCu > 0 ? ctx->tune.shadeBlocksPerCu : 0);
         // the queue tracers run below their residency (5 workgroups per CU at 32 KiB of LDS
         // stack each): queue 3 at 3 per CU, queue 4 at 1, so a bounce queue holds
         // more rays than lanes, lanes refill as rays finish, and the CUs keep room for the
@@ -721,6 +723,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     // this slot's G-buffers (the denoise of frame f-2) and camera outputs (shade of frame f-2).
     const bool side = ctx->postStream && !with_detail;
     hipStream_t cs = side ? ctx->sideStream : ctx->stream;
+    p.ws.shadeClaim = !ctx->postStream;  // dynamic batch claims in synchronous frames (pathtrace.hip)
     if (side) {
         if (fr.setInFlight[g]) HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->postDone[g], 0));
         if (fr.camInFlight[g]) HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->restDone[g], 0));

@@ -84,7 +84,9 @@ enum PtCounter : int { kCntQ3 = 0, kCntQ4 = 1, kCntFetch3 = 2, kCntFetch4 = 3, k
                        kCntSurface = 11, kCntVisCam = 12, kCntTstCam = 13, kCntVisShade = 14, kCntTstShade = 15,
                        kCntVisQ3 = 16, kCntTstQ3 = 17, kCntVisQ4 = 18, kCntTstQ4 = 19, kCntDiffShade = 20,
                        kCntDiffRes3 = 21, kCntCulledCam = 22, kCntSlots = 23 };
-constexpr int kWsCounterWords = 64 + 2 * 8 * 16;  // counters | fetch, zeroed together
+// counters | fetch: [2][8 parts x 16] queue-tracer fetch counters, then [8 parts x 16] the shade
+// kernel's batch claims (k_pt_shade0), all zeroed together
+constexpr int kWsCounterWords = 64 + 3 * 8 * 16;
 constexpr uint32_t kChainMaxQ3 = 1u << 20;  // serial frames fuse the bounce chain below this queue-3 length
 
 struct PtWorkspace {
@@ -103,6 +105,9 @@ struct PtWorkspace {
     uint32_t* fetch;            // [2][8 parts x 16]: k_trace_queue fetch counters, 64 B apart
     uint32_t cap;               // entries per queue (= rows * W * spp)
     uint32_t persistBlocks;     // grid of the persistent queue kernels
+    int shadeClaim = 0;         // k_pt_shade0 claims its batches dynamically (synchronous frames)
+    uint32_t shadeBlocksPerCu = 0;  // ... on this grid per CU (0: its residency); cus: the device's CUs
+    uint32_t cus = 256;
     uint32_t traceBlocks;       // grid of the queue tracer of queue 3 (k_trace_queue)
     uint32_t trace3ShortBlocks = 0;  // its workgroups that run when queue 3 is short (0: all)
     uint32_t trace4Blocks;      // ... of queue 4 (a short queue: a few percent of queue 3)

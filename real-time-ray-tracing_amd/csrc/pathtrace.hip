@@ -601,6 +601,56 @@ __global__ __launch_bounds__(256, kOneRound ? 6 : 4) void k_pt_camera(PathTraceP
     add_rays(P, wgRays, rays);
 }
 
+// Batches of k_pt_shade0.  Synchronous frames (PtWorkspace::shadeClaim) claim them dynamically:
+// the batches are cut into kParts contiguous parts, one counter each (64 B apart, in the
+// workspace's fetch block); a workgroup claims from its home part (blockIdx % kParts) and moves
+// on to the next part once that is drained, thread 0 publishing the batch through LDS.  A batch's
+// time is a chain of dependent loads that varies with its pixels, and the static split (batch b,
+// then b + grid) left the last round to a fraction of the workgroups: serial shade 197 -> 184 us.
+// Pipelined frames keep the static split over the larger grid: there the shade runs beside the
+// previous frame's tracers, and workgroups that stay resident until the list is drained measured
+// 0.79 -> 0.82 ms per frame.  Block-uniform calls, each ending with a barrier.
+struct ShadeClaim {
+    uint32_t batches, partLen, drained, next;
+    int home;
+    bool dyn;
+};
+RT_DEV void claim_init(ShadeClaim& c, uint32_t batches, bool dyn) {
+    c.batches = batches;
+    c.partLen = (batches + kParts - 1) / kParts;
+    c.drained = batches == 0u ? (1u << kParts) - 1u : 0u;
+    c.home = (int)(blockIdx.x % kParts);
+    c.dyn = dyn;
+    c.next = blockIdx.x;
+}
+// the next batch index, or >= batches when every part is drained
+RT_DEV uint32_t claim_next(ShadeClaim& c, uint32_t* counters, uint32_t& slot) {
+    if (!c.dyn) {
+        const uint32_t b = c.next;
+        c.next += gridDim.x;
+        return b;
+    }
+    __syncthreads();  // the previous batch's readers of `slot` are done
+    if (threadIdx.x == 0) {
+        uint32_t b = c.batches;
+        while (c.drained != (1u << kParts) - 1u) {
+            int part = c.home;
+            while (c.drained & (1u << part)) part = (part + 1) % kParts;
+            const uint32_t got = atomicAdd(&counters[part * 16], 1u);
+            const uint32_t lo = (uint32_t)part * c.partLen;
+            const uint32_t len = lo >= c.batches ? 0u : (c.batches - lo < c.partLen ? c.batches - lo : c.partLen);
+            if (got < len) {
+                b = lo + got;
+                break;
+            }
+            c.drained |= 1u << part;
+        }
+        slot = b;
+    }
+    __syncthreads();
+    return slot;
+}
+
 // Steps 0 (hit from k_pt_camera) .. 3 of every sample of the surface pixels.  kGlossy: the
 // material table holds mirror/glass, so steps 1 and 2 may trace (inline, LDS stack).
 //
@@ -625,6 +675,7 @@ __global__ __launch_bounds__(256, (kGlossy || !kOneRound) ? 2 : 3) void k_pt_sha
     __shared__ unsigned long long wgRays[4];
     __shared__ __align__(16) float sSkyTree[kSkyTreeNodes];
     __shared__ __align__(16) float sSunTree[kSunTreeNodes];
+    __shared__ uint32_t wgBatch;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wS = __builtin_amdgcn_readfirstlane(w);  // for add_rays: threadIdx.x need not live to the end
     bn_stage_sobol(P.bluenoise, sob, tid, 256);
@@ -637,8 +688,10 @@ __global__ __launch_bounds__(256, (kGlossy || !kOneRound) ? 2 : 3) void k_pt_sha
     const SceneView sc = scene_of(P);
     const size_t plane = (size_t)P.rows * P.width;
     uint32_t raysWg = 0, shV = 0, shT = 0, shD = 0;
+    ShadeClaim claim;  // batches of perWg surface pixels (claim_next)
+    claim_init(claim, (n + perWg - 1) / perWg, P.ws.shadeClaim != 0);
 #pragma unroll 1
-    for (uint32_t base = blockIdx.x * perWg; base < n; base += gridDim.x * perWg) {  // block-uniform
+    for (uint32_t base; (base = claim_next(claim, P.ws.fetch + 2 * kParts * 16, wgBatch) * perWg) < n;) {
         const uint32_t i = base + (uint32_t)g * 64u + (uint32_t)lane;
         const bool active = i < n;
         const uint32_t pl = active ? P.ws.surface[i] : 0u;
@@ -910,7 +963,10 @@ RT_DEV bool chain_step(const SceneView& sc, const TravRay& r, TravState& s, Trav
     return trav_step<16, false>(sc, r, s, rec, stk, 256, nullptr);  // no carried record: 168 VGPRs, no scratch
 }
 
-__global__ __launch_bounds__(256, 3) void k_pt_chain(PathTraceParams P) {
+#ifndef RTX_CHAIN_WAVES
+#define RTX_CHAIN_WAVES 3
+#endif
+__global__ __launch_bounds__(256, RTX_CHAIN_WAVES) void k_pt_chain(PathTraceParams P) {
     __shared__ uint2 stk[17 * 256];  // 16 entries + trav_step's dead slot
     __shared__ uint32_t sob[256];
     __shared__ uint2 ranges[4][kChainRanges];
@@ -1138,12 +1194,34 @@ extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t
 // hook (optional): called on the host right after each kernel is enqueued; the frame pipeline
 // issues the previous frame's denoise and gates the next frame's camera rays there (frame.cpp).
 namespace {
+// the shade kernel's grid: with dynamic claims ws.shadeBlocksPerCu, or its residency (queried
+// once per variant); the static split keeps persistBlocks
+template <typename K>
+dim3 shade_grid(const PathTraceParams* p, K kernel, int& cached) {
+    if (cached == 0) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 256, 0) != hipSuccess || b < 1) b = 2;
+        cached = b;
+    }
+    if (!p->ws.shadeClaim) return dim3(p->ws.persistBlocks);  // the static split's grid
+    const uint32_t perCu = p->ws.shadeBlocksPerCu ? p->ws.shadeBlocksPerCu : (uint32_t)cached;
+    return dim3(perCu * (p->ws.cus ? p->ws.cus : 256u));
+}
+
 template <bool kOneRound>
 void launch_shade_rounds(const PathTraceParams* p, hipStream_t stream) {
-    const dim3 pg(p->ws.persistBlocks), pb(256);
-    if (p->ws.glossy) hipLaunchKernelGGL((k_pt_shade0<true, false, kOneRound>), pg, pb, 0, stream, *p);
-    else if (p->ws.microfacet) hipLaunchKernelGGL((k_pt_shade0<false, true, kOneRound>), pg, pb, 0, stream, *p);
-    else hipLaunchKernelGGL((k_pt_shade0<false, false, kOneRound>), pg, pb, 0, stream, *p);
+    static int occ[3];
+    const dim3 pb(256);
+    if (p->ws.glossy) {
+        auto k = k_pt_shade0<true, false, kOneRound>;
+        hipLaunchKernelGGL(k, shade_grid(p, k, occ[0]), pb, 0, stream, *p);
+    } else if (p->ws.microfacet) {
+        auto k = k_pt_shade0<false, true, kOneRound>;
+        hipLaunchKernelGGL(k, shade_grid(p, k, occ[1]), pb, 0, stream, *p);
+    } else {
+        auto k = k_pt_shade0<false, false, kOneRound>;
+        hipLaunchKernelGGL(k, shade_grid(p, k, occ[2]), pb, 0, stream, *p);
+    }
 }
 
 void launch_shade(const PathTraceParams* p, hipStream_t stream) {

@@ -163,57 +163,3 @@ def test_parity_metric_vs_libm_oracle(rtx, oracle, tmp_path, default_scene, vari
             json.dump(report, fh, indent=1)
     assert rel_raw <= 1e-3 and rel_hdr <= 1e-3
     assert diverged < 1e-3
-
-
-def _hdr(a):
-    return a[:, :3].astype(np.uint16).view(np.float16).astype(np.float64)
-
-
-def test_parity_metric_vs_libm_oracle(rtx, oracle, tmp_path, default_scene):
-    """SURVEY.md §8d parity metric against an evaluation that shares no transcendental code with
-    the product (the oracle built on glibc's sinf/expf/powf/atan2f/...): relative L2 <= 1e-3 of
-    the raw PathTrace colour x albedo and of the final pre-tone-map HDR, plus the fraction of
-    pixels whose path decisions diverged (ray count differs, or the raw colour moved by more than
-    1 % of its magnitude).  The numbers go to $RTX_REPORT_DIR/parity_metric.json when set."""
-    w, h, spp, frames = 1920, 1080, 4, 2
-    raw = {}
-    # get_buffer(RENDER_COLOR) right after the path trace returns the G-buffer colour only while
-    # the denoise of the frame is still pending; read it from a serial context instead
-    cfg = rtx.write_config(str(tmp_path / "raw.toml"), w, h, spp=spp)
-    rt = rtx.RayTracer(w, h, cfg).init()
-    rt.set_delta_time(DT)
-    for f in range(1, frames + 1):
-        rt.build_bvh()
-        rt.path_trace(f, detail=f == frames)
-        rt.sync()
-        if f == frames:
-            raw["color"] = rt.get_buffer("RENDER_COLOR", (w * h, 4), np.uint16).copy()
-            raw["albedo"] = rt.get_buffer("ALBEDO", (w * h, 4), np.uint16).copy()
-            raw["rays"] = rt.download("RAYS", np.uint32).copy()
-        rt.denoise_post(f)
-    rt.sync()
-    final = rt.get_buffer("RENDER_COLOR", (w * h, 4), np.uint16).copy()
-    rt.cleanup()
-    got = pipeline_frames(rtx, tmp_path, w, h, spp, frames)
-    assert np.array_equal(got["color"], final)  # the pipelined path ends on the same frame
-
-    with oracle.libm():
-        o, g = oracle_frames(oracle, default_scene, w, h, spp, frames)
-    ref_raw = _hdr(g["color"]) * _hdr(g["albedo"])
-    gpu_raw = _hdr(raw["color"]) * _hdr(raw["albedo"])
-    rel_raw = float(np.linalg.norm(gpu_raw - ref_raw) / np.linalg.norm(ref_raw))
-    rel_hdr = float(np.linalg.norm(_hdr(final) - _hdr(o["color"])) / np.linalg.norm(_hdr(o["color"])))
-    moved = np.abs(gpu_raw - ref_raw).max(1) > 1e-2 * np.maximum(np.abs(ref_raw).max(1), 1e-3)
-    diverged = float((moved | (raw["rays"] != g["rays"])).mean())
-    rgba_equal = float((got["rgba"] == o["rgba"]).all(1).mean())
-    report = dict(config="1920x1080 4 spp, frame %d of a default-camera sequence" % frames,
-                  reference="oracle/_build/liboracle_libm.so (host glibc transcendentals)",
-                  rel_l2_raw_color_x_albedo=rel_raw, rel_l2_final_hdr=rel_hdr, diverged_pixel_fraction=diverged,
-                  rgba8_identical_fraction=rgba_equal, bar=1e-3)
-    print(json.dumps(report))
-    if os.environ.get("RTX_REPORT_DIR"):
-        os.makedirs(os.environ["RTX_REPORT_DIR"], exist_ok=True)
-        with open(os.path.join(os.environ["RTX_REPORT_DIR"], "parity_metric.json"), "w") as fh:
-            json.dump(report, fh, indent=1)
-    assert rel_raw <= 1e-3 and rel_hdr <= 1e-3
-    assert diverged < 1e-3

@@ -191,3 +191,51 @@ def test_chain_choice_refreshes_without_sync(rtx, tmp_path):
     assert chains[-1] == 0, chains  # the long queue-3 length arrived without an rt_sync
     rt.sync()
     rt.cleanup()
+
+
+# frames whose denoise skips the active-tile lists: SpatialFilter7x7 off (4, 8) or the a-trous
+# passes off (6); the others after frame 1 run the list chain, which alternates the two
+# accumulation buffers (accum / accumAlt, swapped by the host) and the list counters' parity
+NO_LOCAL, NO_WIDE = (4, 8), (6,)
+
+
+def test_pipelined_list_toggles_match_serial_and_oracle(rtx, oracle, tmp_path, default_scene):
+    """Round-5 verdict item 8: every buffer the post stream shares across frames — the G-buffer
+    sets, the two accumulation buffers the host swaps after a list frame, the list counters of
+    both parities, the single colour ping-pong partner, the exposure state and the RGBA8 output —
+    reused under pipelining while the denoise alternates between list and non-list frames.  The
+    drop-in path (rt_draw_device, asynchronous, one device target per frame) against synchronous
+    draws of the same sequence, frame by frame, and each synchronous frame against the oracle."""
+    import torch
+
+    w, h, spp, frames = 192, 112, 2, 12
+    s, tex = oracle.sky(), oracle.textures()
+    cam = oracle.default_camera(w, h)
+    images = {}
+    for asynchronous in (False, True):
+        cfg = rtx.write_config(str(tmp_path / ("lt%d.toml" % asynchronous)), w, h, spp=spp)
+        rt = rtx.RayTracer(w, h, cfg).init()
+        rt.set_delta_time(16.667)
+        targets = [torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda:0") for _ in range(frames)]
+        torch.cuda.synchronize()
+        for f in range(1, frames + 1):
+            p = rt.params
+            p.pass_.enableLocalSpatialFilter = 0 if f in NO_LOCAL else 1
+            p.pass_.enableWideSpatialFilter = 0 if f in NO_WIDE else 1
+            rt.params = p
+            rt.draw_device(targets[f - 1].data_ptr(), 0, asynchronous=asynchronous)
+        rt.sync()
+        images[asynchronous] = [t.cpu().numpy().reshape(-1, 4) for t in targets]
+        images[asynchronous].append(rt.get_buffer("ACCUMULATION").copy())
+        images[asynchronous].append(rt.get_buffer("HISTORY_COLOR").copy())
+        rt.cleanup()
+    for f, (a, b) in enumerate(zip(images[False], images[True]), start=1):
+        assert np.array_equal(a, b), "frame %d" % f if f <= frames else ("ACCUMULATION", "HISTORY_COLOR")[f - frames - 1]
+    dn = oracle.Denoiser(w, h)
+    for f in range(1, frames + 1):
+        op = oracle.default_params()
+        op.enableLocalSpatialFilter = 0 if f in NO_LOCAL else 1
+        op.enableWideSpatialFilter = 0 if f in NO_WIDE else 1
+        g = oracle.pathtrace(default_scene["bvh"], w, h, frame_num=f, spp=spp, cam=cam, sky_out=s, tex=tex)
+        o = dn.draw(g, f, params=op, delta_time=16.667)
+        assert np.array_equal(images[False][f - 1], o["rgba"]), f

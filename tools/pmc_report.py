@@ -1,14 +1,23 @@
 #!/usr/bin/env python3
 """Per-kernel summary of separate rocprofv3 --pmc passes (tools/prof.sh).
 
-    python tools/pmc_report.py <out.json> <pass_dir>... [--key KEY] [--workload TEXT]
+    python tools/pmc_report.py <out.json> <pass_dir>... [--key KEY] [--workload TEXT] [--calib FILE]
+    python tools/pmc_report.py --make-calib <calib.json> <fetch_pass_dir> <write_pass_dir>
+
+--make-calib reads the FETCH_SIZE and WRITE_SIZE passes of tools/probe/fetch_calib.bin (streaming
+copies of 4, 8 and 16 bytes per lane and a 16x16-tiled 8-byte half4 copy, each of a known byte
+count) and writes, per access width, the factor that turns FETCH_SIZE x 1024 into the bytes read.
+--calib applies those factors: the denoise / post kernels (8-byte half4 texel reads) take the
+8-byte factor, every other kernel the 16-byte one (MI355X_MICROARCH.md: 2, FETCH_SIZE counts half
+the bytes of 16-byte-per-lane reads).  Without --calib every kernel takes 2.
 
 Kernels are named by their symbol with boolean template arguments dropped and integer ones kept
 (k_spatial5<3, false> -> k_spatial5<3>, k_temporal<true> -> k_temporal; k_scale_post<576> ->
 k_scale_post); k_build_bvh<threads> is labelled by its workgroup count (k_build_bvh@61wg, @938wg).  Per kernel the median per-dispatch value of every
 counter is taken, then (MI355X_MICROARCH.md HBM, L2 and SQ sections):
-  hbm_bytes          = (2 * FETCH_SIZE + WRITE_SIZE) * 1024   (FETCH_SIZE, KB, counts half the bytes
-                       of wide reads on gfx950, so it is doubled; WRITE_SIZE in KB)
+  hbm_bytes          = (f * FETCH_SIZE + WRITE_SIZE) * 1024   (FETCH_SIZE, KB, counts half the bytes
+                       of wide reads on gfx950: f = 2, or the calibrated factor of the kernel's
+                       access width, --calib; WRITE_SIZE in KB)
   l2_hit_rate        = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
   valu_busy_frac     = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES
   wait_inst_any_frac = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES   (issue stalls)
@@ -41,8 +50,58 @@ def short(name, grid, wg):
     return n
 
 
+# kernels whose reads are 8-byte half4 texels (the denoiser and the post chain)
+HALF4_KERNELS = set(DENOISE) | {"k_spatial7_list", "k_spatial5_list<3>", "k_spatial5_list<6>", "k_tile_noise",
+                                "k_noise16", "k_downscale4", "k_histogram", "k_bloom_gauss", "k_bloom_apply",
+                                "k_lens_flare", "k_hdr_out"}
+# tools/probe/fetch_calib.hip: bytes each way per dispatch
+CALIB_BYTES = {"copy_k<unsigned int>": (4, 512 << 20), "copy_k<HIP_vector_type<unsigned int, 2u> >": (8, 512 << 20),
+               "copy_k<HIP_vector_type<unsigned int, 4u> >": (16, 512 << 20), "tile8_k": ("tile8", 1920 * 1080 * 8)}
+
+
+def counters_per_kernel(d, counter):
+    out = collections.defaultdict(list)
+    for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+        per = collections.defaultdict(float)
+        names = {}
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            per[r["Dispatch_Id"]] += float(r["Counter_Value"])
+            names[r["Dispatch_Id"]] = r["Kernel_Name"].replace("void ", "").split("(")[0]
+        for did, v in per.items():
+            out[names[did]].append(v)
+    return out
+
+
+def make_calib(out_path, fetch_dir, write_dir):
+    fetch, write = counters_per_kernel(fetch_dir, "FETCH_SIZE"), counters_per_kernel(write_dir, "WRITE_SIZE")
+    res = {"source": "tools/probe/fetch_calib.bin: FETCH_SIZE and WRITE_SIZE passes (rocprofv3 --pmc, one each)",
+           "widths": {}}
+    for name, (width, nbytes) in CALIB_BYTES.items():
+        if name not in fetch or name not in write:
+            continue
+        fk, wk = statistics.median(fetch[name]), statistics.median(write[name])
+        res["widths"][str(width)] = {"kernel": name, "bytes_each_way": nbytes, "dispatches": len(fetch[name]),
+                                     "fetch_size_kb": fk, "write_size_kb": wk,
+                                     "fetch_factor": round(nbytes / (fk * 1024.0), 4),
+                                     "write_factor": round(nbytes / (wk * 1024.0), 4)}
+    with open(out_path, "w") as f:
+        json.dump(res, f, indent=1)
+    for w, e in res["widths"].items():
+        print("%-6s fetch x%.3f write x%.3f  (%s)" % (w, e["fetch_factor"], e["write_factor"], e["kernel"]))
+
+
 def main():
     args = sys.argv[1:]
+    if args and args[0] == "--make-calib":
+        make_calib(*args[1:4])
+        return
+    calib = None
+    if "--calib" in args:
+        i = args.index("--calib")
+        calib = json.load(open(args[i + 1]))["widths"]
+        del args[i:i + 2]
     key = workload = None
     if "--key" in args:
         i = args.index("--key")
@@ -72,8 +131,12 @@ def main():
         c = {n: statistics.median(v) for n, v in cv.items()}
         e = {"dispatches": max(len(v) for v in cv.values()), "us": round(statistics.median(dur[k]), 2)}
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            e["hbm_bytes"] = int(round((2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024))
-            e["fetch_bytes_doubled"] = int(round(2.0 * c["FETCH_SIZE"] * 1024))
+            fac = 2.0
+            if calib:
+                fac = calib["8" if k in HALF4_KERNELS else "16"]["fetch_factor"]
+            e["fetch_factor"] = fac
+            e["hbm_bytes"] = int(round((fac * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024))
+            e["fetch_bytes"] = int(round(fac * c["FETCH_SIZE"] * 1024))
             e["write_bytes"] = int(round(c["WRITE_SIZE"] * 1024))
         hit, miss = c.get("TCC_HIT_sum"), c.get("TCC_MISS_sum")
         if hit is not None and miss is not None and hit + miss > 0:
@@ -94,7 +157,9 @@ def main():
     res = {"workload_key": key, "workload": workload, "passes": dirs, "kernels": kernels,
            "stage_hbm_bytes": sum(kernels[k].get("hbm_bytes", 0) for k in STAGE if k in kernels) or None,
            "denoise_hbm_bytes": sum(kernels[k].get("hbm_bytes", 0) for k in DENOISE if k in kernels) or None,
-           "correction": "FETCH_SIZE doubled (gfx950 counts half the bytes of wide reads), KB x 1024",
+           "correction": ("FETCH_SIZE x the calibrated factor of the kernel's access width (--calib: 8-byte half4 "
+                          "reads for the denoise / post kernels, 16-byte otherwise), KB x 1024" if calib else
+                          "FETCH_SIZE doubled (gfx950 counts half the bytes of wide reads), KB x 1024"),
            "note": "every counter group from its own rocprofv3 --pmc run; medians over all dispatches of the kernel"}
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1)

@@ -42,7 +42,8 @@ typedef struct rt_context rt_context;
  * the reference's [resolution] / [file] / [optimziation] tables; extensions: [scene]
  * chunkDim (VoxelsGenerator::kChunkDim, terrain.h:42), [render] spp, [render] device.
  * [tuning] (scheduling A/B aids; the defaults are the measured best): arena (bool),
- * streams ("cumask" | "prio"), tracePerCu / trace4PerCu (0: automatic), chain ("serial" | "off" |
+ * streams ("cumask" | "prio"), tracePerCu / trace4PerCu (0: automatic), trace3ShortPerCu (a short queue
+ * 3's workgroups per CU on one GPU; 0: all of them), chain ("serial" | "off" |
  * "always"), shadeOnSide (bool), shadeBlocksPerCu (synchronous frames; 0: the kernel's residency),
  * overlapAfter / cameraAfter (-1: automatic).  [debug] (fault
  * injection, tests): bvhSkipPublish, bvhSkipPublishBuilds, bvhWaitMs.  The library reads no

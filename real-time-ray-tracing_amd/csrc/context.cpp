@@ -331,6 +331,7 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
         t.prioStreams = rttoml::find_or_string(doc, "tuning", "streams", "cumask") == "prio";
         t.tracePerCu = rttoml::find_or_int(doc, "tuning", "tracePerCu", 0);
         t.trace4PerCu = rttoml::find_or_int(doc, "tuning", "trace4PerCu", 0);
+        t.trace3ShortPerCu = rttoml::find_or_int(doc, "tuning", "trace3ShortPerCu", 2);
         const std::string chain = rttoml::find_or_string(doc, "tuning", "chain", "serial");
         t.chain = chain == "off" ? 0 : chain == "always" ? 2 : 1;
         t.shadeOnSide = rttoml::find_or_bool(doc, "tuning", "shadeOnSide", true);

@@ -101,6 +101,11 @@ struct FrameResources {
     uint32_t* camSurface[kGbSets] = {};
     uint32_t* camCount[kGbSets] = {};  // counter block per slot (PtWorkspace::counters)
     uint32_t* lastCounters = nullptr;  // the block of the last path trace (RT_ARR_PT_QUEUE)
+    // serial frames: two counter blocks in turn, syncCount[0] = camCount[0]; the resolve of a frame
+    // zeroes the other one (syncZeroed), so the next frame's camera kernel needs no memset
+    uint32_t* syncCount[2] = {};
+    int syncIdx = 0;
+    bool syncZeroed[2] = {};
     bool camInFlight[kGbSets] = {};
     // ... and the bounce queues with their hit records, one slot per set when the shade kernel
     // runs on the side stream (shadeOnSide: frame f+1's shade appends to its queues while frame
@@ -124,6 +129,7 @@ struct FrameResources {
     uint2* colorB = nullptr;       // ping-pong partner of color
     uint2* accum = nullptr;        // AccumulationColorBuffer (the latest)
     uint2* accumAlt = nullptr;     // the list chain writes this one and swaps (null: in place only)
+    bool accumBound = false;       // accum is the caller's (rt_bind_buffer): the list chain copies back
     uint2* histBuf[2] = {};        // HistoryColorBuffer pair: histBuf[histIdx] is the latest, TemporalFilter2
     int histIdx = 0;               // writes the other one, then they swap roles
     uint16_t* histDepth = nullptr; // HistoryDepthBuffer
@@ -199,7 +205,7 @@ struct rt_context {
     struct Tuning {
         bool arena = true;
         bool prioStreams = false;
-        int tracePerCu = 0, trace4PerCu = 0;
+        int tracePerCu = 0, trace4PerCu = 0, trace3ShortPerCu = 2;
         int chain = 1;
         bool shadeOnSide = true;
         int shadeBlocksPerCu = 0;  // k_pt_shade0's grid per CU (0: its residency)

@@ -1612,9 +1612,10 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
     // noise-gated passes over active-tile lists (above); rcp: the depth weights' divisor of pass k
     // as a reciprocal (DenoisePostParams::rcpDepthOk)
     // TemporalFilter reads the previous frame's accumulation buffer at reprojected positions while
-    // it also writes tiles of this frame's, so the list chain writes the other buffer of a pair
-    // (accumAlt; the host swaps them) — not with a caller-bound buffer, nor a strip-local denoise
-    const bool useList = P->tileList && P->accumAlt && !P->stripLocal && P->temporal && P->frameNum != 1 &&
+    // it also writes tiles of this frame's, so the list chain writes another buffer (accumAlt): the
+    // host swaps the two, or, when the accumulation buffer is the caller's (a strip-local denoise
+    // exchanges it), copies the rows this chain finished back into it (frame.cpp run_denoise)
+    const bool useList = P->tileList && P->accumAlt && P->temporal && P->frameNum != 1 &&
                          P->localSpatial && P->wideSpatial && !P->visualize;
     uint2* const accOut = useList ? P->accumAlt : P->accum;
     P->listUsed = useList ? 1 : 0;
@@ -1625,7 +1626,14 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
     const bool pk7 = kDnPk && sn7 > 0.0f && sn7 < __builtin_inff();
     const float snT = P->dn.temporal_denoise_sigma_normal;
     const bool pkT = kDnPk && snT > 0.0f && snT < __builtin_inff();
-    const dim3 gList((unsigned)(kListParts * (P->tileCap / kListParts + 1)));  // one workgroup per list slot
+    // one workgroup per list slot the frame can fill: the lists hold tiles of TemporalFilter's tile
+    // rows only (a strip-local rank's strip and halo), a contiguous run of tile indices, so a
+    // partition (tile % 16) holds at most a sixteenth of them
+    int lt0, lt1;
+    tile_range(P, 4, lt0, lt1);
+    const uint32_t listRows = (uint32_t)(lt1 > lt0 ? ((lt1 - lt0) * ((W + 15) / 16) + kListParts - 1) / kListParts : 0);
+    const uint32_t capRows = P->tileCap / kListParts + 1;
+    const dim3 gList((unsigned)(kListParts * (listRows < capRows ? listRows : capRows)));
     bool noise1 = false, histDepthDone = false;
     if (P->temporal && P->frameNum != 1) {
         noise1 = P->localSpatial && !P->visualize;

@@ -240,7 +240,17 @@ int run_denoise(rt_context* ctx, DenoisePostParams& p, hipStream_t s) {
     HIP_TRY(ctx, rtk_denoise_phase(&p, s, 0));
     if (p.listUsed) {  // the list chain wrote the other accumulation buffer; the next list frame
         ctx->fr.tileParity ^= 1;  // appends under the other counters
-        std::swap(ctx->fr.accum, ctx->fr.accumAlt);
+        if (ctx->fr.accumBound || p.stripLocal) {
+            // the caller's buffer (a strip-local rank exchanges its rows of it) gets the rows this
+            // chain finished — a strip-local rank's own rows, which the rows exchange gathers; the
+            // halo rows the later passes read come from accumAlt (their `alt`) — once TemporalFilter,
+            // the last reader of the previous frame's accumulation, is done
+            const size_t r0 = p.stripLocal ? p.rowA : 0, r1 = p.stripLocal ? p.rowB : p.H;
+            HIP_TRY(ctx, hipMemcpyAsync(p.accum + r0 * p.W, p.accumAlt + r0 * p.W, (r1 - r0) * p.W * 8,
+                                        hipMemcpyDeviceToDevice, s));
+        } else {
+            std::swap(ctx->fr.accum, ctx->fr.accumAlt);
+        }
     }
     // the histogram is recomputed only with the post chain on; summing a stale one again would
     // multiply it by the rank count every frame
@@ -450,6 +460,8 @@ int rt_frame_init(rt_context* ctx) {
         ALLOC(ws.pending, (size_t)ctx->renderW * ctx->stripRows * 4);
         ALLOC(ws.surface, (size_t)ctx->renderW * ctx->stripRows * 4);
         ALLOC(fr.camCount[0], kWsCounterWords * 4);
+        ALLOC(fr.syncCount[1], kWsCounterWords * 4);
+        fr.syncCount[0] = fr.camCount[0];
         fr.camQ3[0] = ws.q3;
         fr.camQ4[0] = ws.q4;
         fr.camHitRec[0] = ws.hitRec;
@@ -483,7 +495,7 @@ int rt_frame_init(rt_context* ctx) {
         // 2 workgroups per CU, which leaves the next frame's camera waves more room (1.091 -> 1.081
         // ms/frame, four repeats); a long one (the terrain view) keeps all of them (2 per CU there:
         // 4.14 -> 4.44 ms); strip ranks keep 3 (at 2 ranks 0.710 vs 0.727 ms, equal at 4 and 8)
-        ws.trace3ShortBlocks = ctx->stripCount == 1 ? (uint32_t)(cus * 2) : 0u;
+        ws.trace3ShortBlocks = ctx->stripCount == 1 && tn.trace3ShortPerCu > 0 ? (uint32_t)(cus * tn.trace3ShortPerCu) : 0u;
         ws.chain = (uint32_t)tn.chain;  // [tuning] chain = "off" | "serial" | "always" (default serial)
         ws.trace4Blocks = (uint32_t)(cus * trace4PerCu);
     }
@@ -653,6 +665,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.strip = (uint32_t)ctx->stripIndex;
     p.frameNum = frame_num;
     p.spp = (uint32_t)ctx->spp;
+    p.invSpp = (ctx->spp & (ctx->spp - 1)) == 0 ? 1.0f / (float)ctx->spp : 0.0f;  // exact for a power of two
     p.materialOverride = ctx->materialOverride;
     p.triCount = ctx->mesh.triCount;
     p.bluenoise = ctx->dBlueNoise;
@@ -687,6 +700,13 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.ws.hit0Err = fr.camHit0Err[g];
     p.ws.surface = fr.camSurface[g];
     p.ws.counters = fr.camCount[g];
+    if (!ctx->postStream) {  // serial frames: the counter block the previous frame's resolve zeroed
+        const int b = fr.syncIdx;
+        p.ws.counters = fr.syncCount[b];
+        p.ws.countersZeroed = fr.syncZeroed[b] ? 1 : 0;
+        p.ws.zeroNext = fr.syncCount[b ^ 1];
+        fr.syncZeroed[b] = fr.syncZeroed[b ^ 1] = false;  // until this frame's resolve is enqueued
+    }
     p.ws.fetch = p.ws.counters + 64;
     fr.lastCounters = p.ws.counters;
     const int qs = fr.camQ3[g].rayO ? g : 0;  // bounce-queue slot: per set when allocated (shadeOnSide)
@@ -771,6 +791,10 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     // pending only once the launches that store it are enqueued: a failed launch leaves the next
     // serial frame to ask again instead of freezing the chain choice
     if (askQ3) fr.q3Pending = true;
+    if (!ctx->postStream) {  // the other block is zeroed by this frame's resolve, enqueued above
+        fr.syncIdx ^= 1;
+        fr.syncZeroed[fr.syncIdx] = true;
+    }
     if (ctx->postPending && (rc = issue_pending_post(ctx)) != RT_OK) return rc;
     if (ctx->postStream) {
         HIP_TRY(ctx, hipEventRecord(ctx->restDone[g], ctx->stream));
@@ -1143,6 +1167,7 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
     if (rc != RT_OK) return rc;
     FrameResources& fr = ctx->fr;
     for (int k = 0; k < kGbSets; ++k) fr.setInFlight[k] = false;
+    fr.syncZeroed[0] = fr.syncZeroed[1] = false;  // pipelined frames use (and dirty) camCount[0] too
     if (!stream) {
         ctx->postStream = nullptr;
         return RT_OK;
@@ -1221,9 +1246,9 @@ int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
                           : name == RT_BUF_HISTOGRAM ? (void**)&fr.histogram : (void**)&fr.rgba;
             HIP_TRY(ctx, hipMemcpy(device_ptr, *slot, need, hipMemcpyDeviceToDevice));
             if (name == RT_BUF_RGBA8 && fr.outRgba == fr.rgba) fr.outRgba = (uint32_t*)device_ptr;
-            // a caller-owned accumulation buffer stays the one the filters write in place: the
-            // list chain, which alternates two, is off from here on
-            if (name == RT_BUF_ACCUMULATION) fr.accumAlt = nullptr;
+            // a caller-owned accumulation buffer stays the accumulation buffer: the list chain
+            // writes the internal one and copies its rows back instead of swapping the two
+            if (name == RT_BUF_ACCUMULATION) fr.accumBound = true;
             *slot = device_ptr;
             return RT_OK;
         }
@@ -1423,6 +1448,7 @@ int rt_trace_rays(rt_context* ctx, const float* rays, uint32_t n, float* hits, u
     if (int rc = sync_streams(ctx)) return rc;  // the queue buffers are shared with in-flight frames
     HIP_TRY(ctx, hipMemcpyAsync(fr.ws.q3.rayO, o.data(), (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(fr.ws.q3.rayD, d.data(), (size_t)n * 16, hipMemcpyHostToDevice, ctx->stream));
+    fr.syncZeroed[0] = false;  // fr.ws.counters is syncCount[0]
     HIP_TRY(ctx, hipMemsetAsync(fr.ws.counters, 0, kWsCounterWords * sizeof(uint32_t), ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(fr.ws.counters + kCntQ3, &n, 4, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipEventRecord(ctx->ev0, ctx->stream));

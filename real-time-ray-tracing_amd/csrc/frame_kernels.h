@@ -117,6 +117,10 @@ struct PtWorkspace {
     uint32_t* itersOut = nullptr;  // optional [cap]: traversal iterations per queue entry (rt_trace_rays)
     unsigned long long* q3HostOut = nullptr;  // optional, pinned host memory: {queue 3's length, q3Tag},
     uint32_t q3Tag = 0;                       // stored by k_pt_resolve in one 64-bit store
+    // serial frames alternate two counter blocks: k_pt_resolve zeroes the other one (zeroNext) for
+    // the next frame, whose camera kernel then starts without a memset (countersZeroed)
+    uint32_t* zeroNext = nullptr;
+    int countersZeroed = 0;
 };
 
 // The frame's traced-ray count is kept as partial sums in kRayCounterSlots slots 128 B apart
@@ -136,6 +140,7 @@ struct PathTraceParams {
     uint32_t nStrips, strip;
     int frameNum;
     uint32_t spp;               // samples per pixel (>= 1), frame index spp*(frameNum-1)+1+s
+    float invSpp;               // 1 / spp when spp is a power of two (exact), else 0 (div_spp)
     int materialOverride;       // < 0: reference material table (material 3 everywhere)
     uint32_t triCount;
     const uint8_t* bluenoise;

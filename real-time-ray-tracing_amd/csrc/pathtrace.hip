@@ -360,6 +360,10 @@ RT_DEV uint2 pack_h4(float a, float b, float c, uint32_t d16) {
     return make_uint2((uint32_t)rt_f2h(a) | ((uint32_t)rt_f2h(b) << 16), (uint32_t)rt_f2h(c) | (d16 << 16));
 }
 
+// v / spp: the product with 1 / spp when spp is a power of two (P.invSpp, set by the host), which is
+// the same real number and so the same correctly rounded result; the division otherwise
+RT_DEV F3 div_spp(const PathTraceParams& P, F3 v) { return P.invSpp != 0.0f ? v * P.invSpp : v / (float)P.spp; }
+
 // wave sum of a per-lane count into a counter: one atomic per wave (every lane of the wave calls)
 RT_DEV void wave_add(uint32_t v, uint32_t* dst) {
 #pragma unroll
@@ -399,11 +403,18 @@ RT_DEV SceneView scene_of(const PathTraceParams& P) { return scene_view(P.nodes,
 // workgroup sum of traced rays into the frame counter (one atomic per workgroup)
 // w: the calling wave's index in the workgroup (wave-uniform); the lane comes from v_mbcnt, so a
 // caller need not keep threadIdx.x live until its end
+// kBits: every lane's count is 0 or 1 (the camera kernel's one round), so the wave's sum is a
+// popcount of a ballot; otherwise a 32-bit butterfly (a lane's count stays far below 2^26)
+template <bool kBits = false>
 RT_DEV void add_rays(const PathTraceParams& P, unsigned long long* wgSlots, uint32_t rays, int w) {
     if (!P.rayCounter) return;
-    unsigned long long r = rays;
+    uint32_t r = rays;
+    if (kBits) {
+        r = (uint32_t)__popcll(__ballot(rays != 0u));
+    } else {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+        for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+    }
     const bool lane0 = __lane_id() == 0;
     if (lane0) wgSlots[w] = r;
     __syncthreads();
@@ -411,8 +422,9 @@ RT_DEV void add_rays(const PathTraceParams& P, unsigned long long* wgSlots, uint
     if (w == 0 && lane0)
         atomicAdd(&P.rayCounter[slot * kRayCounterStride], wgSlots[0] + wgSlots[1] + wgSlots[2] + wgSlots[3]);
 }
+template <bool kBits = false>
 RT_DEV void add_rays(const PathTraceParams& P, unsigned long long* wgSlots, uint32_t rays) {
-    add_rays(P, wgSlots, rays, __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6));
+    add_rays<kBits>(P, wgSlots, rays, __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6));
 }
 
 // per-sample init of PathTrace (pathtrace.cuh:20-60) and GenerateRay (raygen.cuh:7-38)
@@ -588,8 +600,8 @@ __global__ __launch_bounds__(256, kOneRound ? 6 : 4) void k_pt_camera(PathTraceP
             P.ws.surface[slot] = pl;
         } else {  // G-buffer of an all-sky pixel: sample 0 missed (matId 99999, miss normal/depth)
             if (P.spp > 1) {
-                L = L / (float)P.spp;
-                A = A / (float)P.spp;
+                L = div_spp(P, L);
+                A = div_spp(P, A);
             }
             P.colorOut[p] = pack_h4(L.x, L.y, L.z, 99999u & 0xFFFFu);
             P.normalOut[p] = pack_h4(0.0f, -1.0f, 0.0f, 0u);
@@ -598,7 +610,7 @@ __global__ __launch_bounds__(256, kOneRound ? 6 : 4) void k_pt_camera(PathTraceP
             P.motionOut[p] = (uint32_t)rt_f2h(0.5f) | ((uint32_t)rt_f2h(0.5f) << 16);
         }
     }
-    add_rays(P, wgRays, rays);
+    add_rays<kOneRound>(P, wgRays, rays);
 }
 
 // Batches of k_pt_shade0.  Synchronous frames (PtWorkspace::shadeClaim) claim them dynamically:
@@ -667,7 +679,10 @@ RT_DEV uint32_t claim_next(ShadeClaim& c, uint32_t* counters, uint32_t& slot) {
 // scratch: 3 waves per SIMD instead of 2 (229 VGPRs through the step loop; serial 0.212 ->
 // 0.190 ms, synchronous draw 1.089 -> 1.069 ms, profiles/r05_ab/shade0_straight/).
 template <bool kGlossy, bool kMF, bool kOneRound>
-__global__ __launch_bounds__(256, (kGlossy || !kOneRound) ? 2 : 3) void k_pt_shade0(PathTraceParams P) {
+#ifndef RTX_SHADE_WAVES  // A/B builds only (tools/abl_build.sh): waves per SIMD of the default-material variant
+#define RTX_SHADE_WAVES 3
+#endif
+__global__ __launch_bounds__(256, (kGlossy || !kOneRound) ? 2 : RTX_SHADE_WAVES) void k_pt_shade0(PathTraceParams P) {
     __shared__ uint2 stk[kGlossy ? 17 * 256 : 1];  // 16 entries + trav_step's dead slot
     __shared__ uint32_t sob[256];
     __shared__ float4 foldL[4][64];  // this round's samples: finished colour xyz, w = 1 when deferred
@@ -788,8 +803,8 @@ __global__ __launch_bounds__(256, (kGlossy || !kOneRound) ? 2 : 3) void k_pt_sha
                 L = L0s;
                 A = A0s;
             } else {
-                L = L / (float)P.spp;
-                A = A / (float)P.spp;
+                L = div_spp(P, L);
+                A = div_spp(P, A);
             }
             if (N0.x != N0.x || N0.y != N0.y || N0.z != N0.z) N0 = f3(0.0f);
             if (D0 != D0) D0 = 0.0f;
@@ -1149,6 +1164,8 @@ __global__ __launch_bounds__(256, RTX_CHAIN_WAVES) void k_pt_chain(PathTracePara
 // colour of the pixels with a deferred sample: the fp32 sample average in sample order
 __global__ __launch_bounds__(256) void k_pt_resolve(PathTraceParams P) {
     const uint32_t n = P.ws.counters[kCntPending];
+    if (P.ws.zeroNext && blockIdx.x == 0)  // the next serial frame's counter block (frame.cpp)
+        for (int i = (int)threadIdx.x; i < kWsCounterWords; i += 256) P.ws.zeroNext[i] = 0u;
     // serial frames: queue 3's length into pinned host memory for the next frame's chain choice
     // (frame.cpp), a vector store over the bus instead of a copy on the stream
     if (P.ws.q3HostOut && blockIdx.x == 0 && threadIdx.x == 0)
@@ -1166,7 +1183,7 @@ __global__ __launch_bounds__(256) void k_pt_resolve(PathTraceParams P) {
             L = f3(0.0f);
             if (sd > 0) L = f3(ls[sd - 1].x, ls[sd - 1].y, ls[sd - 1].z);  // prefix sum of samples < sd
             for (uint32_t s = sd; s < P.spp; ++s) L = L + f3(ls[s].x, ls[s].y, ls[s].z);
-            L = L / (float)P.spp;
+            L = div_spp(P, L);
         }
         const uint32_t p = row_of(P.y0, P.nStrips, P.strip, pl / P.width) * P.width + pl % P.width;
         const uint32_t mask = P.colorOut[p].y >> 16;
@@ -1179,7 +1196,8 @@ extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t
     if (p->spp < 1 || p->spp > 64 || p->ws.persistBlocks < 1) return hipErrorInvalidValue;
     if ((size_t)p->rows * p->width >= (1u << 26) || (size_t)p->rows * p->width * p->spp > p->ws.cap)
         return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
+    hipError_t e = p->ws.countersZeroed ? hipSuccess  // zeroed by the previous serial frame's resolve
+                                        : hipMemsetAsync(p->ws.counters, 0, kWsCounterWords * sizeof(uint32_t), stream);
     if (e == hipSuccess && marks && marks[0]) e = hipEventRecord(marks[0], stream);  // begin / end of kernel 0
     if (e != hipSuccess) return e;
     const int nSW = cam_sample_waves(p->spp);

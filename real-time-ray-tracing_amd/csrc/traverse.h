@@ -43,41 +43,31 @@ RT_DEV float Dn(float a) { return a * (1.0f - 1.1920928955078125e-07f); }
 RT_DEV float up_(float a) { return a > 0.0f ? Up(a) : Dn(a); }
 RT_DEV float dn_(float a) { return a > 0.0f ? Dn(a) : Up(a); }
 
+// CreateRayBoxIntersectionHelper (geometry.cuh:519-582) names the axes kx, ky, kz (kz the
+// dominant one, kx / ky swapped when dir[kz] < 0) and gives each of kx and ky the same formulas
+// of its own coordinates and the shared max_z, kz its origin coordinate, and swaps an axis's
+// near / far origins when dir is negative along it.  So per world axis a: the kz value when a is
+// kz, else the kx / ky formula on a's coordinates — which of kx and ky it is changes nothing.
+// Evaluated that way, the axis permutation costs one select per axis instead of select chains.
+RT_DEV void raybox_axis(float o, float d, float lower, float upper, float max_z, bool isZ, float& on, float& of) {
+    const float eps = 5.0f * 5.9604644775390625e-08f;
+    const float n = up_(o + Up(eps * Up(lower + max_z)));
+    const float f = dn_(o - Up(eps * Up(upper + max_z)));
+    const bool neg = d < 0.0f;
+    on = isZ ? o : (neg ? f : n);
+    of = isZ ? o : (neg ? n : f);
+}
+
 RT_DEV RayBox make_raybox(F3 org, F3 dir, const Box& scene, F3 inv) {
     const int kz = max_dim(abs3(dir));
-    int kx = kz + 1; if (kx == 3) kx = 0;
-    int ky = kx + 1; if (ky == 3) ky = 0;
-    if (comp(dir, kz) < 0.0f) { const int t = kx; kx = ky; ky = t; }
-    const float eps = 5.0f * 5.9604644775390625e-08f;
     const F3 lo = abs3(org - scene.mn), hi = abs3(org - scene.mx);
     const F3 lower = f3(Dn(lo.x), Dn(lo.y), Dn(lo.z));
     const F3 upper = f3(Up(hi.x), Up(hi.y), Up(hi.z));
     const float max_z = fmx(comp(lower, kz), comp(upper, kz));
-    const float err_near_x = Up(comp(lower, kx) + max_z);
-    const float err_near_y = Up(comp(lower, ky) + max_z);
-    float onx = up_(comp(org, kx) + Up(eps * err_near_x));
-    float ony = up_(comp(org, ky) + Up(eps * err_near_y));
-    const float onz = comp(org, kz);
-    const float err_far_x = Up(comp(upper, kx) + max_z);
-    const float err_far_y = Up(comp(upper, ky) + max_z);
-    float ofx = dn_(comp(org, kx) - Up(eps * err_far_x));
-    float ofy = dn_(comp(org, ky) - Up(eps * err_far_y));
-    const float ofz = comp(org, kz);
-    if (comp(dir, kx) < 0.0f) { const float t = onx; onx = ofx; ofx = t; }
-    if (comp(dir, ky) < 0.0f) { const float t = ony; ony = ofy; ofy = t; }
-    const float on_k[3] = {onx, ony, onz}, of_k[3] = {ofx, ofy, ofz};
-    const int ks[3] = {kx, ky, kz};
     float on[3], of[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            if (ks[q] == a) {
-                on[a] = on_k[q];
-                of[a] = of_k[q];
-            }
-        }
-    }
+    raybox_axis(org.x, dir.x, lower.x, upper.x, max_z, kz == 0, on[0], of[0]);
+    raybox_axis(org.y, dir.y, lower.y, upper.y, max_z, kz == 1, on[1], of[1]);
+    raybox_axis(org.z, dir.z, lower.z, upper.z, max_z, kz == 2, on[2], of[2]);
     RayBox h;
     h.o0 = F2v{on[0], of[0]};
     h.o1 = F2v{on[1], of[1]};

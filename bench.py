@@ -66,8 +66,8 @@ L2_PEAK_GBS = 34500.0   # MI355X_MICROARCH.md, L2 (per XCD) section: aggregate L
 # instruction stream takes on the whole chip (a lower bound: transcendentals and DVFS only add).
 VALU_SIMDS, VALU_CYC, CLOCK_GHZ = 1024, 4, 2.4
 DELTA_MS = 16.667       # fixed AutoExposure step (SURVEY §8d determinism settings)
-PMC_FILE = os.path.join(ROOT, "profiles", "r05_pmc_kernels.json")  # tools/prof.sh pmc of the pipelined frames
-PMC_C2C4 = os.path.join(ROOT, "profiles", "r05_pmc_c2c4.json")  # KEY=c2c4 tools/prof.sh pmc probe.py c2c4
+PMC_FILE = os.path.join(ROOT, "profiles", "r06_pmc_kernels.json")  # tools/prof.sh pmc of the pipelined frames
+PMC_C2C4 = os.path.join(ROOT, "profiles", "r06_pmc_c2c4.json")  # KEY=c2c4 tools/prof.sh pmc probe.py c2c4
 TERRAIN_CAM = dict(pos=(8.0, 15.0, -6.0), yaw=0.0, pitch=-0.7)  # ~50 % primary hits (tests' camera)
 
 # algorithmic bytes: per node visit the 64-B node record, per triangle test the
@@ -377,7 +377,7 @@ def stream_kernels(shade_on_side):
 
 def pmc_c2c4(kernel, key):
     """HBM bytes per launch and L2 hit rate of a config-2 / config-4 kernel from the committed PMC
-    passes (KEY=c2c4 tools/prof.sh <dir> pmc tools/probe.py c2c4 -> profiles/r05_pmc_c2c4.json), when
+    passes (KEY=c2c4 tools/prof.sh <dir> pmc tools/probe.py c2c4 -> profiles/r06_pmc_c2c4.json), when
     its workload matches: k_trace_primary of the 1920x1080 1-spp launch, and the LBVH build of the
     958,720-triangle scene (the build launch with the most workgroups of that run)."""
     if not os.path.exists(PMC_C2C4):
@@ -818,7 +818,7 @@ def main():
                    "timed frames (rt_frame_marks); chosen from warm-up frames 2..%d with every kernel marked; the "
                    "other kernels: the same events over 20 pipelined frames after the timed ones "
                    "(rt_time_frame_kernels); rocprofv3 --kernel-trace --stats of this command: "
-                   "profiles/r05_kernel_stats.csv (this process: warm-up, timed, 1 detail and the 20 split frames)"
+                   "profiles/r06_kernel_stats.csv (this process: warm-up, timed, 1 detail and the 20 split frames)"
                    % (dom, marked, args.warmup)),
         "kernel_ms_split_frames": round(split_dom, 5) if split_dom is not None else None,
     }

@@ -454,11 +454,6 @@ RT_HD void sincosf_fcore(float x, float& sn, float& cs) {
     cs = q == 0 ? c : q == 1 ? -s : q == 2 ? -c : s;
 }
 
-// entry i in {0, 2..8} of a 9-entry table, by a select chain (no indexed private array)
-RT_HD float tab9(int i, float v0, float v2, float v3, float v4, float v5, float v6, float v7, float v8) {
-    return i == 8 ? v8 : i == 7 ? v7 : i == 6 ? v6 : i == 5 ? v5 : i == 4 ? v4 : i == 3 ? v3 : i == 2 ? v2 : v0;
-}
-
 // atan(num / den) as hi + lo (hi a table value, lo the rest) for 0 <= num, den finite, not both 0:
 // with a <= b the smaller and larger of the two, atan(a / b) = atan(c) + atan(t),
 // t = (a - c b) / (b + c a), c = i / 8 nearest to a / b (i = 1 taken as 0, so that |atan t| stays
@@ -478,16 +473,17 @@ RT_HD void atan_ratio_f(float num, float den, float& hi, float& lo) {
     p = f_fma(p, t2, 1.0f / 5.0f);
     p = f_fma(p, t2, -1.0f / 3.0f);
     const float at = f_fma(t * t2, p, t);
-    // atan(i/8) and pi/2 - atan(i/8) as float pairs
-    const float th = swap ? tab9(i, 0x1.921fb6p+0f,
-                            0x1.5368cap+0f, 0x1.36475p+0f, 0x1.1b6e1ap+0f, 0x1.031f58p+0f, 0x1.dac67p-1f, 0x1.b434eep-1f, 0x1.921fb6p-1f)
-                          : tab9(i, 0.0f,
-                            0x1.f5b76p-3f, 0x1.6f6194p-2f, 0x1.dac67p-2f, 0x1.1e00bap-1f, 0x1.4978fap-1f, 0x1.700a7cp-1f, 0x1.921fb6p-1f);
-    const float tl = swap ? tab9(i, -0x1.777a5cp-25f,
-                            -0x1.5c2c6p-25f, 0x1.e57aaep-27f, -0x1.a28838p-25f, -0x1.ab5242p-28f, 0x1.586ed4p-27f, 0x1.8809fep-28f, -0x1.777a5cp-26f)
-                          : tab9(i, 0.0f,
-                            -0x1.b4dfc8p-29f, 0x1.e4defp-30f, 0x1.586ed4p-28f, 0x1.7bdfd6p-26f, 0x1.934f7p-28f, 0x1.5e118cp-27f, -0x1.777a5cp-26f);
-    hi = th;
+    // atan(i/8) (row 0) and pi/2 - atan(i/8) (row 1) as float pairs, i = 0, 2..8 (entry 1 repeats
+    // entry 0): one table read per value (a select chain here became a dozen exec-mask branches)
+    static constexpr float kTh[2][9] = {
+        {0.0f, 0.0f, 0x1.f5b76p-3f, 0x1.6f6194p-2f, 0x1.dac67p-2f, 0x1.1e00bap-1f, 0x1.4978fap-1f, 0x1.700a7cp-1f, 0x1.921fb6p-1f},
+        {0x1.921fb6p+0f, 0x1.921fb6p+0f, 0x1.5368cap+0f, 0x1.36475p+0f, 0x1.1b6e1ap+0f, 0x1.031f58p+0f, 0x1.dac67p-1f, 0x1.b434eep-1f, 0x1.921fb6p-1f}};
+    static constexpr float kTl[2][9] = {
+        {0.0f, 0.0f, -0x1.b4dfc8p-29f, 0x1.e4defp-30f, 0x1.586ed4p-28f, 0x1.7bdfd6p-26f, 0x1.934f7p-28f, 0x1.5e118cp-27f, -0x1.777a5cp-26f},
+        {-0x1.777a5cp-25f, -0x1.777a5cp-25f, -0x1.5c2c6p-25f, 0x1.e57aaep-27f, -0x1.a28838p-25f, -0x1.ab5242p-28f, 0x1.586ed4p-27f, 0x1.8809fep-28f, -0x1.777a5cp-26f}};
+    const int row = swap ? 1 : 0;
+    const float tl = kTl[row][i];
+    hi = kTh[row][i];
     lo = swap ? tl - at : tl + at;
 }
 

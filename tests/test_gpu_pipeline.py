@@ -239,3 +239,79 @@ def test_pipelined_list_toggles_match_serial_and_oracle(rtx, oracle, tmp_path, d
         g = oracle.pathtrace(default_scene["bvh"], w, h, frame_num=f, spp=spp, cam=cam, sky_out=s, tex=tex)
         o = dn.draw(g, f, params=op, delta_time=16.667)
         assert np.array_equal(images[False][f - 1], o["rgba"]), f
+
+
+def test_serial_counter_blocks_across_mode_switches(rtx, tmp_path):
+    """Serial frames start without a counter memset: each frame's resolve zeroes the other of two
+    counter blocks for the next frame (frame.cpp syncZeroed).  Frames interleaved with what dirties
+    those blocks — rt_trace_rays (block 0), a pipelined stretch (block 0 is pipelined slot 0), the
+    per-kernel timing path — must equal an uninterrupted sequence of synchronous draws, frame by frame."""
+    import torch
+
+    w, h = 192, 112
+    ref = draw_sequence_plain(rtx, tmp_path, "plain", w, h, 8)
+    cfg = rtx.write_config(str(tmp_path / "mix.toml"), w, h, spp=2)
+    rt = rtx.RayTracer(w, h, cfg).init()
+    rt.set_delta_time(16.667)
+    target = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda:0")
+    got = []
+    for f in range(1, 9):
+        if f == 3:
+            rt.trace_rays([[0.2, 0.2, 0.0]], [[0.0, 0.0, 1.0]])
+        if f == 5:  # frames 5 and 6 pipelined, then synchronous again
+            rt.set_post_stream(post_stream().cuda_stream)
+        if f == 7:
+            rt.set_post_stream(None)
+        rt.draw_device(target.data_ptr(), 0, asynchronous=f in (5, 6))
+        rt.sync()
+        got.append(target.cpu().numpy().copy())
+    rt.cleanup()
+    for f, (a, b) in enumerate(zip(ref, got), start=1):
+        assert np.array_equal(a, b), "frame %d" % f
+
+
+def draw_sequence_plain(rtx, tmp_path, name, w, h, frames):
+    import torch
+
+    cfg = rtx.write_config(str(tmp_path / (name + ".toml")), w, h, spp=2)
+    rt = rtx.RayTracer(w, h, cfg).init()
+    rt.set_delta_time(16.667)
+    target = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda:0")
+    out = []
+    for _ in range(frames):
+        rt.draw_device(target.data_ptr(), 0)
+        out.append(target.cpu().numpy().copy())
+    rt.cleanup()
+    return out
+
+
+def test_bound_accumulation_keeps_the_list_chain(rtx, tmp_path):
+    """A caller-bound accumulation buffer (rt_bind_buffer) no longer turns the active-tile list chain
+    off: the chain writes the internal buffer and copies the frame back into the caller's.  Every
+    frame's RGBA8 and the caller's buffer equal a context without the binding."""
+    import torch
+
+    w, h, frames = 192, 112, 6
+    outs = []
+    for bound in (False, True):
+        cfg = rtx.write_config(str(tmp_path / ("acc%d.toml" % bound)), w, h, spp=2)
+        rt = rtx.RayTracer(w, h, cfg).init()
+        rt.set_delta_time(16.667)
+        acc = None
+        if bound:
+            acc = torch.zeros(rt.buffer_bytes("ACCUMULATION"), dtype=torch.uint8, device="cuda:0")
+            rt.bind_buffer("ACCUMULATION", acc.data_ptr(), acc.numel())
+        imgs = []
+        rgba = np.zeros((h, w, 4), np.uint8)
+        for _ in range(frames):
+            rt.draw(rgba)
+            imgs.append(rgba.copy())
+        accum = rt.get_buffer("ACCUMULATION").copy()
+        if bound:
+            torch.cuda.synchronize()
+            assert np.array_equal(acc.cpu().numpy()[:accum.size], accum)
+        outs.append((imgs, accum))
+        rt.cleanup()
+    for f, (a, b) in enumerate(zip(outs[0][0], outs[1][0]), start=1):
+        assert np.array_equal(a, b), "frame %d" % f
+    assert np.array_equal(outs[0][1], outs[1][1])

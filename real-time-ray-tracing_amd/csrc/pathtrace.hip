@@ -472,7 +472,8 @@ inline bool one_round(uint32_t spp) { return spp >= 1 && ((int)spp + cam_sample_
 //
 // kOneRound: every sample wave runs one round (spp <= 4 except 3: the launcher checks), so the
 // round loop and its carried state compile away.
-template <bool kOneRound>
+// kStats: the launch keeps per-pixel statistics (P.statsOut), so the traversal counts visits and tests
+template <bool kOneRound, bool kStats>
 __global__ __launch_bounds__(256, kOneRound ? 6 : 4) void k_pt_camera(PathTraceParams P) {
     // stack entries in LDS (the rest in registers): 26 KB per workgroup, 6 workgroups per CU
     // (measured: 16 entries 4 per CU 0.948 ms/frame, 12 entries 5 per CU 0.918, 10 entries 6 per CU
@@ -526,7 +527,7 @@ __global__ __launch_bounds__(256, kOneRound ? 6 : 4) void k_pt_camera(PathTraceP
                 DeepStack deep;
                 TravRec trec;  // each iteration loads its own record (kCarry false: occupancy)
                 for (int it = 0; it < 1024; ++it)
-                    if (trav_step<kCamLds, false>(sc, tr, st, trec, stk + tid, 256, &deep)) break;
+                    if (trav_step<kCamLds, false, kStats>(sc, tr, st, trec, stk + tid, 256, &deep)) break;
             }
             ++rays;
             if (P.statsOut) {  // the pixel's counters are added after the round loop
@@ -974,13 +975,15 @@ constexpr bool kChainStaticFirst = RTX_CHAIN_STATIC != 0;  // ablation: static f
 // Per sample the code is the one the separate kernels run (resume_entry, trav_step), so the
 // G-buffers are identical.  The hit records a wave reads in phase 2 are ones its own lanes wrote
 // (a workgroup-scope fence orders them), so no record crosses workgroups inside the launch.
+template <bool kStats>
 RT_DEV bool chain_step(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk) {
-    return trav_step<16, false>(sc, r, s, rec, stk, 256, nullptr);  // no carried record: 168 VGPRs, no scratch
+    return trav_step<16, false, kStats>(sc, r, s, rec, stk, 256, nullptr);  // no carried record: 168 VGPRs, no scratch
 }
 
 #ifndef RTX_CHAIN_WAVES
 #define RTX_CHAIN_WAVES 3
 #endif
+template <bool kStats>  // as k_pt_camera's
 __global__ __launch_bounds__(256, RTX_CHAIN_WAVES) void k_pt_chain(PathTraceParams P) {
     __shared__ uint2 stk[17 * 256];  // 16 entries + trav_step's dead slot
     __shared__ uint32_t sob[256];
@@ -1050,7 +1053,7 @@ __global__ __launch_bounds__(256, RTX_CHAIN_WAVES) void k_pt_chain(PathTracePara
             if (tail ? active : trav_lane_steps(active, s)) {
                 bool done = false;
                 do {
-                    done = chain_step(sc, r, s, rec, stk + tid) || s.iters >= 1024u || (occlusion && s.hitIdx >= 0);
+                    done = chain_step<kStats>(sc, r, s, rec, stk + tid) || s.iters >= 1024u || (occlusion && s.hitIdx >= 0);
                 } while (tail && !done);
                 if (done) {
                     P.ws.hitRec[idx] = make_float4(s.t, __uint_as_float((uint32_t)s.hitIdx), s.hitU, s.hitV);
@@ -1094,12 +1097,12 @@ __global__ __launch_bounds__(256, RTX_CHAIN_WAVES) void k_pt_chain(PathTracePara
                 if (nq4 < 16u) {  // few rays: plain per-lane loop (no ballots, no leaf batching)
 #pragma unroll 1
                     while (act)
-                        if (chain_step(sc, r4, s4, rec4, stk + tid) || s4.iters >= 1024u || s4.hitIdx >= 0) act = false;
+                        if (chain_step<kStats>(sc, r4, s4, rec4, stk + tid) || s4.iters >= 1024u || s4.hitIdx >= 0) act = false;
                 } else {
 #pragma unroll 1
                     while (__ballot(act) != 0ull) {
                         if (trav_lane_steps(act, s4)) {
-                            if (chain_step(sc, r4, s4, rec4, stk + tid) || s4.iters >= 1024u || s4.hitIdx >= 0)
+                            if (chain_step<kStats>(sc, r4, s4, rec4, stk + tid) || s4.iters >= 1024u || s4.hitIdx >= 0)
                                 act = false;
                         }
                     }
@@ -1203,8 +1206,10 @@ extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t
     const int nSW = cam_sample_waves(p->spp);
     const int BW = nSW == 4 ? 8 : 16, BH = nSW == 1 ? 16 : 8;
     const dim3 grid((p->width + BW - 1) / BW, (p->rows + BH - 1) / BH);
-    if (one_round(p->spp)) hipLaunchKernelGGL(k_pt_camera<true>, grid, dim3(256), 0, stream, *p);
-    else hipLaunchKernelGGL(k_pt_camera<false>, grid, dim3(256), 0, stream, *p);
+    const bool stats = p->statsOut != nullptr;
+    void (*k)(PathTraceParams) = one_round(p->spp) ? (stats ? k_pt_camera<true, true> : k_pt_camera<true, false>)
+                                                   : (stats ? k_pt_camera<false, true> : k_pt_camera<false, false>);
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, *p);
     if (marks && marks[1] && (e = hipEventRecord(marks[1], stream)) != hipSuccess) return e;
     return hipGetLastError();
 }
@@ -1299,7 +1304,7 @@ hipError_t launch_rest(const PathTraceParams* p, hipStream_t stream, hipEvent_t*
     if (p->ws.chain && !p->ws.glossy && !p->ws.microfacet) {
         // kernel 2 = the fused bounce chain (trace<3> .. resume<4>); slots 3-5 stay empty, so the
         // hook's kernel numbers and the per-kernel timing slots keep their meaning
-        hipLaunchKernelGGL(k_pt_chain, dim3(p->ws.traceBlocks), pb, 0, stream, *p);
+        hipLaunchKernelGGL(p->statsOut ? k_pt_chain<true> : k_pt_chain<false>, dim3(p->ws.traceBlocks), pb, 0, stream, *p);
         for (int j = 0; j < 4; ++j)
             if ((e = end()) != hipSuccess || (e = begin()) != hipSuccess) return e;
     } else {

@@ -17,6 +17,9 @@
 
 using namespace rtd;
 
+// kStats: the launch writes per-ray statistics (P.statsOut), so the traversal counts visits, tests
+// and dropped pushes
+template <bool kStats>
 #ifndef RTX_PRIMARY_WPE  // ablation builds only (tools/abl_build.sh): force waves per SIMD
 __global__ __launch_bounds__(256) void k_trace_primary(TracePrimaryParams P) {
 #else
@@ -40,13 +43,13 @@ void k_trace_primary(TracePrimaryParams P) {
 
     const SceneView sc = scene_view(P.nodes, P.tlasNodes, P.triPos, P.triNrm);
     HitInfo hi;
-    intersect<kLds>(sc, org, dir, stk + tid, 256, hi);
+    intersect<kLds, kStats>(sc, org, dir, stk + tid, 256, hi);
 
     const size_t p = (size_t)y * P.width + x;
     P.hitOut[p] = make_float4(hi.t, __int_as_float(hi.objectIdx), hi.u, hi.v);
     if (P.normalOut) P.normalOut[p] = make_float4(hi.normal.x, hi.normal.y, hi.normal.z, hi.hit ? 1.0f : 0.0f);
     if (P.fakeNormalOut) P.fakeNormalOut[p] = make_float4(hi.fakeNormal.x, hi.fakeNormal.y, hi.fakeNormal.z, hi.offset);
-    if (P.statsOut) {
+    if (kStats) {
         P.statsOut[4 * p + 0] = hi.visits;
         P.statsOut[4 * p + 1] = hi.tests;
         P.statsOut[4 * p + 2] = hi.dropped;
@@ -56,7 +59,8 @@ void k_trace_primary(TracePrimaryParams P) {
 
 extern "C" hipError_t rtk_launch_trace_primary(const TracePrimaryParams* p, hipStream_t stream) {
     dim3 grid((p->width + 15) / 16, (p->rows + 15) / 16);
-    hipLaunchKernelGGL(k_trace_primary, grid, dim3(256), 0, stream, *p);
+    if (p->statsOut) hipLaunchKernelGGL(k_trace_primary<true>, grid, dim3(256), 0, stream, *p);
+    else hipLaunchKernelGGL(k_trace_primary<false>, grid, dim3(256), 0, stream, *p);
     return hipGetLastError();
 }
 

@@ -30,7 +30,8 @@ constexpr uint32_t kTrace3Short = 1u << 20;  // queue-3 length below which trace
 #endif
 constexpr bool kLeafBatch = RTX_LEAF_BATCH != 0;  // ablation: -DRTX_LEAF_BATCH=0
 
-template <int kStep>
+// kStats: the launch keeps per-pixel statistics (P.statsOut), so the traversal counts visits and tests
+template <int kStep, bool kStats>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) {
     __shared__ uint2 stk[17 * kTraceBlock];  // 16 entries + the dead slot trav_step stores above the top
     // The tracers' waves issue at the denoise kernels' priority (DN_PRIO), above the next frame's
@@ -100,10 +101,10 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
         if (tail || !kLeafBatch ? active : trav_lane_steps(active, s)) {
             bool done;
             do {  // two steps per trip: the loop's refill / exec-mask bookkeeping once per two
-                done = trav_step<16>(sc, r, s, rec, stk + tid, kTraceBlock, nullptr) || s.iters >= 1024u ||
+                done = trav_step<16, true, kStats>(sc, r, s, rec, stk + tid, kTraceBlock, nullptr) || s.iters >= 1024u ||
                        (occlusion && s.hitIdx >= 0);
                 if (!done && (tail || !kLeafBatch || trav_lane_steps(true, s)))
-                    done = trav_step<16>(sc, r, s, rec, stk + tid, kTraceBlock, nullptr) || s.iters >= 1024u ||
+                    done = trav_step<16, true, kStats>(sc, r, s, rec, stk + tid, kTraceBlock, nullptr) || s.iters >= 1024u ||
                            (occlusion && s.hitIdx >= 0);
             } while (tail && !done);
             if (done) {
@@ -140,7 +141,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_queue(PathTraceParams P) 
 
 extern "C" int rtk_trace_queue_blocks_per_cu() {
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_trace_queue<3>, kTraceBlock, 0) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_trace_queue<3, false>, kTraceBlock, 0) != hipSuccess) return 0;
     return b;
 }
 
@@ -148,7 +149,9 @@ extern "C" hipError_t rtk_launch_trace_queue(const PathTraceParams* p, int step,
     const uint32_t blocks = step == 3 ? p->ws.traceBlocks : p->ws.trace4Blocks;
     if (blocks < 1) return hipErrorInvalidValue;
     const dim3 grid(blocks);
-    if (step == 3) hipLaunchKernelGGL(k_trace_queue<3>, grid, dim3(kTraceBlock), 0, stream, *p);
-    else hipLaunchKernelGGL(k_trace_queue<4>, grid, dim3(kTraceBlock), 0, stream, *p);
+    const bool stats = p->statsOut != nullptr;
+    void (*k)(PathTraceParams) = step == 3 ? (stats ? k_trace_queue<3, true> : k_trace_queue<3, false>)
+                                           : (stats ? k_trace_queue<4, true> : k_trace_queue<4, false>);
+    hipLaunchKernelGGL(k, grid, dim3(kTraceBlock), 0, stream, *p);
     return hipGetLastError();
 }

@@ -368,7 +368,9 @@ RT_DEV TravRec trav_first_rec(const SceneView& sc) { return trav_load(sc, sc.roo
 // kCarry false: the iteration loads its own record at its start instead (rec is scratch, nothing
 // is carried from one iteration to the next: 14 fewer registers live across the loop, for kernels
 // whose occupancy the registers set — the camera rays, the fused chain).
-template <int kLds, bool kCarry = true>
+// kStats false: the node-visit, triangle-test and dropped-push counters are not kept (launches
+// without per-pixel statistics; the iteration count, which the 1024 cap reads, always is).
+template <int kLds, bool kCarry = true, bool kStats = true>
 RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, TravRec& rec, uint2* stk, int stride,
                       DeepStack* deep) {
     static_assert(kLds >= 10 && kLds <= 16, "LDS stack depth: 10..16 entries (at most 6 in registers)");
@@ -394,8 +396,10 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, TravR
     const bool both = i1 && i2;
     const bool goLeft = i1 && (!i2 || t1 < t2);
     const bool push = both && tp < 15;  // a push onto a full stack is dropped
-    s.dropped += (both && !push) ? 1u : 0u;
-    s.visits += isNode ? 1u : 0u;
+    if (kStats) {
+        s.dropped += (both && !push) ? 1u : 0u;
+        s.visits += isNode ? 1u : 0u;
+    }
     const uint2 pushed = make_uint2(goLeft ? rec.d.y : rec.d.x, __float_as_uint(goLeft ? t2 : t1));
     if (kLds == 16) {
         stk[(tp + 1) * stride] = pushed;
@@ -416,7 +420,7 @@ RT_DEV bool trav_step(const SceneView& sc, const TravRay& r, TravState& s, TravR
     // hit; otherwise the loop makes every pop (a +inf start enters it)
     float et = pop ? (kLds == 16 ? __uint_as_float((uint32_t)(e >> 32)) : __builtin_inff()) : -kFltMax;
     if (isTri) {  // after the box tests' values are spent: fewer registers live through it
-        ++s.tests;
+        if (kStats) ++s.tests;
         float tt;
         if (watertight(r.tr, r.org, f3_of(rec.a), f3_of(rec.b), f3_of(rec.c), s.t, tt, s.u, s.v, s.errT) && tt < s.t) {
             s.t = tt;
@@ -494,7 +498,7 @@ RT_DEV void finalize_hit(const SceneView& sc, F3 org, F3 dir, float t, int hitId
 
 // One ray's closest hit (RaySceneIntersect): scene cull, then trav_step to the end.  stk: this
 // thread's stack column (kLds + 1 slots when kLds is 16).
-template <int kLds = 16>
+template <int kLds = 16, bool kStats = true>
 RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint2* stk, int stride, HitInfo& out) {
     TravState s;
     if (root_surely_missed(sc, org, dir)) {
@@ -506,7 +510,7 @@ RT_DEV void intersect(const SceneView& sc, F3 org, F3 dir, uint2* stk, int strid
         DeepStack deep;
         TravRec rec = trav_first_rec(sc);
         for (int it = 0; it < 1024; ++it)
-            if (trav_step<kLds>(sc, r, s, rec, stk, stride, &deep)) break;
+            if (trav_step<kLds, true, kStats>(sc, r, s, rec, stk, stride, &deep)) break;
     }
     finalize_hit(sc, org, dir, s.t, s.hitIdx, s.hitU, s.hitV, s.hitErrT, out);
     out.u = s.u;

@@ -47,6 +47,10 @@ constexpr bool kDnPk = RTX_DN_PK != 0;  // paired tap weights (rtmath_pk.h)
 #endif
 constexpr int kDnBatch = 5;  // SpatialFilterGlobal5x5 taps per load batch (unpaired)
 #define DN5_BOUNDS __launch_bounds__(256)
+#ifndef RTX_DN_SPLIT  // ablation builds only: 0 = the list passes at one thread per pixel
+#define RTX_DN_SPLIT 1
+#endif
+constexpr bool kDnSplit = RTX_DN_SPLIT != 0;
 
 // gaussian.cuh:12-43 (double literals converted to float, as the reference's float arrays)
 __constant__ float cG3[9] = RT_GAUSS3_INIT;
@@ -448,6 +452,10 @@ __global__ __launch_bounds__(256) void k_noise_visualize(DenoisePostParams P, ui
 template <int kParity, bool kRcp, bool kPk = false>
 RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD, int tx,
                             int ty);
+constexpr int kS7Split = 12;  // SpatialFilter7x7 with two threads per pixel: half 0 takes taps [0, 12)
+template <int kParity, bool kRcp, bool kPk>
+RT_DEV uint2 spatial7_pixel_split(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD,
+                                  int tx, int ty, int half, bool inside, float4* sX);
 
 struct S7Lds {
     uint2 C[22 * 22];
@@ -517,6 +525,42 @@ __global__ __launch_bounds__(256) void k_spatial7_list(DenoisePostParams P, cons
     if (threadIdx.x == 0 && !(n16 < P.dn.noise_threshold_large)) list_append(P, 1, tile);
 }
 
+// k_spatial7_list with two threads per pixel (spatial7_pixel_split)
+template <bool kRcp, bool kPk>
+__global__ __launch_bounds__(512) void k_spatial7_list2(DenoisePostParams P, const uint2* in, uint2* out) {
+    DN_PRIO();
+    __shared__ S7Lds L;
+    __shared__ float4 sX[(24 - kS7Split) * 256];
+    const int W = (int)P.W, H = (int)P.H, W16 = (W + 15) / 16;
+    uint32_t tile;
+    if (!list_tile(P, 0, tile)) return;
+    const int BX = (int)(tile % (uint32_t)W16), TY = (int)(tile / (uint32_t)W16);
+    if (TY < P.ty0 || TY >= P.ty1) return;
+    const int lid = (int)(threadIdx.x & 255u), half = (int)(threadIdx.x >> 8);
+    const int tx = lid & 15, ty = lid >> 4;
+    const int x = BX * 16 + tx, y = TY * 16 + ty;
+    const View2 col{in, W, H}, nrm{P.normal, W, H};
+    const View1 dep{P.depth, W, H};
+    for (int i = (int)threadIdx.x; i < 22 * 22; i += 512) {
+        const int lx = BX * 16 - 3 + i % 22, ly = TY * 16 - 3 + i / 22;
+        L.C[i] = col.at(lx, ly);
+        L.N[i] = nrm.at(lx, ly);
+        L.D[i] = dep.at(lx, ly);
+    }
+    __syncthreads();
+    const bool inside = x < W && y < H;
+    // the tap set alternates with the frame parity: both sets compiled with constant offsets
+    const uint2 res = P.frameNum % 2 == 0 ? spatial7_pixel_split<0, kRcp, kPk>(P, L.C, L.N, L.D, tx, ty, half, inside, sX)
+                                          : spatial7_pixel_split<1, kRcp, kPk>(P, L.C, L.N, L.D, tx, ty, half, inside, sX);
+    if (half == 0 && inside) {
+        out[(size_t)y * W + x] = res;
+        L.Out[lid] = res;
+    }
+    __syncthreads();
+    const float n16 = noise_epilogue(P, L.Out, L.N8, BX, TY);
+    if (threadIdx.x == 0 && !(n16 < P.dn.noise_threshold_large)) list_append(P, 1, tile);
+}
+
 // the weight of one SpatialFilter7x7 tap (tap d, n already sanitised)
 template <bool kRcp>
 RT_DEV float spatial7_weight(const DenoisePostParams& P, F3 nV, float dV, uint32_t mV, uint32_t mq, float d, F3 n,
@@ -548,71 +592,129 @@ RT_DEV rtpk::F2 spatial7_weight2(const DenoisePostParams& P, F3 nV, float dV, ui
     return w * F2{cG7[g0], cG7[g1]};
 }
 
+// The centre pixel of SpatialFilter7x7 (NaNs sanitised) and whether it is filtered
+struct S7Centre {
+    uint2 c0;
+    F3 nV;
+    float dV;
+    uint32_t mV;
+    bool filt;
+};
+RT_DEV S7Centre spatial7_centre(const uint2* sC, const uint2* sN, const float* sD, int tx, int ty) {
+    const int ci = (tx + 3) + (ty + 3) * 22;
+    S7Centre c;
+    c.c0 = sC[ci];
+    const F3 cV = rgb_of(c.c0);
+    c.dV = sD[ci];
+    c.nV = rgb_of(sN[ci]);
+    c.mV = mask_of(c.c0);
+    if (c.dV != c.dV) c.dV = 0.0f;
+    if (isnan3(c.nV)) c.nV = f3(0.0f);
+    c.filt = !isnan3(cV) && c.dV < kRayMaxF;
+    return c;
+}
+
+// Taps i in [kBeg, kEnd) of SpatialFilter7x7 (tap j = kParity + 2i of the 7x7 window), in tap order:
+// each tap's sanitised colour and its weight go to sink(i, cc, w).  kBeg is a multiple of 6.
+template <int kParity, bool kRcp, bool kPk, int kBeg, int kEnd, class Sink>
+RT_DEV void spatial7_taps(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD, int tx, int ty,
+                          const S7Centre& c, Sink&& sink) {
+    static_assert(kBeg % 6 == 0 && kEnd % 6 == 0 && kBeg < kEnd && kEnd <= 24, "tap range");
+    // LDS reads in batches of six taps (as k_spatial5's loads)
+#pragma unroll
+    for (int i0 = kBeg; i0 < kEnd; i0 += 6) {
+        uint2 qv[6], nq[6];
+        float dv[6];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            const int j = kParity + 2 * (i0 + m);  // P.frameNum % 2 + 2i
+            const int li = (tx + j % 7) + (ty + j / 7) * 22;
+            qv[m] = sC[li];
+            dv[m] = sD[li];
+            nq[m] = sN[li];
+        }
+        F3 cc[6], n[6];
+        float d[6], w[6];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            cc[m] = rgb_of(qv[m]);
+            d[m] = dv[m];
+            n[m] = rgb_of(nq[m]);
+            if (isnan3(cc[m])) cc[m] = f3(0.0f);
+            if (d[m] != d[m]) d[m] = 0.0f;
+            if (isnan3(n[m])) n[m] = f3(0.0f);
+        }
+#pragma unroll
+        for (int m = 0; m < 6; m += (kPk ? 2 : 1)) {
+            const int j = kParity + 2 * (i0 + m), g = j % 7 + (j / 7) * 7;
+            if (kPk) {
+                const int j1 = j + 2, g1 = j1 % 7 + (j1 / 7) * 7;
+                const rtpk::F2 w2 = spatial7_weight2<kRcp>(P, c.nV, c.dV, c.mV, mask_of(qv[m]), mask_of(qv[m + 1]), d[m],
+                                                           d[m + 1], n[m], n[m + 1], g, g1);
+                w[m] = w2.x;
+                w[m + 1] = w2.y;
+            } else {
+                w[m] = spatial7_weight<kRcp>(P, c.nV, c.dV, c.mV, mask_of(qv[m]), d[m], n[m], g);
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 6; ++m) sink(i0 + m, cc[m], w[m]);
+    }
+}
+
+RT_DEV uint2 spatial7_finish(F3 sum, float sw, uint32_t mV) {
+    if (isnan3(sum)) sum = f3(0.0f);
+    if (sw != sw) sw = 0.0f;
+    F3 fin = sw == 0 ? f3(0.0f) : sum / sw;
+    if (isnan3(fin)) fin = f3(0.0f);
+    return pack_color(fin, mV);
+}
+
 template <int kParity, bool kRcp, bool kPk>
 RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD, int tx,
                             int ty) {
-    const int ci = (tx + 3) + (ty + 3) * 22;
-    const uint2 c0 = sC[ci];
-    uint2 res = c0;
-    const F3 cV = rgb_of(c0);
-    float dV = sD[ci];
-    F3 nV = rgb_of(sN[ci]);
-    const uint32_t mV = mask_of(c0);
-    if (dV != dV) dV = 0.0f;
-    if (isnan3(nV)) nV = f3(0.0f);
-    if (!isnan3(cV) && dV < kRayMaxF) {
-        F3 sum = f3(0.0f);
-        float sw = 0.0f;
-        // LDS reads in batches of six taps (as k_spatial5's loads)
-#pragma unroll
-        for (int i0 = 0; i0 < 24; i0 += 6) {
-            uint2 qv[6], nq[6];
-            float dv[6];
-#pragma unroll
-            for (int m = 0; m < 6; ++m) {
-                const int j = kParity + 2 * (i0 + m);  // P.frameNum % 2 + 2i
-                const int li = (tx + j % 7) + (ty + j / 7) * 22;
-                qv[m] = sC[li];
-                dv[m] = sD[li];
-                nq[m] = sN[li];
-            }
-            F3 cc[6], n[6];
-            float d[6], w[6];
-#pragma unroll
-            for (int m = 0; m < 6; ++m) {
-                cc[m] = rgb_of(qv[m]);
-                d[m] = dv[m];
-                n[m] = rgb_of(nq[m]);
-                if (isnan3(cc[m])) cc[m] = f3(0.0f);
-                if (d[m] != d[m]) d[m] = 0.0f;
-                if (isnan3(n[m])) n[m] = f3(0.0f);
-            }
-#pragma unroll
-            for (int m = 0; m < 6; m += (kPk ? 2 : 1)) {
-                const int j = kParity + 2 * (i0 + m), g = j % 7 + (j / 7) * 7;
-                if (kPk) {
-                    const int j1 = j + 2, g1 = j1 % 7 + (j1 / 7) * 7;
-                    const rtpk::F2 w2 = spatial7_weight2<kRcp>(P, nV, dV, mV, mask_of(qv[m]), mask_of(qv[m + 1]), d[m],
-                                                               d[m + 1], n[m], n[m + 1], g, g1);
-                    w[m] = w2.x;
-                    w[m + 1] = w2.y;
-                } else {
-                    w[m] = spatial7_weight<kRcp>(P, nV, dV, mV, mask_of(qv[m]), d[m], n[m], g);
-                }
-            }
-#pragma unroll
-            for (int m = 0; m < 6; ++m) {  // the sums in tap order
-                sum = sum + cc[m] * w[m];
-                sw += w[m];
-            }
-        }
-        if (isnan3(sum)) sum = f3(0.0f);
-        if (sw != sw) sw = 0.0f;
-        F3 fin = sw == 0 ? f3(0.0f) : sum / sw;
-        if (isnan3(fin)) fin = f3(0.0f);
-        res = pack_color(fin, mV);
+    const S7Centre c = spatial7_centre(sC, sN, sD, tx, ty);
+    if (!c.filt) return c.c0;
+    F3 sum = f3(0.0f);
+    float sw = 0.0f;
+    spatial7_taps<kParity, kRcp, kPk, 0, 24>(P, sC, sN, sD, tx, ty, c, [&](int, F3 cc, float w) {  // the sums in tap order
+        sum = sum + cc * w;
+        sw += w;
+    });
+    return spatial7_finish(sum, sw, c.mV);
+}
+
+// Two threads per pixel (spatial5_tile_split's scheme): half 0 sums taps 0..11, half 1 leaves taps
+// 12..23's weighted colours and weights in LDS (sX) for half 0 to add in order after the barrier
+template <int kParity, bool kRcp, bool kPk>
+RT_DEV uint2 spatial7_pixel_split(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD,
+                                  int tx, int ty, int half, bool inside, float4* sX) {
+    const int lid = ty * 16 + tx;
+    const S7Centre c = spatial7_centre(sC, sN, sD, tx, ty);  // in the staged apron for every lane
+    const bool filt = inside && c.filt;
+    F3 sum = f3(0.0f);
+    float sw = 0.0f;
+    if (half == 1) {
+        if (filt)
+            spatial7_taps<kParity, kRcp, kPk, kS7Split, 24>(P, sC, sN, sD, tx, ty, c, [&](int i, F3 cc, float w) {
+                const F3 pr = cc * w;
+                sX[(i - kS7Split) * 256 + lid] = make_float4(pr.x, pr.y, pr.z, w);
+            });
+    } else if (filt) {
+        spatial7_taps<kParity, kRcp, kPk, 0, kS7Split>(P, sC, sN, sD, tx, ty, c, [&](int, F3 cc, float w) {
+            sum = sum + cc * w;
+            sw += w;
+        });
     }
-    return res;
+    __syncthreads();
+    if (!filt || half != 0) return c.c0;
+#pragma unroll
+    for (int i = kS7Split; i < 24; ++i) {
+        const float4 v = sX[(i - kS7Split) * 256 + lid];
+        sum = sum + f3(v.x, v.y, v.z);
+        sw += v.w;
+    }
+    return spatial7_finish(sum, sw, c.mV);
 }
 
 // ------------------------------------------------------------------ SpatialFilterGlobal5x5<S>
@@ -663,81 +765,155 @@ RT_DEV rtpk::F2 spatial5_weight2(const DenoisePostParams& P, F3 nV, float dV, ui
     return w * F2{cG5[k], cG5[k + 1]};
 }
 
-// One pixel of SpatialFilterGlobal5x5<S> in a filtered tile (TX, TY).  kRedirect: `in` holds only
-// the list-1 tiles, so a tap whose (clamped) texel lies in a tile off the list (its bit clear in
-// `act`) reads `alt`, the accumulation buffer those tiles would have been copied from.  kPk: tap
-// weights two at a time (spatial5_weight2), batches of six taps.
+// Taps [kBeg, kEnd) of SpatialFilterGlobal5x5<S> around pixel (x, y) of a filtered tile (TX, TY), in
+// tap order: each tap's colour and weight, after the NaN rule, go to sink(k, cc, w).  kRedirect: `in`
+// holds only the list-1 tiles, so a tap whose (clamped) texel lies in a tile off the list (its bit
+// clear in `act`) reads `alt`, the accumulation buffer those tiles would have been copied from.  kPk:
+// tap weights two at a time (spatial5_weight2), batches of RTX_DN_PKB taps; kBeg is even.
+template <int S, bool kRcp, bool kRedirect, bool kPk, int kBeg, int kEnd, class Sink>
+RT_DEV void spatial5_taps(const DenoisePostParams& P, const uint2* in, const uint2* alt, uint32_t act, int x, int y,
+                          int TX, int TY, F3 nV, float dV, uint32_t mV, bool yOdd, Sink&& sink) {
+    static_assert(kBeg % 2 == 0 && kBeg < kEnd && kEnd <= 25, "tap range");
+    constexpr int kB = kPk ? RTX_DN_PKB : kDnBatch;
+    const int W = (int)P.W, H = (int)P.H;
+    // taps in batches of kB: a batch's loads are issued together, then its weights computed
+    // (the branches of rt_powf otherwise keep the compiler from hoisting the next tap's loads,
+    // one memory round trip per tap)
+#pragma unroll
+    for (int k0 = kBeg; k0 < kEnd; k0 += kB) {
+        uint2 qv[kB], nq[kB];
+        float dv[kB];
+#pragma unroll
+        for (int m = 0; m < kB; ++m) {
+            const int k = k0 + m < kEnd ? k0 + m : kEnd - 1;
+            const int cx = clampi(x + (k % 5 - 2) * S, 0, W - 1), cy = clampi(y + (k / 5 - 2) * S, 0, H - 1);
+            const size_t q = (size_t)cy * W + cx;
+            const uint2* src = in;
+            if (kRedirect) {
+                const int bit = ((cy >> 4) - TY + 2) * 5 + ((cx >> 4) - TX + 2);
+                src = ((act >> bit) & 1u) ? in : alt;
+            }
+            qv[m] = src[q];
+            dv[m] = h2f(P.depth[q]);
+            nq[m] = P.normal[q];
+        }
+        float wv[kB];
+#pragma unroll
+        for (int m = 0; m < kB; ++m) {
+            const int k = k0 + m;
+            if (k >= kEnd) break;
+            if (kPk && m % 2 == 0 && k + 1 < kEnd && m + 1 < kB) {
+                const rtpk::F2 w2 = spatial5_weight2<kRcp>(P, nV, dV, mV, qv[m], qv[m + 1], dv[m], dv[m + 1],
+                                                           nq[m], nq[m + 1], k, yOdd);
+                wv[m] = w2.x;
+                wv[m + 1] = w2.y;
+            } else if (!kPk || m % 2 == 0) {
+                wv[m] = spatial5_weight<kRcp>(P, nV, dV, mV, qv[m], dv[m], nq[m], k);
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < kB; ++m) {
+            if (k0 + m >= kEnd) break;
+            F3 cc = rgb_of(qv[m]);
+            float w = wv[m];
+            if (isnan3(cc)) { cc = f3(0.0f); w = 0.0f; }
+            sink(k0 + m, cc, w);
+        }
+    }
+}
+
+// The centre pixel's values SpatialFilterGlobal5x5 weighs its taps against (NaNs sanitised)
+struct S5Centre {
+    uint2 c0;
+    F3 nV;
+    float dV;
+    uint32_t mV;
+};
+RT_DEV S5Centre spatial5_centre(const DenoisePostParams& P, const uint2* in, size_t p) {
+    S5Centre c;
+    c.c0 = in[p];
+    c.nV = rgb_of(P.normal[p]);
+    c.mV = mask_of(c.c0);
+    c.dV = h2f(P.depth[p]);
+    if (c.dV != c.dV) c.dV = 0.0f;
+    if (isnan3(c.nV)) c.nV = f3(0.0f);
+    return c;
+}
+// the filtered pixel from the tap sums
+RT_DEV uint2 spatial5_finish(F3 sum, float sw, uint32_t mV) {
+    if (isnan3(sum)) sum = f3(0.0f);
+    if (sw != sw) sw = 0.0f;
+    F3 fin = sw == 0 ? f3(0.0f) : sum / sw;
+    if (isnan3(fin)) fin = f3(0.0f);
+    return pack_color(fin, mV);
+}
+
+// One pixel of SpatialFilterGlobal5x5<S> in a filtered tile (TX, TY): the 25 taps summed in tap order
 template <int S, bool kRcp, bool kRedirect, bool kPk = false>
 RT_DEV uint2 spatial5_pixel(const DenoisePostParams& P, const uint2* in, const uint2* alt, uint32_t act, int x, int y,
                             int TX, int TY) {
-    constexpr int kB = kPk ? RTX_DN_PKB : kDnBatch;
-    const int W = (int)P.W, H = (int)P.H;
-    const size_t p = (size_t)y * W + x;
-    const uint2 c0 = in[p];
-    uint2 res = c0;
-    F3 nV = rgb_of(P.normal[p]);
-    F3 cV = rgb_of(c0);
-    const uint32_t mV = mask_of(c0);
-    float dV = h2f(P.depth[p]);
-    if (isnan3(cV)) cV = f3(0.0f);
-    if (dV != dV) dV = 0.0f;
-    if (isnan3(nV)) nV = f3(0.0f);
+    const S5Centre c = spatial5_centre(P, in, (size_t)y * P.W + x);
+    if (!(c.dV < 10e9f)) return c.c0;
     const bool yOdd = kPk && rtpk::pow_y_odd(P.dn.large_denoise_sigma_normal);
-    if (dV < 10e9f) {
-        F3 sum = f3(0.0f);
-        float sw = 0.0f;
-        // taps in batches of kB: a batch's loads are issued together, then its weights computed
-        // (the branches of rt_powf otherwise keep the compiler from hoisting the next tap's loads,
-        // one memory round trip per tap)
-#pragma unroll
-        for (int k0 = 0; k0 < 25; k0 += kB) {
-            uint2 qv[kB], nq[kB];
-            float dv[kB];
-#pragma unroll
-            for (int m = 0; m < kB; ++m) {
-                const int k = k0 + m < 25 ? k0 + m : 24;
-                const int cx = clampi(x + (k % 5 - 2) * S, 0, W - 1), cy = clampi(y + (k / 5 - 2) * S, 0, H - 1);
-                const size_t q = (size_t)cy * W + cx;
-                const uint2* src = in;
-                if (kRedirect) {
-                    const int bit = ((cy >> 4) - TY + 2) * 5 + ((cx >> 4) - TX + 2);
-                    src = ((act >> bit) & 1u) ? in : alt;
-                }
-                qv[m] = src[q];
-                dv[m] = h2f(P.depth[q]);
-                nq[m] = P.normal[q];
-            }
-            float wv[kB];
-#pragma unroll
-            for (int m = 0; m < kB; ++m) {
-                const int k = k0 + m;
-                if (k >= 25) break;
-                if (kPk && m % 2 == 0 && k + 1 < 25 && m + 1 < kB) {
-                    const rtpk::F2 w2 = spatial5_weight2<kRcp>(P, nV, dV, mV, qv[m], qv[m + 1], dv[m], dv[m + 1],
-                                                               nq[m], nq[m + 1], k, yOdd);
-                    wv[m] = w2.x;
-                    wv[m + 1] = w2.y;
-                } else if (!kPk || m % 2 == 0) {
-                    wv[m] = spatial5_weight<kRcp>(P, nV, dV, mV, qv[m], dv[m], nq[m], k);
-                }
-            }
-#pragma unroll
-            for (int m = 0; m < kB; ++m) {  // the sums in tap order
-                if (k0 + m >= 25) break;
-                F3 cc = rgb_of(qv[m]);
-                float w = wv[m];
-                if (isnan3(cc)) { cc = f3(0.0f); w = 0.0f; }
-                sum = sum + cc * w;
-                sw += w;
-            }
-        }
-        if (isnan3(sum)) sum = f3(0.0f);
-        if (sw != sw) sw = 0.0f;
-        F3 fin = sw == 0 ? f3(0.0f) : sum / sw;
-        if (isnan3(fin)) fin = f3(0.0f);
-        res = pack_color(fin, mV);
+    F3 sum = f3(0.0f);
+    float sw = 0.0f;
+    spatial5_taps<S, kRcp, kRedirect, kPk, 0, 25>(P, in, alt, act, x, y, TX, TY, c.nV, c.dV, c.mV, yOdd,
+                                                   [&](int, F3 cc, float w) {
+                                                       sum = sum + cc * w;
+                                                       sw += w;
+                                                   });
+    return spatial5_finish(sum, sw, c.mV);
+}
+
+// Two threads per pixel (a 512-thread workgroup per 16x16 tile), for the passes that filter only
+// the tiles of a short list: half 0 sums taps 0..11 in order, half 1 computes taps 12..24 and
+// leaves each tap's weighted colour and weight in LDS, and half 0 adds those in order after the
+// barrier — the same products and the same sums in the same order as spatial5_pixel, on twice the
+// waves (a list pass's few tiles otherwise leave ~2 waves per SIMD to cover the taps' latency).
+constexpr int kS5Split = 12;  // half 0: taps [0, kS5Split)
+template <int S, bool kRcp, bool kRedirect, bool kPk>
+RT_DEV void spatial5_tile_split(const DenoisePostParams& P, const uint2* in, const uint2* alt, uint2* out, uint32_t act,
+                                int TX, int TY, float4* sX, bool albedo) {
+    const int W = (int)P.W, H = (int)P.H;
+    const int lid = (int)(threadIdx.x & 255u), half = (int)(threadIdx.x >> 8);
+    const int x = TX * 16 + (lid & 15), y = TY * 16 + (lid >> 4);
+    const bool inside = x < W && y < H;
+    const size_t p = (size_t)y * W + x;
+    // read at the clamped pixel outside the image (no lane keeps it), so the centre is never a
+    // conditionally initialised aggregate (which the compiler had put in scratch)
+    const S5Centre c = spatial5_centre(P, in, (size_t)(y < H ? y : H - 1) * W + (x < W ? x : W - 1));
+    const bool filt = inside && c.dV < 10e9f;
+    const bool yOdd = kPk && rtpk::pow_y_odd(P.dn.large_denoise_sigma_normal);
+    F3 sum = f3(0.0f);
+    float sw = 0.0f;
+    if (half == 1) {
+        if (filt)
+            spatial5_taps<S, kRcp, kRedirect, kPk, kS5Split, 25>(
+                P, in, alt, act, x, y, TX, TY, c.nV, c.dV, c.mV, yOdd, [&](int k, F3 cc, float w) {
+                    const F3 pr = cc * w;
+                    sX[(k - kS5Split) * 256 + lid] = make_float4(pr.x, pr.y, pr.z, w);
+                });
+    } else if (filt) {
+        spatial5_taps<S, kRcp, kRedirect, kPk, 0, kS5Split>(P, in, alt, act, x, y, TX, TY, c.nV, c.dV, c.mV, yOdd,
+                                                             [&](int, F3 cc, float w) {
+                                                                 sum = sum + cc * w;
+                                                                 sw += w;
+                                                             });
     }
-    return res;
+    __syncthreads();
+    if (half != 0 || !inside) return;
+    uint2 res = c.c0;
+    if (filt) {
+#pragma unroll
+        for (int k = kS5Split; k < 25; ++k) {
+            const float4 v = sX[(k - kS5Split) * 256 + lid];
+            sum = sum + f3(v.x, v.y, v.z);
+            sw += v.w;
+        }
+        res = spatial5_finish(sum, sw, c.mV);
+    }
+    if (albedo) res = pack_color(rgb_of(res) * rgb_of(P.albedo[p]), 0x3C00u);  // w = half(1.0)
+    out[p] = res;
 }
 
 // every tile of the launch's rows: tiles below the large threshold pass their input through (from
@@ -773,6 +949,36 @@ __global__ DN5_BOUNDS void k_spatial5_list(DenoisePostParams P, const uint2* in,
     const uint32_t act = kRedirect ? active_neighbourhood(P, TX, TY) : 0u;
     const int x = TX * 16 + (threadIdx.x & 15), y = TY * 16 + (threadIdx.x >> 4);
     if (x < W && y < H) out[(size_t)y * W + x] = spatial5_pixel<S, kRcp, kRedirect, kPk>(P, in, alt, act, x, y, TX, TY);
+}
+
+// k_spatial5_list with two threads per pixel (spatial5_tile_split).  kAlbedo: the last a-trous pass
+// (ApplyAlbedo fused into its store).  kCopy: the first one, which also writes the last pass's output
+// for the tiles off list 1 — ApplyAlbedo over the accumulation buffer (`alt`), what the last pass
+// would pass through for them — workgroup b for tile b of rows [P.cty0, P.cty1): list 1 is final
+// once SpatialFilter7x7 has run, and no a-trous pass reads `out` outside list-1 tiles (their taps
+// there read `alt`), so those tiles need no pass of their own after the list passes.
+template <int S, bool kRcp, bool kRedirect, bool kPk, bool kAlbedo = false, bool kCopy = false>
+__global__ __launch_bounds__(512) void k_spatial5_list2(DenoisePostParams P, const uint2* in, uint2* out, const uint2* alt) {
+    DN_PRIO();
+    __shared__ float4 sX[(25 - kS5Split) * 256];
+    const int W = (int)P.W, H = (int)P.H, W16 = (W + 15) / 16;
+    if (kCopy && threadIdx.x < 256) {
+        const uint32_t t = (uint32_t)P.cty0 * (uint32_t)W16 + blockIdx.x;
+        const int CX = (int)(t % (uint32_t)W16), CY = (int)(t / (uint32_t)W16);
+        if (CY < P.cty1 && h2f(P.noise16[t]) < P.dn.noise_threshold_large) {
+            const int x = CX * 16 + (int)(threadIdx.x & 15u), y = CY * 16 + (int)(threadIdx.x >> 4);
+            if (x < W && y < H) {
+                const size_t p = (size_t)y * W + x;
+                out[p] = pack_color(rgb_of(alt[p]) * rgb_of(P.albedo[p]), 0x3C00u);  // w = half(1.0)
+            }
+        }
+    }
+    uint32_t tile;
+    if (!list_tile(P, 1, tile)) return;
+    const int TX = (int)(tile % (uint32_t)W16), TY = (int)(tile / (uint32_t)W16);
+    if (TY < P.ty0 || TY >= P.ty1) return;
+    const uint32_t act = kRedirect ? active_neighbourhood(P, TX, TY) : 0u;
+    spatial5_tile_split<S, kRcp, kRedirect, kPk>(P, in, alt, out, act, TX, TY, sX, kAlbedo);
 }
 
 // ------------------------------------------------------------------ ApplyAlbedo (in place, pointwise)
@@ -1455,9 +1661,17 @@ __global__ __launch_bounds__(256) void k_hdr_out(const uint2* color, float4* hdr
 }  // namespace
 
 // the list chain's first two a-trous passes: depth-weight reciprocal x paired tap weights
-template <int S, bool kRedirect>
+template <int S, bool kRedirect, bool kAlbedo = false, bool kCopy = false>
 static void launch_s5_list(bool rcp, bool pk, dim3 g, hipStream_t s, const DenoisePostParams& Q, const uint2* in,
                            uint2* out, const uint2* alt) {
+    if (kDnSplit) {  // two threads per pixel (spatial5_tile_split)
+        const dim3 b2(512);
+        if (rcp && pk) hipLaunchKernelGGL((k_spatial5_list2<S, true, kRedirect, true, kAlbedo, kCopy>), g, b2, 0, s, Q, in, out, alt);
+        else if (rcp) hipLaunchKernelGGL((k_spatial5_list2<S, true, kRedirect, false, kAlbedo, kCopy>), g, b2, 0, s, Q, in, out, alt);
+        else if (pk) hipLaunchKernelGGL((k_spatial5_list2<S, false, kRedirect, true, kAlbedo, kCopy>), g, b2, 0, s, Q, in, out, alt);
+        else hipLaunchKernelGGL((k_spatial5_list2<S, false, kRedirect, false, kAlbedo, kCopy>), g, b2, 0, s, Q, in, out, alt);
+        return;
+    }
     const dim3 b(256);
     if (rcp && pk) hipLaunchKernelGGL((k_spatial5_list<S, true, kRedirect, true>), g, b, 0, s, Q, in, out, alt);
     else if (rcp) hipLaunchKernelGGL((k_spatial5_list<S, true, kRedirect, false>), g, b, 0, s, Q, in, out, alt);
@@ -1668,7 +1882,12 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         if (tiles(3, Q, g)) {
             DN_MARK(1, 0);
             if (useList) {  // list 0 only; TemporalFilter wrote the other tiles into the accumulation buffer
-                if (rcp7 && pk7) hipLaunchKernelGGL((k_spatial7_list<true, true>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
+                const dim3 b512(512);
+                if (kDnSplit && rcp7 && pk7) hipLaunchKernelGGL((k_spatial7_list2<true, true>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
+                else if (kDnSplit && rcp7) hipLaunchKernelGGL((k_spatial7_list2<true, false>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
+                else if (kDnSplit && pk7) hipLaunchKernelGGL((k_spatial7_list2<false, true>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
+                else if (kDnSplit) hipLaunchKernelGGL((k_spatial7_list2<false, false>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
+                else if (rcp7 && pk7) hipLaunchKernelGGL((k_spatial7_list<true, true>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
                 else if (rcp7) hipLaunchKernelGGL((k_spatial7_list<true, false>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
                 else if (pk7) hipLaunchKernelGGL((k_spatial7_list<false, true>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
                 else hipLaunchKernelGGL((k_spatial7_list<false, false>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
@@ -1698,9 +1917,18 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         uint2* a = cur == P->colorA ? P->colorB : cur == P->colorB ? P->colorA : spare;
         uint2* b = a == P->colorA ? P->colorB : P->colorA;
         const uint2* alt = cur;
+        // the list chain with two threads per pixel: the first pass also finishes the tiles off
+        // list 1 for the last (k_spatial5_list2 kCopy), which then runs over list 1 only
+        const bool fold = useList && kDnSplit;
+        int c0 = 0, c1 = 0;
+        tile_range(P, 1, c0, c1);
         if (tiles(3, Q, g)) {
             DN_MARK(2, 0);
-            if (useList) {
+            if (fold) {
+                Q.cty0 = c0;
+                Q.cty1 = c1;
+                launch_s5_list<3, false, false, true>(rcp5, pk5, gList, s, Q, (const uint2*)cur, a, alt);
+            } else if (useList) {
                 launch_s5_list<3, false>(rcp5, pk5, gList, s, Q, (const uint2*)cur, a, alt);
             } else {
                 if (rcp5) hipLaunchKernelGGL((k_spatial5<3, false, true, false>), g, b256, 0, s, Q, (const uint2*)cur, a, alt);
@@ -1722,7 +1950,9 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         }
         if (tiles(1, Q, g)) {
             DN_MARK(4, 0);
-            if (useList) {
+            if (fold) {
+                launch_s5_list<12, true, true>(rcp5, pk5, gList, s, Q, (const uint2*)b, a, alt);
+            } else if (useList) {
                 if (rcp5 && pk5) hipLaunchKernelGGL((k_spatial5<12, true, true, true, true>), g, b256, 0, s, Q, (const uint2*)b, a, alt);
                 else if (rcp5) hipLaunchKernelGGL((k_spatial5<12, true, true, true>), g, b256, 0, s, Q, (const uint2*)b, a, alt);
                 else if (pk5) hipLaunchKernelGGL((k_spatial5<12, true, false, true, true>), g, b256, 0, s, Q, (const uint2*)b, a, alt);

@@ -223,6 +223,8 @@ struct DenoisePostParams {
     uint32_t* rgbaTarget;       // strip-local: the caller's draw target, filled from `rgba` after the rows
     uint32_t rgbaTargetPitch;   // exchange (rgba is then the exchanged buffer); pitch in pixels
     int ty0, ty1;               // per launch (set by the launcher): tile rows of the 16x16-tile kernels
+    int cty0, cty1;             // the list chain's first a-trous launch: tile rows of the last pass it
+                                // finishes for tiles off list 1 (set by the launcher)
     uint32_t* chainCounter;     // k_downscale_chain's workgroup counter (zero between launches)
     int exposureDone;           // set by phase 0 when k_downscale_chain ran AutoExposure
     int histDepthInTemporal;    // k_temporal also copies depth into the history depth (per launch)

@@ -283,6 +283,85 @@ __global__ __launch_bounds__(256) void k_temporal(DenoisePostParams P, const uin
     }
 }
 
+// TemporalFilter after its spatial taps: the normalised sum, then the reprojected history clamped to
+// the neighbourhood's YCoCg box and blended with the pixel
+RT_DEV uint2 temporal_tail(const DenoisePostParams& P, const View2& acc, int x, int y, size_t p, F3 filt, float wsum,
+                           F3 nMin, F3 nMax, F3 cV, uint32_t mV) {
+    const int W = (int)P.W, H = (int)P.H;
+    uint2 res;
+    if (wsum > 0) filt = filt / wsum;
+    else filt = f3(0.0f);
+    if (isnan3(filt)) filt = f3(0.0f);
+    const uint32_t mvq = P.motion[p];
+    const F2 mv = {h2f(mvq & 0xFFFFu) - 0.5f, h2f(mvq >> 16) - 0.5f};
+    const F2 inv = {1.0f / (float)W, 1.0f / (float)H};
+    const F2 uv = {((float)x + 0.5f) * inv.x, ((float)y + 0.5f) * inv.y};
+    const F2 huv = {uv.x + mv.x, uv.y + mv.y};
+    if (huv.x < 0 || huv.y < 0 || huv.x > 1.0f || huv.y > 1.0f) {
+        res = pack_color(filt, mV);
+    } else {
+        F3 cH = bicubic_smooth(acc, huv);
+        const F3 cHy = clamp3(ycocg(cH), nMin, nMax);
+        cH = ycocg_inv(cHy);
+        const float lumaMin = nMin.x, lumaMax = nMax.x, lumaC = ycocg(cV).x;
+        float discard = 0.0f;
+        const int hx = (int)floorf(huv.x * (float)acc.W), hy = (int)floorf(huv.y * (float)acc.H);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) discard += (mV != mask_of(acc.at(hx + i % 2, hy + i / 2))) ? 1.0f : 0.0f;
+        discard /= 4.0f;
+        cH = cH * (1.0f - discard) + filt * discard;
+        const float lumaH = ycocg(cH).x;
+        if (isnan3(cH)) cH = f3(0.0f);
+        float blend = 1.0f / 8.0f;
+        blend *= 0.2f + 0.8f * clampf(0.5f * fminf(fabsf(lumaH - lumaMin), fabsf(lumaH - lumaMax)) /
+                                     fmaxf(fmaxf(lumaH, lumaC), 1e-4f));
+        float wA = blend * fmaxf(0.0001f, 1.0f / (lumaC + 4.0f));
+        float wB = (1.0f - blend) * fmaxf(0.0001f, 1.0f / (lumaH + 4.0f));
+        const float ws = safe_divide(1.0f, wA + wB);
+        wA *= ws;
+        wB *= ws;
+        F3 o = cV * wA + cH * wB;
+        if (isnan3(o)) o = f3(0.0f);
+        res = pack_color(o, mV);
+    }
+    return res;
+}
+
+// TemporalFilter's weights of taps [kBeg, kEnd) (kBeg even: the pairs are those of the whole set)
+template <bool kRcp, bool kPk, int kBeg, int kEnd>
+RT_DEV void temporal_weights(const DenoisePostParams& P, F3 nV, float dV, uint32_t mV, bool yOdd, const uint2* qv,
+                             const float* dv, const uint2* nq, float* wv) {
+#pragma unroll
+    for (int j = kBeg; j < kEnd; j += (kPk ? 2 : 1)) {
+        if (kPk && j + 1 < kEnd) {  // taps j, j + 1 as one register pair (rtmath_pk.h)
+            using rtpk::F2;
+            const F3 n0 = rgb_of(nq[j]), n1 = rgb_of(nq[j + 1]);
+            const F2 dt = rtpk::inner3_2(nV.x, F2{n0.x, n1.x}, nV.y, F2{n0.y, n1.y}, nV.z, F2{n0.z, n1.z});
+            const F2 pw = rtpk::pow_pos2(F2{fmaxf(dt.x, 0.0f), fmaxf(dt.y, 0.0f)},
+                                         P.dn.temporal_denoise_sigma_normal, yOdd);
+            const F2 dz = F2{dV - dv[j], dV - dv[j + 1]};
+            const float sd = P.dn.temporal_denoise_sigma_depth;
+            const F2 dd = kRcp ? rtpk::div_rcp2(dz, sd, P.rcpDepth[0]) : F2{dz.x / sd, dz.y / sd};
+            const F2 ew = rtpk::expf2((rtpk::splat(-0.5f) * dd) * dd);
+            const float mw = 1.0f / P.dn.temporal_denoise_sigma_material;
+            F2 w = pw * ew;
+            w = w * F2{mV != mask_of(qv[j]) ? mw : 1.0f, mV != mask_of(qv[j + 1]) ? mw : 1.0f};
+            w = w * F2{cG3[j], cG3[j + 1]};
+            wv[j] = w.x;
+            wv[j + 1] = w.y;
+        } else {
+            const F3 n = rgb_of(nq[j]);
+            float w = 1.0f;
+            w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.temporal_denoise_sigma_normal);
+            const float dd = depth_ratio<kRcp>(P, 0, dV - dv[j], P.dn.temporal_denoise_sigma_depth);
+            w *= DN_EXP(-0.5f * dd * dd);
+            w *= (mV != mask_of(qv[j])) ? 1.0f / P.dn.temporal_denoise_sigma_material : 1.0f;
+            w *= cG3[j];  // (j % 3) + (j / 3) * 3
+            wv[j] = w;
+        }
+    }
+}
+
 template <bool kRcp, bool kPk>
 RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, int y) {
     const int W = (int)P.W, H = (int)P.H;
@@ -313,35 +392,7 @@ RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, 
             nq[j] = nrm.at(sx, sy);
         }
         float wv[9];
-#pragma unroll
-        for (int j = 0; j < 9; j += (kPk ? 2 : 1)) {
-            if (kPk && j + 1 < 9) {  // taps j, j + 1 as one register pair (rtmath_pk.h)
-                using rtpk::F2;
-                const F3 n0 = rgb_of(nq[j]), n1 = rgb_of(nq[j + 1]);
-                const F2 dt = rtpk::inner3_2(nV.x, F2{n0.x, n1.x}, nV.y, F2{n0.y, n1.y}, nV.z, F2{n0.z, n1.z});
-                const F2 pw = rtpk::pow_pos2(F2{fmaxf(dt.x, 0.0f), fmaxf(dt.y, 0.0f)},
-                                             P.dn.temporal_denoise_sigma_normal, yOdd);
-                const F2 dz = F2{dV - dv[j], dV - dv[j + 1]};
-                const float sd = P.dn.temporal_denoise_sigma_depth;
-                const F2 dd = kRcp ? rtpk::div_rcp2(dz, sd, P.rcpDepth[0]) : F2{dz.x / sd, dz.y / sd};
-                const F2 ew = rtpk::expf2((rtpk::splat(-0.5f) * dd) * dd);
-                const float mw = 1.0f / P.dn.temporal_denoise_sigma_material;
-                F2 w = pw * ew;
-                w = w * F2{mV != mask_of(qv[j]) ? mw : 1.0f, mV != mask_of(qv[j + 1]) ? mw : 1.0f};
-                w = w * F2{cG3[j], cG3[j + 1]};
-                wv[j] = w.x;
-                wv[j + 1] = w.y;
-            } else {
-                const F3 n = rgb_of(nq[j]);
-                float w = 1.0f;
-                w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.temporal_denoise_sigma_normal);
-                const float dd = depth_ratio<kRcp>(P, 0, dV - dv[j], P.dn.temporal_denoise_sigma_depth);
-                w *= DN_EXP(-0.5f * dd * dd);
-                w *= (mV != mask_of(qv[j])) ? 1.0f / P.dn.temporal_denoise_sigma_material : 1.0f;
-                w *= cG3[j];  // (j % 3) + (j / 3) * 3
-                wv[j] = w;
-            }
-        }
+        temporal_weights<kRcp, kPk, 0, 9>(P, nV, dV, mV, yOdd, qv, dv, nq, wv);
 #pragma unroll
         for (int j = 0; j < 9; ++j) {  // the sums in tap order
             const F3 cc = rgb_of(qv[j]);
@@ -352,41 +403,7 @@ RT_DEV uint2 temporal_pixel(const DenoisePostParams& P, const uint2* in, int x, 
             nMax = fmax3(nMax, nc);
             nMin = fmin3(nMin, nc);
         }
-        if (wsum > 0) filt = filt / wsum;
-        else filt = f3(0.0f);
-        if (isnan3(filt)) filt = f3(0.0f);
-        const uint32_t mvq = P.motion[p];
-        const F2 mv = {h2f(mvq & 0xFFFFu) - 0.5f, h2f(mvq >> 16) - 0.5f};
-        const F2 inv = {1.0f / (float)W, 1.0f / (float)H};
-        const F2 uv = {((float)x + 0.5f) * inv.x, ((float)y + 0.5f) * inv.y};
-        const F2 huv = {uv.x + mv.x, uv.y + mv.y};
-        if (huv.x < 0 || huv.y < 0 || huv.x > 1.0f || huv.y > 1.0f) {
-            res = pack_color(filt, mV);
-        } else {
-            F3 cH = bicubic_smooth(acc, huv);
-            const F3 cHy = clamp3(ycocg(cH), nMin, nMax);
-            cH = ycocg_inv(cHy);
-            const float lumaMin = nMin.x, lumaMax = nMax.x, lumaC = ycocg(cV).x;
-            float discard = 0.0f;
-            const int hx = (int)floorf(huv.x * (float)acc.W), hy = (int)floorf(huv.y * (float)acc.H);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) discard += (mV != mask_of(acc.at(hx + i % 2, hy + i / 2))) ? 1.0f : 0.0f;
-            discard /= 4.0f;
-            cH = cH * (1.0f - discard) + filt * discard;
-            const float lumaH = ycocg(cH).x;
-            if (isnan3(cH)) cH = f3(0.0f);
-            float blend = 1.0f / 8.0f;
-            blend *= 0.2f + 0.8f * clampf(0.5f * fminf(fabsf(lumaH - lumaMin), fabsf(lumaH - lumaMax)) /
-                                         fmaxf(fmaxf(lumaH, lumaC), 1e-4f));
-            float wA = blend * fmaxf(0.0001f, 1.0f / (lumaC + 4.0f));
-            float wB = (1.0f - blend) * fmaxf(0.0001f, 1.0f / (lumaH + 4.0f));
-            const float ws = safe_divide(1.0f, wA + wB);
-            wA *= ws;
-            wB *= ws;
-            F3 o = cV * wA + cH * wB;
-            if (isnan3(o)) o = f3(0.0f);
-            res = pack_color(o, mV);
-        }
+        res = temporal_tail(P, acc, x, y, p, filt, wsum, nMin, nMax, cV, mV);
     }
     return res;
 }
@@ -455,7 +472,7 @@ RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const u
 constexpr int kS7Split = 12;  // SpatialFilter7x7 with two threads per pixel: half 0 takes taps [0, 12)
 template <int kParity, bool kRcp, bool kPk>
 RT_DEV uint2 spatial7_pixel_split(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD,
-                                  int tx, int ty, int half, bool inside, float4* sX);
+                                  int tx, int ty, int half, bool inside, float* sX);
 
 struct S7Lds {
     uint2 C[22 * 22];
@@ -530,7 +547,7 @@ template <bool kRcp, bool kPk>
 __global__ __launch_bounds__(512) void k_spatial7_list2(DenoisePostParams P, const uint2* in, uint2* out) {
     DN_PRIO();
     __shared__ S7Lds L;
-    __shared__ float4 sX[(24 - kS7Split) * 256];
+    __shared__ float sX[(24 - kS7Split) * 256];
     const int W = (int)P.W, H = (int)P.H, W16 = (W + 15) / 16;
     uint32_t tile;
     if (!list_tile(P, 0, tile)) return;
@@ -685,10 +702,11 @@ RT_DEV uint2 spatial7_pixel(const DenoisePostParams& P, const uint2* sC, const u
 }
 
 // Two threads per pixel (spatial5_tile_split's scheme): half 0 sums taps 0..11, half 1 leaves taps
-// 12..23's weighted colours and weights in LDS (sX) for half 0 to add in order after the barrier
+// 12..23's weights in LDS (sX), and half 0 adds those taps in order after the barrier, their colours
+// read again from the staged apron (the same texels, sanitised the same way)
 template <int kParity, bool kRcp, bool kPk>
 RT_DEV uint2 spatial7_pixel_split(const DenoisePostParams& P, const uint2* sC, const uint2* sN, const float* sD,
-                                  int tx, int ty, int half, bool inside, float4* sX) {
+                                  int tx, int ty, int half, bool inside, float* sX) {
     const int lid = ty * 16 + tx;
     const S7Centre c = spatial7_centre(sC, sN, sD, tx, ty);  // in the staged apron for every lane
     const bool filt = inside && c.filt;
@@ -696,10 +714,8 @@ RT_DEV uint2 spatial7_pixel_split(const DenoisePostParams& P, const uint2* sC, c
     float sw = 0.0f;
     if (half == 1) {
         if (filt)
-            spatial7_taps<kParity, kRcp, kPk, kS7Split, 24>(P, sC, sN, sD, tx, ty, c, [&](int i, F3 cc, float w) {
-                const F3 pr = cc * w;
-                sX[(i - kS7Split) * 256 + lid] = make_float4(pr.x, pr.y, pr.z, w);
-            });
+            spatial7_taps<kParity, kRcp, kPk, kS7Split, 24>(P, sC, sN, sD, tx, ty, c,
+                                                            [&](int i, F3, float w) { sX[(i - kS7Split) * 256 + lid] = w; });
     } else if (filt) {
         spatial7_taps<kParity, kRcp, kPk, 0, kS7Split>(P, sC, sN, sD, tx, ty, c, [&](int, F3 cc, float w) {
             sum = sum + cc * w;
@@ -710,9 +726,12 @@ RT_DEV uint2 spatial7_pixel_split(const DenoisePostParams& P, const uint2* sC, c
     if (!filt || half != 0) return c.c0;
 #pragma unroll
     for (int i = kS7Split; i < 24; ++i) {
-        const float4 v = sX[(i - kS7Split) * 256 + lid];
-        sum = sum + f3(v.x, v.y, v.z);
-        sw += v.w;
+        const int j = kParity + 2 * i;
+        F3 cc = rgb_of(sC[(tx + j % 7) + (ty + j / 7) * 22]);
+        if (isnan3(cc)) cc = f3(0.0f);
+        const float w = sX[(i - kS7Split) * 256 + lid];
+        sum = sum + cc * w;
+        sw += w;
     }
     return spatial7_finish(sum, sw, c.mV);
 }
@@ -732,15 +751,27 @@ RT_DEV uint32_t active_neighbourhood(const DenoisePostParams& P, int TX, int TY)
 }
 
 // One tap's weight and weighted colour of SpatialFilterGlobal5x5 (the scalar form)
+// The a-trous passes' sigmas and depth reciprocal, read from the launch parameters once per pixel
+// and passed by value (reading them in each tap's weight, the split kernels had copied them through
+// a private array)
+struct S5Sig {
+    float sn, sd, sm, rcp;
+};
+RT_DEV S5Sig s5_sig(const DenoisePostParams& P) {
+    // uniform values: through readfirstlane, so that no vectorised copy of the triple is formed
+    auto u = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+    return S5Sig{u(P.dn.large_denoise_sigma_normal), u(P.dn.large_denoise_sigma_depth),
+                 u(P.dn.large_denoise_sigma_material), u(P.rcpDepth[2])};
+}
+
 template <bool kRcp>
-RT_DEV float spatial5_weight(const DenoisePostParams& P, F3 nV, float dV, uint32_t mV, uint2 q, float d, uint2 nq,
-                             int k) {
+RT_DEV float spatial5_weight(const S5Sig g, F3 nV, float dV, uint32_t mV, uint2 q, float d, uint2 nq, int k) {
     const F3 n = rgb_of(nq);
     float w = 1.0f;
-    w *= DN_POW(fmaxf(dot(nV, n), 0.0f), P.dn.large_denoise_sigma_normal);
-    const float dd = depth_ratio<kRcp>(P, 2, dV - d, P.dn.large_denoise_sigma_depth);
+    w *= DN_POW(fmaxf(dot(nV, n), 0.0f), g.sn);
+    const float dd = kRcp ? rt_div_rcp(dV - d, g.sd, g.rcp) : (dV - d) / g.sd;  // depth_ratio of pass 2
     w *= DN_EXP(-0.5f * dd * dd);
-    w *= (mV != mask_of(q)) ? 1.0f / P.dn.large_denoise_sigma_material : 1.0f;
+    w *= (mV != mask_of(q)) ? 1.0f / g.sm : 1.0f;
     w *= cG5[k];
     return w;
 }
@@ -749,20 +780,32 @@ RT_DEV float spatial5_weight(const DenoisePostParams& P, F3 nV, float dV, uint32
 // element, the polynomial and compensated-dot chains issued once for both); pow's special cases
 // need large_denoise_sigma_normal finite and > 0 (rtpk::pow_pos_ok, checked by the launcher)
 template <bool kRcp>
-RT_DEV rtpk::F2 spatial5_weight2(const DenoisePostParams& P, F3 nV, float dV, uint32_t mV, uint2 q0, uint2 q1, float d0,
-                                 float d1, uint2 nq0, uint2 nq1, int k, bool yOdd) {
+RT_DEV rtpk::F2 spatial5_weight2(const S5Sig g, F3 nV, float dV, uint32_t mV, uint2 q0, uint2 q1, float d0, float d1,
+                                 uint2 nq0, uint2 nq1, int k, bool yOdd) {
     using rtpk::F2;
     const F3 n0 = rgb_of(nq0), n1 = rgb_of(nq1);
     const F2 dt = rtpk::inner3_2(nV.x, F2{n0.x, n1.x}, nV.y, F2{n0.y, n1.y}, nV.z, F2{n0.z, n1.z});
-    const F2 pw = rtpk::pow_pos2(F2{fmaxf(dt.x, 0.0f), fmaxf(dt.y, 0.0f)}, P.dn.large_denoise_sigma_normal, yOdd);
+    const F2 pw = rtpk::pow_pos2(F2{fmaxf(dt.x, 0.0f), fmaxf(dt.y, 0.0f)}, g.sn, yOdd);
     const F2 dz = F2{dV - d0, dV - d1};
-    const float sd = P.dn.large_denoise_sigma_depth;
-    const F2 dd = kRcp ? rtpk::div_rcp2(dz, sd, P.rcpDepth[2]) : F2{dz.x / sd, dz.y / sd};
+    const float sd = g.sd;
+    const F2 dd = kRcp ? rtpk::div_rcp2(dz, sd, g.rcp) : F2{dz.x / sd, dz.y / sd};
     const F2 ew = rtpk::expf2((rtpk::splat(-0.5f) * dd) * dd);
-    const float mw = 1.0f / P.dn.large_denoise_sigma_material;
+    const float mw = 1.0f / g.sm;
     F2 w = pw * ew;
     w = w * F2{mV != mask_of(q0) ? mw : 1.0f, mV != mask_of(q1) ? mw : 1.0f};
     return w * F2{cG5[k], cG5[k + 1]};
+}
+
+// the texel of tap k (clamped; kRedirect: `alt` outside the list-1 tiles of `act`)
+template <int S, bool kRedirect>
+RT_DEV const uint2* spatial5_tap_src(const DenoisePostParams& P, const uint2* in, const uint2* alt, uint32_t act, int x,
+                                     int y, int TX, int TY, int k, size_t& q) {
+    const int W = (int)P.W, H = (int)P.H;
+    const int cx = clampi(x + (k % 5 - 2) * S, 0, W - 1), cy = clampi(y + (k / 5 - 2) * S, 0, H - 1);
+    q = (size_t)cy * W + cx;
+    if (!kRedirect) return in;
+    const int bit = ((cy >> 4) - TY + 2) * 5 + ((cx >> 4) - TX + 2);
+    return ((act >> bit) & 1u) ? in : alt;
 }
 
 // Taps [kBeg, kEnd) of SpatialFilterGlobal5x5<S> around pixel (x, y) of a filtered tile (TX, TY), in
@@ -772,10 +815,9 @@ RT_DEV rtpk::F2 spatial5_weight2(const DenoisePostParams& P, F3 nV, float dV, ui
 // tap weights two at a time (spatial5_weight2), batches of RTX_DN_PKB taps; kBeg is even.
 template <int S, bool kRcp, bool kRedirect, bool kPk, int kBeg, int kEnd, class Sink>
 RT_DEV void spatial5_taps(const DenoisePostParams& P, const uint2* in, const uint2* alt, uint32_t act, int x, int y,
-                          int TX, int TY, F3 nV, float dV, uint32_t mV, bool yOdd, Sink&& sink) {
+                          int TX, int TY, F3 nV, float dV, uint32_t mV, bool yOdd, const S5Sig g, Sink&& sink) {
     static_assert(kBeg % 2 == 0 && kBeg < kEnd && kEnd <= 25, "tap range");
     constexpr int kB = kPk ? RTX_DN_PKB : kDnBatch;
-    const int W = (int)P.W, H = (int)P.H;
     // taps in batches of kB: a batch's loads are issued together, then its weights computed
     // (the branches of rt_powf otherwise keep the compiler from hoisting the next tap's loads,
     // one memory round trip per tap)
@@ -786,13 +828,8 @@ RT_DEV void spatial5_taps(const DenoisePostParams& P, const uint2* in, const uin
 #pragma unroll
         for (int m = 0; m < kB; ++m) {
             const int k = k0 + m < kEnd ? k0 + m : kEnd - 1;
-            const int cx = clampi(x + (k % 5 - 2) * S, 0, W - 1), cy = clampi(y + (k / 5 - 2) * S, 0, H - 1);
-            const size_t q = (size_t)cy * W + cx;
-            const uint2* src = in;
-            if (kRedirect) {
-                const int bit = ((cy >> 4) - TY + 2) * 5 + ((cx >> 4) - TX + 2);
-                src = ((act >> bit) & 1u) ? in : alt;
-            }
+            size_t q;
+            const uint2* src = spatial5_tap_src<S, kRedirect>(P, in, alt, act, x, y, TX, TY, k, q);
             qv[m] = src[q];
             dv[m] = h2f(P.depth[q]);
             nq[m] = P.normal[q];
@@ -803,12 +840,12 @@ RT_DEV void spatial5_taps(const DenoisePostParams& P, const uint2* in, const uin
             const int k = k0 + m;
             if (k >= kEnd) break;
             if (kPk && m % 2 == 0 && k + 1 < kEnd && m + 1 < kB) {
-                const rtpk::F2 w2 = spatial5_weight2<kRcp>(P, nV, dV, mV, qv[m], qv[m + 1], dv[m], dv[m + 1],
+                const rtpk::F2 w2 = spatial5_weight2<kRcp>(g, nV, dV, mV, qv[m], qv[m + 1], dv[m], dv[m + 1],
                                                            nq[m], nq[m + 1], k, yOdd);
                 wv[m] = w2.x;
                 wv[m + 1] = w2.y;
             } else if (!kPk || m % 2 == 0) {
-                wv[m] = spatial5_weight<kRcp>(P, nV, dV, mV, qv[m], dv[m], nq[m], k);
+                wv[m] = spatial5_weight<kRcp>(g, nV, dV, mV, qv[m], dv[m], nq[m], k);
             }
         }
 #pragma unroll
@@ -857,7 +894,7 @@ RT_DEV uint2 spatial5_pixel(const DenoisePostParams& P, const uint2* in, const u
     const bool yOdd = kPk && rtpk::pow_y_odd(P.dn.large_denoise_sigma_normal);
     F3 sum = f3(0.0f);
     float sw = 0.0f;
-    spatial5_taps<S, kRcp, kRedirect, kPk, 0, 25>(P, in, alt, act, x, y, TX, TY, c.nV, c.dV, c.mV, yOdd,
+    spatial5_taps<S, kRcp, kRedirect, kPk, 0, 25>(P, in, alt, act, x, y, TX, TY, c.nV, c.dV, c.mV, yOdd, s5_sig(P),
                                                    [&](int, F3 cc, float w) {
                                                        sum = sum + cc * w;
                                                        sw += w;
@@ -866,14 +903,15 @@ RT_DEV uint2 spatial5_pixel(const DenoisePostParams& P, const uint2* in, const u
 }
 
 // Two threads per pixel (a 512-thread workgroup per 16x16 tile), for the passes that filter only
-// the tiles of a short list: half 0 sums taps 0..11 in order, half 1 computes taps 12..24 and
-// leaves each tap's weighted colour and weight in LDS, and half 0 adds those in order after the
-// barrier — the same products and the same sums in the same order as spatial5_pixel, on twice the
-// waves (a list pass's few tiles otherwise leave ~2 waves per SIMD to cover the taps' latency).
+// the tiles of a short list: half 0 sums taps 0..11 in order, half 1 computes the weights of taps
+// 12..24 and leaves them in LDS, and half 0 — which loads those taps' texels again while it waits at
+// the barrier — adds them in order after it: the same products and the same sums in the same order
+// as spatial5_pixel, on twice the waves (a list pass's few tiles otherwise leave ~2 waves per SIMD
+// to cover the taps' latency), with 4 bytes of LDS per tap.
 constexpr int kS5Split = 12;  // half 0: taps [0, kS5Split)
 template <int S, bool kRcp, bool kRedirect, bool kPk>
 RT_DEV void spatial5_tile_split(const DenoisePostParams& P, const uint2* in, const uint2* alt, uint2* out, uint32_t act,
-                                int TX, int TY, float4* sX, bool albedo) {
+                                int TX, int TY, float* sX, bool albedo) {
     const int W = (int)P.W, H = (int)P.H;
     const int lid = (int)(threadIdx.x & 255u), half = (int)(threadIdx.x >> 8);
     const int x = TX * 16 + (lid & 15), y = TY * 16 + (lid >> 4);
@@ -889,26 +927,34 @@ RT_DEV void spatial5_tile_split(const DenoisePostParams& P, const uint2* in, con
     if (half == 1) {
         if (filt)
             spatial5_taps<S, kRcp, kRedirect, kPk, kS5Split, 25>(
-                P, in, alt, act, x, y, TX, TY, c.nV, c.dV, c.mV, yOdd, [&](int k, F3 cc, float w) {
-                    const F3 pr = cc * w;
-                    sX[(k - kS5Split) * 256 + lid] = make_float4(pr.x, pr.y, pr.z, w);
-                });
-    } else if (filt) {
-        spatial5_taps<S, kRcp, kRedirect, kPk, 0, kS5Split>(P, in, alt, act, x, y, TX, TY, c.nV, c.dV, c.mV, yOdd,
+                P, in, alt, act, x, y, TX, TY, c.nV, c.dV, c.mV, yOdd, s5_sig(P),
+                [&](int k, F3, float w) { sX[(k - kS5Split) * 256 + lid] = w; });
+    }
+    uint2 qv[25 - kS5Split];
+    if (half == 0 && filt) {
+        spatial5_taps<S, kRcp, kRedirect, kPk, 0, kS5Split>(P, in, alt, act, x, y, TX, TY, c.nV, c.dV, c.mV, yOdd, s5_sig(P),
                                                              [&](int, F3 cc, float w) {
                                                                  sum = sum + cc * w;
                                                                  sw += w;
                                                              });
+#pragma unroll
+        for (int k = kS5Split; k < 25; ++k) {
+            size_t q;
+            const uint2* src = spatial5_tap_src<S, kRedirect>(P, in, alt, act, x, y, TX, TY, k, q);
+            qv[k - kS5Split] = src[q];
+        }
     }
     __syncthreads();
     if (half != 0 || !inside) return;
     uint2 res = c.c0;
     if (filt) {
 #pragma unroll
-        for (int k = kS5Split; k < 25; ++k) {
-            const float4 v = sX[(k - kS5Split) * 256 + lid];
-            sum = sum + f3(v.x, v.y, v.z);
-            sw += v.w;
+        for (int k = kS5Split; k < 25; ++k) {  // spatial5_taps' sink for these taps
+            F3 cc = rgb_of(qv[k - kS5Split]);
+            float w = sX[(k - kS5Split) * 256 + lid];
+            if (isnan3(cc)) { cc = f3(0.0f); w = 0.0f; }
+            sum = sum + cc * w;
+            sw += w;
         }
         res = spatial5_finish(sum, sw, c.mV);
     }
@@ -960,7 +1006,7 @@ __global__ DN5_BOUNDS void k_spatial5_list(DenoisePostParams P, const uint2* in,
 template <int S, bool kRcp, bool kRedirect, bool kPk, bool kAlbedo = false, bool kCopy = false>
 __global__ __launch_bounds__(512) void k_spatial5_list2(DenoisePostParams P, const uint2* in, uint2* out, const uint2* alt) {
     DN_PRIO();
-    __shared__ float4 sX[(25 - kS5Split) * 256];
+    __shared__ float sX[(25 - kS5Split) * 256];
     const int W = (int)P.W, H = (int)P.H, W16 = (W + 15) / 16;
     if (kCopy && threadIdx.x < 256) {
         const uint32_t t = (uint32_t)P.cty0 * (uint32_t)W16 + blockIdx.x;

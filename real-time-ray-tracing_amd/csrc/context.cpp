@@ -338,6 +338,11 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
         t.shadeBlocksPerCu = rttoml::find_or_int(doc, "tuning", "shadeBlocksPerCu", 0);
         t.overlapAfter = rttoml::find_or_int(doc, "tuning", "overlapAfter", -1);
         t.cameraAfter = rttoml::find_or_int(doc, "tuning", "cameraAfter", -1);
+        t.syncSpec = rttoml::find_or_bool(doc, "tuning", "syncSpec", true);
+        t.specChain = rttoml::find_or_int(doc, "tuning", "specChain", -1);
+        t.specAfter = rttoml::find_or_int(doc, "tuning", "specAfter", 1);
+        t.specShade = rttoml::find_or_int(doc, "tuning", "specShade", 1);
+        t.specTracePerCu = rttoml::find_or_int(doc, "tuning", "specTracePerCu", 2);
     }
     if (ctx->screenW <= 0 || ctx->screenH <= 0 || ctx->screenW > 16384 || ctx->screenH > 16384 || ctx->spp < 1 ||
         ctx->spp > 64 || ctx->chunkDim < 1 || ctx->chunkDim > 8 ||
@@ -494,7 +499,8 @@ int rt_init(rt_context* ctx) {
 void rt_destroy(rt_context* ctx) {
     if (!ctx) return;
     if (ctx->inited) (void)sync_streams(ctx, false);  // also when the context stream is the null stream
-    for (hipEvent_t e : {ctx->overlapEv, ctx->cameraGate, ctx->buildDone[0], ctx->buildDone[1], ctx->bvhFree[0], ctx->bvhFree[1]})
+    for (hipEvent_t e : {ctx->overlapEv, ctx->cameraGate, ctx->specGate, ctx->specDone, ctx->buildDone[0], ctx->buildDone[1],
+                         ctx->bvhFree[0], ctx->bvhFree[1]})
         if (e) (void)hipEventDestroy(e);
     for (int k = 0; k < kGbSets; ++k)
         for (hipEvent_t e : {ctx->ptDone[k], ctx->postDone[k], ctx->camDone[k], ctx->restDone[k], ctx->gatherDone[k]})
@@ -605,6 +611,9 @@ int rt_build_bvh(rt_context* ctx) {
     if (!ctx->inited) { ctx->err = "rt_build_bvh before rt_init"; return RT_ERR_STATE; }
     if (int rc = check_device_status(ctx)) return rc;  // a previous build's failure, once it is known
     hipStream_t stream = ctx->stream;
+    // camera rays a synchronous draw traced ahead read this set (frame.cpp launch_spec_camera): the
+    // rebuild writes the same values, but after them
+    if (ctx->fr.spec.valid) HIP_TRY(ctx, hipStreamWaitEvent(stream, ctx->specDone, 0));
     ctx->bvhPrebuilt = false;  // an explicit build supersedes a synchronous draw's prebuild
     if (!ctx->postStream) ctx->buildOnSide[ctx->bvhSet] = false;
     if (ctx->postStream) {  // frame pipelining: build into the other set, on the side stream

@@ -101,11 +101,24 @@ struct FrameResources {
     uint32_t* camSurface[kGbSets] = {};
     uint32_t* camCount[kGbSets] = {};  // counter block per slot (PtWorkspace::counters)
     uint32_t* lastCounters = nullptr;  // the block of the last path trace (RT_ARR_PT_QUEUE)
-    // serial frames: two counter blocks in turn, syncCount[0] = camCount[0]; the resolve of a frame
-    // zeroes the other one (syncZeroed), so the next frame's camera kernel needs no memset
-    uint32_t* syncCount[2] = {};
+    // serial frames: three counter blocks in turn, syncCount[0] = camCount[0]; the resolve of a
+    // frame using block b zeroes block b + 2 (syncZeroed), so the camera kernel of the frame after
+    // next needs no memset — and the next frame's, traced ahead (spec), has a zeroed block of its own
+    uint32_t* syncCount[3] = {};
     int syncIdx = 0;
-    bool syncZeroed[2] = {};
+    bool syncZeroed[3] = {};
+    // synchronous draws: the next frame's camera rays traced ahead, beside this frame's bounces and
+    // denoise, into the other G-buffer set (frame.cpp launch_spec_camera); the next rt_path_trace
+    // uses them when its launch parameters equal `p`, and traces them again otherwise
+    struct Spec {
+        bool valid = false;
+        bool shade = false;  // the shade kernel went ahead too
+        int block = 0;
+        PathTraceParams p{};
+    } spec;
+    bool specReady = false;          // set 1's buffers and the events exist (ensure_sync_spec)
+    bool gbBound = false;            // a G-buffer is the caller's (rt_bind_buffer): no set rotation
+    unsigned long long* specRayCounter = nullptr;  // the rays of the launches ahead (folded in when used)
     bool camInFlight[kGbSets] = {};
     // ... and the bounce queues with their hit records, one slot per set when the shade kernel
     // runs on the side stream (shadeOnSide: frame f+1's shade appends to its queues while frame
@@ -210,6 +223,11 @@ struct rt_context {
         bool shadeOnSide = true;
         int shadeBlocksPerCu = 0;  // k_pt_shade0's grid per CU (0: its residency)
         int overlapAfter = -1, cameraAfter = -1;
+        bool syncSpec = true;   // synchronous draws trace the next frame's camera rays ahead
+        int specChain = -1;     // ... and their bounces with the fused chain (1), the four kernels (0) or by queue 3's length (-1)
+        int specAfter = 1;      // ... the next camera rays after kernel k of this frame (1 shade, 2 trace<3>, ..)
+        int specShade = 1;      // ... and the next frame's shade kernel after them: 0 never, 1 beside the lean kernels, 2 always
+        int specTracePerCu = 2; // ... this frame's bounce chain / queue-3 tracer at so many workgroups per CU (0: as usual)
     } tune;
 
     std::string err;
@@ -258,6 +276,7 @@ struct rt_context {
                            // ends (0: no gate; 1 GPU), kernel 2 = trace<3> on 2 GPUs, kernel 3 =
                            // resume<3> on more (set by rt_set_post_stream)
     hipEvent_t cameraGate = nullptr;
+    hipEvent_t specGate = nullptr, specDone = nullptr;  // synchronous draws' camera rays traced ahead
     bool cameraGated = false;
     // pipelined frames: the shade kernel follows the camera kernel on the side stream (set by
     // rt_set_post_stream), so the next frame's shading runs beside this frame's tracers;

@@ -116,6 +116,7 @@ int update_sky(rt_context* ctx) {
     const V3 sunDir = sun_direction(sp.timeOfDay, sp.sunAxisAngle);
     fr.sunDir[0] = sunDir.x; fr.sunDir[1] = sunDir.y; fr.sunDir[2] = sunDir.z;
     if (fr.skyValid && !sp.needRegenerate && sky_params_equal(sp, fr.lastSky)) return RT_OK;
+    if (fr.spec.valid) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->specDone, 0));  // they read the sky
     if (ctx->postStream) {  // frame pipelining: nothing may read the sky while it is rewritten
         const int rc = sync_streams(ctx, false);
         if (rc != RT_OK) return rc;
@@ -326,7 +327,23 @@ int sync_streams(rt_context* ctx, bool report) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->postStream) HIP_TRY(ctx, hipStreamSynchronize(ctx->postStream));
     poll_q3(ctx);
+    // camera rays a synchronous draw traced ahead are kept only up to the next draw: any call that
+    // waits for the streams (a read, a setter, a mode change) drops them
+    if (ctx->fr.spec.valid) {
+        ctx->fr.spec.valid = false;
+        ctx->fr.syncZeroed[ctx->fr.spec.block] = false;
+        HIP_TRY(ctx, hipMemset(ctx->fr.specRayCounter, 0, (size_t)kRayCounterSlots * kRayCounterStride * 8));
+    }
     return report ? check_device_status(ctx) : RT_OK;
+}
+
+// The end of a synchronous draw: its frame is complete (kernel.cu:393-397) once the context stream
+// is idle; the next frame's camera rays traced ahead may still run on the side stream
+static int sync_draw(rt_context* ctx) {
+    if (!ctx->fr.spec.valid) return sync_streams(ctx);
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    poll_q3(ctx);
+    return check_device_status(ctx);
 }
 
 // The last serial frame's queue-3 length (rt_path_trace's chain choice), if k_pt_resolve has
@@ -461,6 +478,7 @@ int rt_frame_init(rt_context* ctx) {
         ALLOC(ws.surface, (size_t)ctx->renderW * ctx->stripRows * 4);
         ALLOC(fr.camCount[0], kWsCounterWords * 4);
         ALLOC(fr.syncCount[1], kWsCounterWords * 4);
+        ALLOC(fr.syncCount[2], kWsCounterWords * 4);
         fr.syncCount[0] = fr.camCount[0];
         fr.camQ3[0] = ws.q3;
         fr.camQ4[0] = ws.q4;
@@ -632,23 +650,15 @@ int alloc_ws_slot(rt_context* ctx, int k, bool queues) {
     return rc;
 }
 
-}  // namespace
-
-int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
-    if (!ctx || frame_num < 1) return RT_ERR_ARG;
-    if (!ctx->inited) { ctx->err = "rt_path_trace before rt_init"; return RT_ERR_STATE; }
-    FrameResources& fr = ctx->fr;
-    if (ctx->postStream) {  // frame pipelining: trace into the set no denoise still reads
-        fr.gbSet = (fr.gbSet + 1) % kGbSets;
-        select_gbuffers(fr);
-        if (fr.setInFlight[fr.gbSet]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->postDone[fr.gbSet], 0));
-    }
-    int rc = update_sky(ctx);
-    if (rc != RT_OK) return rc;
-    HostCamera hc;
-    rt_camera_update(ctx->camera, ctx->renderW, ctx->renderH, hc);
-    if (frame_num == 1 || !fr.histValid) fr.hist = hist_of(hc);  // kernel.cu:133-136
-    PathTraceParams p;
+// The launch parameters of frame `frame_num`'s path trace into G-buffer / camera-output set g, with
+// that set's counter block (the serial frames' block, the stream plan and the bookkeeping are
+// rt_path_trace's).  Zero-filled first, so that two calls with the same state compare equal byte
+// for byte (the synchronous draws' camera rays traced ahead, launch_spec_camera).  Returns the
+// bounce-queue slot.
+int fill_pt_params(const rt_context* ctx, int frame_num, int with_detail, const HostCamera& hc, int g,
+                   PathTraceParams& p) {
+    const FrameResources& fr = ctx->fr;
+    memset(&p, 0, sizeof p);
     p.cam = rt_trace_camera(hc);
     p.tanHalfFov[0] = hc.tanHalfFov[0];
     p.tanHalfFov[1] = hc.tanHalfFov[1];
@@ -686,29 +696,20 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.cosThetaMax = fr.cosThetaMax;
     p.oneMinusCosThetaMax = 1.0f - fr.cosThetaMax;
     sun_frame(fr.sunDir, p.sunT, p.sunB);
-    p.colorOut = fr.color;
-    p.normalOut = fr.normal;
-    p.albedoOut = fr.albedo;
-    p.depthOut = fr.depth;
-    p.motionOut = fr.motion;
+    p.colorOut = fr.gColor[g];
+    p.normalOut = fr.gNormal[g];
+    p.albedoOut = fr.gAlbedo[g];
+    p.depthOut = fr.gDepth[g];
+    p.motionOut = fr.gMotion[g];
     p.raysOut = with_detail ? fr.rays : nullptr;
     p.statsOut = with_detail ? fr.ptStats : nullptr;
     p.rayCounter = fr.rayCounter;
     p.ws = fr.ws;
-    const int g = fr.gbSet;  // camera-output slot = G-buffer set
     p.ws.hit0Rec = fr.camHit0Rec[g];
     p.ws.hit0Err = fr.camHit0Err[g];
     p.ws.surface = fr.camSurface[g];
     p.ws.counters = fr.camCount[g];
-    if (!ctx->postStream) {  // serial frames: the counter block the previous frame's resolve zeroed
-        const int b = fr.syncIdx;
-        p.ws.counters = fr.syncCount[b];
-        p.ws.countersZeroed = fr.syncZeroed[b] ? 1 : 0;
-        p.ws.zeroNext = fr.syncCount[b ^ 1];
-        fr.syncZeroed[b] = fr.syncZeroed[b ^ 1] = false;  // until this frame's resolve is enqueued
-    }
     p.ws.fetch = p.ws.counters + 64;
-    fr.lastCounters = p.ws.counters;
     const int qs = fr.camQ3[g].rayO ? g : 0;  // bounce-queue slot: per set when allocated (shadeOnSide)
     p.ws.q3 = fr.camQ3[qs];
     p.ws.q4 = fr.camQ4[qs];
@@ -716,12 +717,79 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     p.ws.hitErr = fr.camHitErr[qs];
     p.ws.pathL = fr.camPathL[qs];
     p.ws.pending = fr.camPending[qs];
-    fr.lastSlot = qs;
     {  // material table (init.cu:215-251): only mirror / glass ids make steps 1-2 trace
         const int m = ctx->materialOverride;
         p.ws.glossy = m >= 0 && (m == 1 || m == 5 || m >= 10);
         p.ws.microfacet = m == 4;  // mat_type: only id 4 is MICROFACET, the reference table uses 3 / 6
     }
+    return qs;
+}
+
+// Synchronous draws trace the next frame's camera rays ahead (launch_spec_camera): one GPU, no
+// post stream, the G-buffer sets the context's own, [tuning] syncSpec
+bool spec_on(const rt_context* ctx) {
+    return ctx->tune.syncSpec && ctx->fr.specReady && !ctx->postStream && ctx->stripCount == 1 && !ctx->fr.gbBound;
+}
+
+// whether the camera and shade kernels launched with `a` wrote what ones launched with `b` would:
+// the same parameters but for those they do not read (or that only select the later kernels)
+bool spec_matches(const PathTraceParams& a, const PathTraceParams& b) {
+    PathTraceParams x = a, y = b;
+    for (PathTraceParams* q : {&x, &y}) {
+        q->rayCounter = nullptr;  // the launches ahead count into specRayCounter
+        // they read the LBVH set of the frame that launched them, the next frame reads the other:
+        // the geometry is fixed after rt_init, so both hold the same build (tests/test_gpu_bvh.py)
+        q->nodes = q->tlasNodes = nullptr;
+        q->triPos = nullptr;
+        q->triNrm = nullptr;
+        q->ws.traceBlocks = 0;
+        q->ws.countersZeroed = 0;
+        q->ws.chain = 0;
+        q->ws.q3HostOut = nullptr;
+        q->ws.q3Tag = 0;
+    }
+    return memcmp(&x, &y, sizeof x) == 0;
+}
+
+// PtLaunchHook of a synchronous frame whose successor's camera rays are traced ahead: after
+// kernel tune.specAfter (1 = shade) the gate they wait for
+hipError_t spec_hook(void* arg, int kernel) {
+    rt_context* ctx = (rt_context*)arg;
+    return kernel == ctx->tune.specAfter ? hipEventRecord(ctx->specGate, ctx->stream) : hipSuccess;
+}
+
+}  // namespace
+
+int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
+    if (!ctx || frame_num < 1) return RT_ERR_ARG;
+    if (!ctx->inited) { ctx->err = "rt_path_trace before rt_init"; return RT_ERR_STATE; }
+    FrameResources& fr = ctx->fr;
+    if (ctx->postStream) {  // frame pipelining: trace into the set no denoise still reads
+        fr.gbSet = (fr.gbSet + 1) % kGbSets;
+        select_gbuffers(fr);
+        if (fr.setInFlight[fr.gbSet]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->postDone[fr.gbSet], 0));
+    } else if (spec_on(ctx)) {  // synchronous frames alternate two sets: the next one's camera rays go ahead
+        fr.gbSet ^= 1;
+        select_gbuffers(fr);
+    }
+    int rc = update_sky(ctx);
+    if (rc != RT_OK) return rc;
+    HostCamera hc;
+    rt_camera_update(ctx->camera, ctx->renderW, ctx->renderH, hc);
+    if (frame_num == 1 || !fr.histValid) fr.hist = hist_of(hc);  // kernel.cu:133-136
+    const int g = fr.gbSet;  // camera-output slot = G-buffer set
+    PathTraceParams p;
+    const int qs = fill_pt_params(ctx, frame_num, with_detail, hc, g, p);
+    if (!ctx->postStream) {  // serial frames: the counter block the resolve before last zeroed
+        const int b = fr.syncIdx;
+        p.ws.counters = fr.syncCount[b];
+        p.ws.countersZeroed = fr.syncZeroed[b] ? 1 : 0;
+        p.ws.zeroNext = fr.syncCount[(b + 2) % 3];
+        p.ws.fetch = p.ws.counters + 64;
+        fr.syncZeroed[b] = fr.syncZeroed[(b + 2) % 3] = false;  // until this frame's resolve is enqueued
+    }
+    fr.lastCounters = p.ws.counters;
+    fr.lastSlot = qs;
     // the fused bounce chain shortens a serial frame; pipelined frames keep the four lean kernels,
     // beside which the next frame's camera waves fit (k_pt_chain's 168 VGPRs at 3 waves/SIMD leave
     // them no room); on ranks of 8 strips too, since the queue tracers' refill-free tail loops
@@ -732,6 +800,12 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     // resolve kernel, read in sync_streams: a fixed schedule, no event on the stream).
     poll_q3(ctx);
     p.ws.chain = fr.ws.chain == 2 || (fr.ws.chain == 1 && !ctx->postStream && fr.lastQ3 < kChainMaxQ3);
+    if (spec_on(ctx)) {  // beside the next frame's camera rays
+        if (ctx->tune.specChain >= 0) p.ws.chain = ctx->tune.specChain != 0;  // A/B aid
+        // fewer bounce-chain / queue-3 workgroups per CU leave the camera waves room beside them
+        // (synchronous draw 0.985 -> 0.972 ms at 2 per CU against 3)
+        if (ctx->tune.specTracePerCu > 0) p.ws.traceBlocks = fr.ws.cus * (uint32_t)ctx->tune.specTracePerCu;
+    }
     fr.lastChain = p.ws.chain && !p.ws.glossy && !p.ws.microfacet;  // as rtk_launch_pt_rest decides
     if (with_detail) {  // per-pixel counters: everything in order on the context stream
         if (ctx->postStream && (rc = sync_streams(ctx)) != RT_OK) return rc;
@@ -764,7 +838,24 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
     if (ringSlot)  // the slot's denoise pairs, recorded once here: a frame no rt_denoise_post follows
         for (int k = 2 * kPtKernels; k < 2 * kFrameKernels; ++k)  // reads 0 ms for them
             if (ctx->ptMarks[k]) HIP_TRY(ctx, hipEventRecord(ctx->ptMarks[k], cs));
-    HIP_TRY(ctx, rtk_launch_pt_camera(&p, cs, ctx->ptMarks));
+    // the camera rays traced ahead by the previous synchronous draw: used when this launch would
+    // write what they wrote, dropped otherwise; either way nothing after them runs before they end
+    bool reuse = false, reuseShade = false;
+    if (fr.spec.valid) {
+        fr.spec.valid = false;
+        HIP_TRY(ctx, hipStreamWaitEvent(cs, ctx->specDone, 0));
+        reuse = !side && spec_matches(p, fr.spec.p);
+        reuseShade = reuse && fr.spec.shade;
+        if (!reuse) p.ws.countersZeroed = 0;  // their counts are in the block: the launcher clears it
+        // their ray counts: into the frame's when used; the partial sums zeroed for the next ones
+        HIP_TRY(ctx, rtk_fold_ray_counts(reuse ? fr.rayCounter : nullptr, fr.specRayCounter, cs));
+    }
+    if (reuse) {
+        for (int k = 0; k < (reuseShade ? 4 : 2) && ctx->ptMarks; ++k)  // zero-length slots for the marks
+            if (ctx->ptMarks[k]) HIP_TRY(ctx, hipEventRecord(ctx->ptMarks[k], cs));
+    } else {
+        HIP_TRY(ctx, rtk_launch_pt_camera(&p, cs, ctx->ptMarks));
+    }
     // the shade kernel follows on the side stream, so it runs beside the previous frame's queue
     // tracers instead of after them (its bounce queues are this set's own, camQ3[g] ..)
     const bool shadeSide = side && ctx->shadeOnSide && qs == g;
@@ -786,14 +877,20 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
         p.ws.q3HostOut = fr.q3Host;  // stored by k_pt_resolve (no copy on the stream)
         p.ws.q3Tag = ++fr.q3Tag;
     }
+    PtLaunchHook shook{spec_hook, ctx};
     if (shadeSide) HIP_TRY(ctx, rtk_launch_pt_rest_after_shade(&p, ctx->stream, ctx->ptMarks, &hook));
-    else HIP_TRY(ctx, rtk_launch_pt_rest(&p, ctx->stream, ctx->ptMarks, ctx->postStream ? &hook : nullptr));
+    else if (reuseShade) HIP_TRY(ctx, rtk_launch_pt_rest_after_shade(&p, ctx->stream, ctx->ptMarks, &shook));
+    else {
+        const PtLaunchHook* h = ctx->postStream ? &hook : spec_on(ctx) && !with_detail ? &shook : nullptr;
+        HIP_TRY(ctx, rtk_launch_pt_rest(&p, ctx->stream, ctx->ptMarks, h));
+    }
     // pending only once the launches that store it are enqueued: a failed launch leaves the next
     // serial frame to ask again instead of freezing the chain choice
     if (askQ3) fr.q3Pending = true;
-    if (!ctx->postStream) {  // the other block is zeroed by this frame's resolve, enqueued above
-        fr.syncIdx ^= 1;
-        fr.syncZeroed[fr.syncIdx] = true;
+    if (!ctx->postStream) {  // block b + 2 is zeroed by this frame's resolve, enqueued above
+        const int b = fr.syncIdx;
+        fr.syncZeroed[(b + 2) % 3] = true;
+        fr.syncIdx = (b + 1) % 3;
     }
     if (ctx->postPending && (rc = issue_pending_post(ctx)) != RT_OK) return rc;
     if (ctx->postStream) {
@@ -1016,6 +1113,71 @@ int prebuild_next_bvh(rt_context* ctx) {
     return rc;
 }
 
+// Set 1's G-buffers and camera outputs and the events of the synchronous draws' camera rays traced
+// ahead (allocated at full size, once)
+int ensure_sync_spec(rt_context* ctx) {
+    FrameResources& fr = ctx->fr;
+    int rc;
+    const size_t P = (size_t)ctx->allocW * ctx->allocH;
+#define ALLOC(p, bytes) if (!(p) && (rc = dalloc(ctx, &(p), (bytes))) != RT_OK) return rc
+    ALLOC(fr.gColor[1], P * 8);
+    ALLOC(fr.gNormal[1], P * 8);
+    ALLOC(fr.gAlbedo[1], P * 8);
+    ALLOC(fr.gDepth[1], P * 2);
+    ALLOC(fr.gMotion[1], P * 4);
+#undef ALLOC
+    if ((rc = alloc_ws_slot(ctx, 1, true)) != RT_OK) return rc;  // with bounce queues: the shade goes ahead too
+    if (!fr.specRayCounter) {  // zero between uses (rtk_fold_ray_counts)
+        if ((rc = dalloc(ctx, &fr.specRayCounter, (size_t)kRayCounterSlots * kRayCounterStride * 8)) != RT_OK) return rc;
+        HIP_TRY(ctx, hipMemset(fr.specRayCounter, 0, (size_t)kRayCounterSlots * kRayCounterStride * 8));
+    }
+    for (hipEvent_t* e : {&ctx->specGate, &ctx->specDone})
+        if (!*e) HIP_TRY(ctx, hipEventCreateWithFlags(e, hipEventDisableTiming));
+    fr.specReady = true;
+    return RT_OK;
+}
+
+// Synchronous draws: the next frame's camera rays, traced ahead on the side stream after this
+// frame's shade kernel (spec_hook) and ahead of the next frame's LBVH build (prebuild_next_bvh), on
+// this frame's LBVH, into the other G-buffer set and the next counter block, with the camera, sky
+// and frame number as they are now.
+// They then run beside this frame's bounces and denoise instead of at the head of the next draw.
+// The next rt_path_trace uses them only when its own launch parameters equal these (spec_matches:
+// a host that moves the camera, changes the sky, the size or the frame number between the draws
+// gets them traced again), and any call that waits for the streams drops them, so no draw's output
+// depends on this.
+int launch_spec_camera(rt_context* ctx) {
+    FrameResources& fr = ctx->fr;
+    if (!ctx->tune.syncSpec || ctx->postStream || ctx->stripCount != 1 || fr.gbBound) return RT_OK;
+    int rc;
+    if (!fr.specReady && (rc = ensure_sync_spec(ctx)) != RT_OK) return rc;
+    HostCamera hc;
+    rt_camera_update(ctx->camera, ctx->renderW, ctx->renderH, hc);
+    PathTraceParams p;  // on this frame's LBVH set (spec_matches)
+    fill_pt_params(ctx, ctx->nextFrame, 0, hc, fr.gbSet ^ 1, p);
+    const int b = fr.syncIdx;
+    p.ws.counters = fr.syncCount[b];
+    p.ws.countersZeroed = fr.syncZeroed[b] ? 1 : 0;
+    p.ws.zeroNext = fr.syncCount[(b + 2) % 3];
+    p.ws.fetch = p.ws.counters + 64;
+    p.ws.shadeClaim = 1;  // as rt_path_trace sets it for synchronous frames
+    p.rayCounter = fr.specRayCounter;
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->sideStream, ctx->specGate, 0));
+    HIP_TRY(ctx, rtk_launch_pt_camera(&p, ctx->sideStream, nullptr));
+    // the shade kernel too when this frame's bounces run as the four lean kernels (a long queue 3,
+    // fr.lastChain false): beside the fused chain's 168-VGPR waves it finds no room and only
+    // delays the frame (synchronous draw 0.990 -> 0.997 ms; the terrain view 3.70 -> 3.53 ms)
+    const bool shade = ctx->tune.specShade == 2 || (ctx->tune.specShade == 1 && !fr.lastChain);
+    if (shade) HIP_TRY(ctx, rtk_launch_pt_shade(&p, ctx->sideStream, nullptr));
+    HIP_TRY(ctx, hipEventRecord(ctx->specDone, ctx->sideStream));
+    fr.syncZeroed[b] = false;
+    fr.spec.valid = true;
+    fr.spec.shade = shade;
+    fr.spec.block = b;
+    fr.spec.p = p;
+    return RT_OK;
+}
+
 // UpdateFrame (kernel.cu:61-137) + BuildBvhLevel1/2 + PathTrace + TemporalSpatialDenoising +
 // PostProcessing + CopyToOutput of one frame, enqueued (draw, kernel.cu:259-398); the RGBA8 image
 // goes to `target` (pitch in pixels) or, when NULL, to the context's own buffer
@@ -1034,6 +1196,8 @@ int enqueue_frame(rt_context* ctx, uint32_t* target, uint32_t pitch, bool hdr) {
         return rc;
     }
     if ((rc = rt_path_trace(ctx, frame, 0)) != RT_OK) return rc;
+    // the next frame's camera rays first on the side stream, then its LBVH (which only its bounces read)
+    if (!ctx->postStream && (rc = launch_spec_camera(ctx)) != RT_OK) return rc;
     if (!ctx->postStream && (rc = prebuild_next_bvh(ctx)) != RT_OK) return rc;
     ctx->fr.drawTarget = target;
     ctx->fr.drawPitch = pitch;
@@ -1050,7 +1214,7 @@ int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out) {
     if (!ctx->inited) { ctx->err = "rt_draw before rt_init"; return RT_ERR_STATE; }
     int rc;
     if ((rc = enqueue_frame(ctx, nullptr, 0, hdr_out != nullptr)) != RT_OK) return rc;
-    if ((rc = sync_streams(ctx)) != RT_OK) return rc;
+    if ((rc = sync_draw(ctx)) != RT_OK) return rc;
     if (rgba8_out && (rc = copy_rgba_out(ctx, rgba8_out)) != RT_OK) return rc;
     if (hdr_out)
         HIP_TRY(ctx, hipMemcpy(hdr_out, ctx->fr.hdr, (size_t)ctx->renderW * ctx->renderH * 16, hipMemcpyDeviceToHost));
@@ -1076,7 +1240,7 @@ int rt_draw_device(rt_context* ctx, void* rgba8_device, size_t pitch_bytes, int 
         if ((rc = rt_set_post_stream(ctx, ctx->ownPostStream)) != RT_OK) return rc;
     }
     if ((rc = enqueue_frame(ctx, (uint32_t*)rgba8_device, (uint32_t)(pitch_bytes / 4), false)) != RT_OK) return rc;
-    if (!(flags & RT_DRAW_ASYNC)) return sync_streams(ctx);  // draw ends with a device sync (kernel.cu:393-397)
+    if (!(flags & RT_DRAW_ASYNC)) return sync_draw(ctx);  // draw ends with a device sync (kernel.cu:393-397)
     return RT_OK;
 }
 
@@ -1167,7 +1331,7 @@ int rt_set_post_stream(rt_context* ctx, void* stream) {
     if (rc != RT_OK) return rc;
     FrameResources& fr = ctx->fr;
     for (int k = 0; k < kGbSets; ++k) fr.setInFlight[k] = false;
-    fr.syncZeroed[0] = fr.syncZeroed[1] = false;  // pipelined frames use (and dirty) camCount[0] too
+    fr.syncZeroed[0] = fr.syncZeroed[1] = fr.syncZeroed[2] = false;  // pipelined frames use (and dirty) camCount[0] too
     if (!stream) {
         ctx->postStream = nullptr;
         return RT_OK;
@@ -1254,6 +1418,7 @@ int rt_bind_buffer(rt_context* ctx, int name, void* device_ptr, size_t bytes) {
         }
         default: ctx->err = "rt_bind_buffer: this buffer cannot be bound"; return RT_ERR_ARG;
     }
+    fr.gbBound = true;  // synchronous frames then stay in their set (no camera rays traced ahead)
     if (set == fr.gbSet) select_gbuffers(fr);
     return RT_OK;
 }

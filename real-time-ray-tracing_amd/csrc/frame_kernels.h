@@ -278,6 +278,10 @@ extern "C" hipError_t rtk_launch_pt_rest(const PathTraceParams* p, hipStream_t s
 // camera kernel on another stream; rtk_launch_pt_rest_after_shade then enqueues trace<3> ..
 // resolve and calls the hook for kernel 1 first, with nothing enqueued for it.
 extern "C" hipError_t rtk_launch_pt_shade(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks);
+// dst[k * kRayCounterStride] += src[k * kRayCounterStride] over the kRayCounterSlots slots (the
+// ray counts of kernels launched ahead, folded into the frame's when it uses them), then src = 0;
+// dst null: only the zeroing
+extern "C" hipError_t rtk_fold_ray_counts(unsigned long long* dst, unsigned long long* src, hipStream_t stream);
 extern "C" hipError_t rtk_launch_pt_rest_after_shade(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks,
                                                      const PtLaunchHook* hook);
 extern "C" int rtk_trace_queue_blocks_per_cu();

@@ -1195,6 +1195,20 @@ __global__ __launch_bounds__(256) void k_pt_resolve(PathTraceParams P) {
 }
 
 
+// src is zeroed for the next launches ahead; dst null: zero src only (they were dropped)
+__global__ __launch_bounds__(256) void k_fold_ray_counts(unsigned long long* dst, unsigned long long* src) {
+    const int k = (int)threadIdx.x;
+    if (k >= kRayCounterSlots) return;
+    if (dst) dst[k * kRayCounterStride] += src[k * kRayCounterStride];
+    src[k * kRayCounterStride] = 0ull;
+}
+
+extern "C" hipError_t rtk_fold_ray_counts(unsigned long long* dst, unsigned long long* src, hipStream_t stream) {
+    static_assert(kRayCounterSlots <= 256, "one workgroup");
+    hipLaunchKernelGGL(k_fold_ray_counts, dim3(1), dim3(256), 0, stream, dst, src);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t rtk_launch_pt_camera(const PathTraceParams* p, hipStream_t stream, hipEvent_t* marks) {
     if (p->spp < 1 || p->spp > 64 || p->ws.persistBlocks < 1) return hipErrorInvalidValue;
     if ((size_t)p->rows * p->width >= (1u << 26) || (size_t)p->rows * p->width * p->spp > p->ws.cap)

@@ -315,3 +315,50 @@ def test_bound_accumulation_keeps_the_list_chain(rtx, tmp_path):
     for f, (a, b) in enumerate(zip(outs[0][0], outs[1][0]), start=1):
         assert np.array_equal(a, b), "frame %d" % f
     assert np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_sync_draws_trace_camera_rays_ahead(rtx, tmp_path):
+    """A synchronous draw traces the next frame's camera rays ahead, beside its own bounces and
+    denoise (frame.cpp launch_spec_camera), and the next draw uses them only when its launch
+    parameters equal theirs.  A sequence that moves the camera, changes the sky, reads a buffer,
+    resets the frame index, and draws into host memory between device draws — each of which makes
+    the next draw trace its camera rays again — against the same sequence with [tuning] syncSpec
+    off: every frame's RGBA8, and the ray count, identical."""
+    import torch
+
+    w, h, frames = 192, 112, 12
+    outs = []
+    for spec in (False, True):
+        cfg = rtx.write_config(str(tmp_path / ("sp%d.toml" % spec)), w, h, spp=2, tuning={"syncSpec": spec})
+        rt = rtx.RayTracer(w, h, cfg).init()
+        rt.set_delta_time(16.667)
+        target = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda:0")
+        imgs = []
+        for f in range(1, frames + 1):
+            if f == 3:
+                cam = rt.camera
+                cam.yaw += 0.05
+                rt.camera = cam
+            if f == 5:
+                p = rt.params
+                p.sky.timeOfDay += 0.02
+                rt.params = p
+            if f == 7:
+                rt.get_buffer("DEPTH")
+            if f == 9:
+                rt.set_frame_index(4)
+            if f == 11:
+                rgba = np.zeros((h, w, 4), np.uint8)
+                rt.draw(rgba)
+                imgs.append(rgba.reshape(-1).copy())
+                continue
+            rt.draw_device(target.data_ptr(), 0)
+            imgs.append(target.cpu().numpy().copy())
+        rays = rt.ray_count()
+        info = rt.info()
+        rt.cleanup()
+        outs.append((imgs, rays, info.gbufferSet))
+    for f, (a, b) in enumerate(zip(outs[0][0], outs[1][0]), start=1):
+        assert np.array_equal(a, b), "frame %d" % f
+    assert outs[0][1] == outs[1][1]
+    assert outs[0][2] == 0 and outs[1][2] in (0, 1)  # the sets alternate with the camera rays traced ahead

@@ -119,6 +119,7 @@ struct FrameResources {
     bool specReady = false;          // set 1's buffers and the events exist (ensure_sync_spec)
     bool gbBound = false;            // a G-buffer is the caller's (rt_bind_buffer): no set rotation
     unsigned long long* specRayCounter = nullptr;  // the rays of the launches ahead (folded in when used)
+    int specCounts = 0;  // specRayCounter holds: 0 nothing, 1 the counts of used launches (to fold), 2 dropped ones
     bool camInFlight[kGbSets] = {};
     // ... and the bounce queues with their hit records, one slot per set when the shade kernel
     // runs on the side stream (shadeOnSide: frame f+1's shade appends to its queues while frame

@@ -329,10 +329,16 @@ int sync_streams(rt_context* ctx, bool report) {
     poll_q3(ctx);
     // camera rays a synchronous draw traced ahead are kept only up to the next draw: any call that
     // waits for the streams (a read, a setter, a mode change) drops them
-    if (ctx->fr.spec.valid) {
-        ctx->fr.spec.valid = false;
-        ctx->fr.syncZeroed[ctx->fr.spec.block] = false;
-        HIP_TRY(ctx, hipMemset(ctx->fr.specRayCounter, 0, (size_t)kRayCounterSlots * kRayCounterStride * 8));
+    FrameResources& fr = ctx->fr;
+    if (fr.spec.valid) {
+        fr.spec.valid = false;
+        fr.syncZeroed[fr.spec.block] = false;
+        fr.specCounts = 2;
+    }
+    if (fr.specCounts) {  // the ray counts of launches ahead: the used ones into the frame's
+        HIP_TRY(ctx, rtk_fold_ray_counts(fr.specCounts == 1 ? fr.rayCounter : nullptr, fr.specRayCounter, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        fr.specCounts = 0;
     }
     return report ? check_device_status(ctx) : RT_OK;
 }
@@ -847,8 +853,7 @@ int rt_path_trace(rt_context* ctx, int frame_num, int with_detail) {
         reuse = !side && spec_matches(p, fr.spec.p);
         reuseShade = reuse && fr.spec.shade;
         if (!reuse) p.ws.countersZeroed = 0;  // their counts are in the block: the launcher clears it
-        // their ray counts: into the frame's when used; the partial sums zeroed for the next ones
-        HIP_TRY(ctx, rtk_fold_ray_counts(reuse ? fr.rayCounter : nullptr, fr.specRayCounter, cs));
+        fr.specCounts = reuse ? 1 : 2;  // folded into the frame's (or cleared) ahead of the next ones
     }
     if (reuse) {
         for (int k = 0; k < (reuseShade ? 4 : 2) && ctx->ptMarks; ++k)  // zero-length slots for the marks
@@ -1162,6 +1167,10 @@ int launch_spec_camera(rt_context* ctx) {
     p.ws.fetch = p.ws.counters + 64;
     p.ws.shadeClaim = 1;  // as rt_path_trace sets it for synchronous frames
     p.rayCounter = fr.specRayCounter;
+    if (fr.specCounts) {  // the last launches' ray counts: into the frame's if they were used, then cleared
+        HIP_TRY(ctx, rtk_fold_ray_counts(fr.specCounts == 1 ? fr.rayCounter : nullptr, fr.specRayCounter, ctx->sideStream));
+        fr.specCounts = 0;
+    }
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->sideStream, ctx->specGate, 0));
     HIP_TRY(ctx, rtk_launch_pt_camera(&p, ctx->sideStream, nullptr));
     // the shade kernel too when this frame's bounces run as the four lean kernels (a long queue 3,

@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(256) void k_pt_resolve(PathTraceParams P) {
 __global__ __launch_bounds__(256) void k_fold_ray_counts(unsigned long long* dst, unsigned long long* src) {
     const int k = (int)threadIdx.x;
     if (k >= kRayCounterSlots) return;
-    if (dst) dst[k * kRayCounterStride] += src[k * kRayCounterStride];
+    if (dst) atomicAdd(&dst[k * kRayCounterStride], src[k * kRayCounterStride]);  // beside a frame's own counts
     src[k * kRayCounterStride] = 0ull;
 }
 

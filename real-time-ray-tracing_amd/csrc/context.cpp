@@ -341,7 +341,8 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
         t.syncSpec = rttoml::find_or_bool(doc, "tuning", "syncSpec", true);
         t.specChain = rttoml::find_or_int(doc, "tuning", "specChain", -1);
         t.specAfter = rttoml::find_or_int(doc, "tuning", "specAfter", 1);
-        t.specShade = rttoml::find_or_int(doc, "tuning", "specShade", 1);
+        t.specShade = rttoml::find_or_int(doc, "tuning", "specShade", 2);
+        t.specShadePerCu = rttoml::find_or_int(doc, "tuning", "specShadePerCu", 2);
         t.specTracePerCu = rttoml::find_or_int(doc, "tuning", "specTracePerCu", 2);
     }
     if (ctx->screenW <= 0 || ctx->screenH <= 0 || ctx->screenW > 16384 || ctx->screenH > 16384 || ctx->spp < 1 ||

@@ -227,7 +227,8 @@ struct rt_context {
         bool syncSpec = true;   // synchronous draws trace the next frame's camera rays ahead
         int specChain = -1;     // ... and their bounces with the fused chain (1), the four kernels (0) or by queue 3's length (-1)
         int specAfter = 1;      // ... the next camera rays after kernel k of this frame (1 shade, 2 trace<3>, ..)
-        int specShade = 1;      // ... and the next frame's shade kernel after them: 0 never, 1 beside the lean kernels, 2 always
+        int specShade = 2;      // ... and the next frame's shade kernel after them: 0 never, 1 beside the lean kernels, 2 always
+        int specShadePerCu = 2; // ... that shade kernel's grid per CU (0: its residency)
         int specTracePerCu = 2; // ... this frame's bounce chain / queue-3 tracer at so many workgroups per CU (0: as usual)
     } tune;
 

@@ -749,6 +749,7 @@ bool spec_matches(const PathTraceParams& a, const PathTraceParams& b) {
         q->triPos = nullptr;
         q->triNrm = nullptr;
         q->ws.traceBlocks = 0;
+        q->ws.shadeBlocksPerCu = 0;  // the shade's grid (dynamic claims: the same result on any grid)
         q->ws.countersZeroed = 0;
         q->ws.chain = 0;
         q->ws.q3HostOut = nullptr;
@@ -1173,11 +1174,14 @@ int launch_spec_camera(rt_context* ctx) {
     }
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->sideStream, ctx->specGate, 0));
     HIP_TRY(ctx, rtk_launch_pt_camera(&p, ctx->sideStream, nullptr));
-    // the shade kernel too when this frame's bounces run as the four lean kernels (a long queue 3,
-    // fr.lastChain false): beside the fused chain's 168-VGPR waves it finds no room and only
-    // delays the frame (synchronous draw 0.990 -> 0.997 ms; the terrain view 3.70 -> 3.53 ms)
+    // then the next frame's shade kernel, which runs beside this frame's denoise (synchronous draw
+    // 0.969 -> 0.945 ms, the terrain view 3.70 -> 3.33 ms), on 2 workgroups per CU so that the
+    // denoise passes' workgroups fit beside it (0.942 -> 0.935 ms)
     const bool shade = ctx->tune.specShade == 2 || (ctx->tune.specShade == 1 && !fr.lastChain);
-    if (shade) HIP_TRY(ctx, rtk_launch_pt_shade(&p, ctx->sideStream, nullptr));
+    if (shade) {
+        if (ctx->tune.specShadePerCu > 0) p.ws.shadeBlocksPerCu = (uint32_t)ctx->tune.specShadePerCu;
+        HIP_TRY(ctx, rtk_launch_pt_shade(&p, ctx->sideStream, nullptr));
+    }
     HIP_TRY(ctx, hipEventRecord(ctx->specDone, ctx->sideStream));
     fr.syncZeroed[b] = false;
     fr.spec.valid = true;

@@ -115,9 +115,11 @@ def denoise_bytes(st, Ws, Hs):
         # also into the accumulation buffer
         "k_temporal": 28 * P + 12 * S + 8 * (P - A7),
         "k_spatial7": int((apron7 + 8 + 2) * A7),  # list 0: apron, out, the noise epilogue's depth
-        "k_spatial5<3>": 26 * A5,                 # list 1: colour, normal, depth in, colour out
+        # list 1: colour, normal, depth in, colour out; the first pass also writes the last pass's
+        # output for the tiles off list 1 (accumulation and albedo in, colour out)
+        "k_spatial5<3>": 26 * A5 + 24 * (P - A5),
         "k_spatial5<6>": 26 * A5,
-        "k_spatial5<12>": 24 * P + 10 * A5,       # every tile: colour, albedo in, colour out (+ normal, depth)
+        "k_spatial5<12>": 34 * A5,                # list 1: colour, normal, depth, albedo in, colour out
         "k_temporal2": 28 * P,                    # colour, motion, history in, history out
         "k_downscale_chain": 8 * P + P // 2 + P // 32,  # colour in, 1/4 and 1/16 levels out
         "k_scale_post": 8 * P + 12 * Ws * Hs,     # render colour in, scaled half4 + RGBA8 out
@@ -302,14 +304,20 @@ def valu_issue_us(insts):
 
 
 # the denoise kernels' HIP-event names (by position in the chain) -> their PMC names when the frame
-# runs the active-tile-list chain: the list kernels replace the full-frame ones
-PMC_LIST_NAMES = {"k_spatial7": "k_spatial7_list", "k_spatial5<3>": "k_spatial5_list<3>",
-                  "k_spatial5<6>": "k_spatial5_list<6>"}
+# runs the active-tile-list chain: the list kernels (two threads per pixel since
+# round 6, one before) replace the full-frame ones
+PMC_LIST_NAMES = {"k_spatial7": ("k_spatial7_list2", "k_spatial7_list"),
+                  "k_spatial5<3>": ("k_spatial5_list2<3>", "k_spatial5_list<3>"),
+                  "k_spatial5<6>": ("k_spatial5_list2<6>", "k_spatial5_list<6>"),
+                  "k_spatial5<12>": ("k_spatial5_list2<12>",)}
 
 
 def pmc_entry(pmc, k):
     ks = pmc.get("kernels", {})
-    return ks.get(PMC_LIST_NAMES.get(k, k)) or ks.get(k)
+    for name in PMC_LIST_NAMES.get(k, ()) + (k,):
+        if ks.get(name):
+            return ks[name]
+    return None
 
 
 def add_pmc(e, k, pmc, workload_matches):

@@ -45,7 +45,10 @@ typedef struct rt_context rt_context;
  * streams ("cumask" | "prio"), tracePerCu / trace4PerCu (0: automatic), trace3ShortPerCu (a short queue
  * 3's workgroups per CU on one GPU; 0: all of them), chain ("serial" | "off" |
  * "always"), shadeOnSide (bool), shadeBlocksPerCu (synchronous frames; 0: the kernel's residency),
- * overlapAfter / cameraAfter (-1: automatic).  [debug] (fault
+ * overlapAfter / cameraAfter (-1: automatic); the synchronous draws' launches ahead (rt_draw):
+ * syncSpec (bool), specAfter (the kernel of this frame they follow: 1 shade), specShade (0 / 1 / 2:
+ * the shade kernel never / beside the lean bounce kernels / always), specShadePerCu, specTracePerCu,
+ * specChain (-1: by queue 3's length).  [debug] (fault
  * injection, tests): bvhSkipPublish, bvhSkipPublishBuilds, bvhWaitMs.  The library reads no
  * environment variables. */
 int rt_create(int screen_width, int screen_height, const char* config_toml, rt_context** out);
@@ -63,7 +66,13 @@ int rt_init(rt_context* ctx);
  * frame.  rgba8_out (screen W*H*4) and hdr_out (render W*H*4 floats, pre-tone-map HDR) may
  * each be NULL.  With [optimziation] useDynamicResolution the render size follows the frame
  * time from the second frame on (rt_get_info's renderWidth/Height); size hdr_out for
- * maxWidth x maxHeight. */
+ * maxWidth x maxHeight.
+ * Synchronous draws (this one, and rt_draw_device without RT_DRAW_ASYNC) on one GPU launch the
+ * next frame's camera-ray and shade kernels ahead, beside this frame's bounces and denoise, into
+ * the other G-buffer set ([tuning] syncSpec): the draw still returns with its frame complete, and
+ * those kernels may still run on the context's side stream.  The next draw uses their results only
+ * when its launch parameters (camera, sky, size, frame number, materials, buffers) equal theirs;
+ * any call that waits for the streams (rt_sync, the reads, the setters) discards them first. */
 int rt_draw(rt_context* ctx, uint8_t* rgba8_out, float* hdr_out);
 
 /* RayTracer::draw(SurfObj* renderTarget), kernel.cu:259-398 (CopyToOutput kernel.cu:26-59 writes

@@ -50,8 +50,13 @@ def short(name, grid, wg):
     return n
 
 
+# a denoise pass's kernel when the frame runs the active-tile-list chain (bench.py PMC_LIST_NAMES)
+LIST_NAMES = {"k_spatial7": ("k_spatial7_list2", "k_spatial7_list"), "k_spatial5<3>": ("k_spatial5_list2<3>", "k_spatial5_list<3>"),
+              "k_spatial5<6>": ("k_spatial5_list2<6>", "k_spatial5_list<6>"), "k_spatial5<12>": ("k_spatial5_list2<12>",)}
+
 # kernels whose reads are 8-byte half4 texels (the denoiser and the post chain)
-HALF4_KERNELS = set(DENOISE) | {"k_spatial7_list", "k_spatial5_list<3>", "k_spatial5_list<6>", "k_tile_noise",
+HALF4_KERNELS = set(DENOISE) | {"k_spatial7_list", "k_spatial5_list<3>", "k_spatial5_list<6>", "k_spatial7_list2",
+                                "k_spatial5_list2<3>", "k_spatial5_list2<6>", "k_spatial5_list2<12>", "k_tile_noise",
                                 "k_noise16", "k_downscale4", "k_histogram", "k_bloom_gauss", "k_bloom_apply",
                                 "k_lens_flare", "k_hdr_out"}
 # tools/probe/fetch_calib.hip: bytes each way per dispatch
@@ -156,7 +161,9 @@ def main():
         kernels[k] = e
     res = {"workload_key": key, "workload": workload, "passes": dirs, "kernels": kernels,
            "stage_hbm_bytes": sum(kernels[k].get("hbm_bytes", 0) for k in STAGE if k in kernels) or None,
-           "denoise_hbm_bytes": sum(kernels[k].get("hbm_bytes", 0) for k in DENOISE if k in kernels) or None,
+           "denoise_hbm_bytes": sum(kernels[k].get("hbm_bytes", 0) for k in
+                                    (next((n for n in LIST_NAMES.get(d, ()) + (d,) if n in kernels), None)
+                                     for d in DENOISE) if k) or None,
            "correction": ("FETCH_SIZE x the calibrated factor of the kernel's access width (--calib: 8-byte half4 "
                           "reads for the denoise / post kernels, 16-byte otherwise), KB x 1024" if calib else
                           "FETCH_SIZE doubled (gfx950 counts half the bytes of wide reads), KB x 1024"),

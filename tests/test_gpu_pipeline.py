@@ -362,3 +362,33 @@ def test_sync_draws_trace_camera_rays_ahead(rtx, tmp_path):
         assert np.array_equal(a, b), "frame %d" % f
     assert outs[0][1] == outs[1][1]
     assert outs[0][2] == 0 and outs[1][2] in (0, 1)  # the sets alternate with the camera rays traced ahead
+
+
+@pytest.mark.parametrize("material", [5, 4])
+def test_sync_draws_ahead_with_glossy_materials(rtx, tmp_path, material):
+    """The launches ahead of synchronous draws with the mirror (5) and microfacet (4) materials
+    ([render] materialOverride: the glossy shade kernel traces inline, the bounces run as the four
+    kernels), and a camera move in between: every frame equal to draws without them."""
+    import torch
+
+    w, h, frames = 160, 96, 6
+    outs = []
+    for spec in (False, True):
+        cfg = rtx.write_config(str(tmp_path / ("g%d%d.toml" % (material, spec))), w, h, spp=2,
+                               extra="materialOverride = %d\n" % material, tuning={"syncSpec": spec})
+        rt = rtx.RayTracer(w, h, cfg).init()
+        rt.set_delta_time(16.667)
+        target = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda:0")
+        imgs = []
+        for f in range(1, frames + 1):
+            if f == 4:
+                cam = rt.camera
+                cam.pos[1] += 0.1
+                rt.camera = cam
+            rt.draw_device(target.data_ptr(), 0)
+            imgs.append(target.cpu().numpy().copy())
+        outs.append((imgs, rt.ray_count()))
+        rt.cleanup()
+    for f, (a, b) in enumerate(zip(outs[0][0], outs[1][0]), start=1):
+        assert np.array_equal(a, b), "frame %d" % f
+    assert outs[0][1] == outs[1][1]

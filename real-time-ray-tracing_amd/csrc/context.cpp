@@ -344,6 +344,8 @@ int rt_create(int screen_width, int screen_height, const char* config_toml, rt_c
         t.specShade = rttoml::find_or_int(doc, "tuning", "specShade", 2);
         t.specShadePerCu = rttoml::find_or_int(doc, "tuning", "specShadePerCu", 2);
         t.specTracePerCu = rttoml::find_or_int(doc, "tuning", "specTracePerCu", 2);
+        t.dnSplit = rttoml::find_or_int(doc, "tuning", "dnSplit", 0);
+        t.dnFold = rttoml::find_or_int(doc, "tuning", "dnFold", 0) != 0;
     }
     if (ctx->screenW <= 0 || ctx->screenH <= 0 || ctx->screenW > 16384 || ctx->screenH > 16384 || ctx->spp < 1 ||
         ctx->spp > 64 || ctx->chunkDim < 1 || ctx->chunkDim > 8 ||

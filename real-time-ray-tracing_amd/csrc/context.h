@@ -230,6 +230,8 @@ struct rt_context {
         int specShade = 2;      // ... and the next frame's shade kernel after them: 0 never, 1 beside the lean kernels, 2 always
         int specShadePerCu = 2; // ... that shade kernel's grid per CU (0: its residency)
         int specTracePerCu = 2; // ... this frame's bounce chain / queue-3 tracer at so many workgroups per CU (0: as usual)
+        int dnSplit = 0;        // the denoise list passes at two threads per pixel: 0 never, 1 synchronous frames, 2 always
+        bool dnFold = false;    // the last a-trous pass over list 1 only, its other tiles written by the first
     } tune;
 
     std::string err;

@@ -982,19 +982,39 @@ __global__ DN5_BOUNDS void k_spatial5(DenoisePostParams P, const uint2* in, uint
     out[p] = res;
 }
 
+// ApplyAlbedo over `alt` into `out` for tile b of rows [P.cty0, P.cty1) when it is off list 1 (kCopy
+// of the list kernels below: what the last a-trous pass would pass through for that tile)
+RT_DEV void copy_off_list_tile(const DenoisePostParams& P, const uint2* alt, uint2* out, int W, int H, int W16) {
+    const uint32_t t = (uint32_t)P.cty0 * (uint32_t)W16 + blockIdx.x;
+    const int CX = (int)(t % (uint32_t)W16), CY = (int)(t / (uint32_t)W16);
+    if (CY < P.cty1 && h2f(P.noise16[t]) < P.dn.noise_threshold_large) {
+        const int x = CX * 16 + (int)(threadIdx.x & 15u), y = CY * 16 + (int)(threadIdx.x >> 4);
+        if (x < W && y < H) {
+            const size_t p = (size_t)y * W + x;
+            out[p] = pack_color(rgb_of(alt[p]) * rgb_of(P.albedo[p]), 0x3C00u);  // w = half(1.0)
+        }
+    }
+}
+
 // SpatialFilterGlobal5x5<S> over active-tile list 1 only (tile rows outside [ty0, ty1) are skipped):
-// `out` is written in those tiles only
-template <int S, bool kRcp, bool kRedirect, bool kPk = false>
+// `out` is written in those tiles only.  kAlbedo / kCopy: as k_spatial5_list2 below
+template <int S, bool kRcp, bool kRedirect, bool kPk = false, bool kAlbedo = false, bool kCopy = false>
 __global__ DN5_BOUNDS void k_spatial5_list(DenoisePostParams P, const uint2* in, uint2* out, const uint2* alt) {
     DN_PRIO();
     const int W = (int)P.W, H = (int)P.H, W16 = (W + 15) / 16;
+    if (kCopy) copy_off_list_tile(P, alt, out, W, H, W16);
     uint32_t tile;
     if (!list_tile(P, 1, tile)) return;
     const int TX = (int)(tile % (uint32_t)W16), TY = (int)(tile / (uint32_t)W16);
     if (TY < P.ty0 || TY >= P.ty1) return;
     const uint32_t act = kRedirect ? active_neighbourhood(P, TX, TY) : 0u;
     const int x = TX * 16 + (threadIdx.x & 15), y = TY * 16 + (threadIdx.x >> 4);
-    if (x < W && y < H) out[(size_t)y * W + x] = spatial5_pixel<S, kRcp, kRedirect, kPk>(P, in, alt, act, x, y, TX, TY);
+    if (x < W && y < H) {
+        uint2 res = spatial5_pixel<S, kRcp, kRedirect, kPk>(P, in, alt, act, x, y, TX, TY);
+        const size_t p = (size_t)y * W + x;
+        if (kAlbedo) res = pack_color(rgb_of(res) * rgb_of(P.albedo[p]), 0x3C00u);  // w = half(1.0)
+        out[p] = res;
+    }
 }
 
 // k_spatial5_list with two threads per pixel (spatial5_tile_split).  kAlbedo: the last a-trous pass
@@ -1008,17 +1028,7 @@ __global__ __launch_bounds__(512) void k_spatial5_list2(DenoisePostParams P, con
     DN_PRIO();
     __shared__ float sX[(25 - kS5Split) * 256];
     const int W = (int)P.W, H = (int)P.H, W16 = (W + 15) / 16;
-    if (kCopy && threadIdx.x < 256) {
-        const uint32_t t = (uint32_t)P.cty0 * (uint32_t)W16 + blockIdx.x;
-        const int CX = (int)(t % (uint32_t)W16), CY = (int)(t / (uint32_t)W16);
-        if (CY < P.cty1 && h2f(P.noise16[t]) < P.dn.noise_threshold_large) {
-            const int x = CX * 16 + (int)(threadIdx.x & 15u), y = CY * 16 + (int)(threadIdx.x >> 4);
-            if (x < W && y < H) {
-                const size_t p = (size_t)y * W + x;
-                out[p] = pack_color(rgb_of(alt[p]) * rgb_of(P.albedo[p]), 0x3C00u);  // w = half(1.0)
-            }
-        }
-    }
+    if (kCopy && threadIdx.x < 256) copy_off_list_tile(P, alt, out, W, H, W16);
     uint32_t tile;
     if (!list_tile(P, 1, tile)) return;
     const int TX = (int)(tile % (uint32_t)W16), TY = (int)(tile / (uint32_t)W16);
@@ -1710,7 +1720,7 @@ __global__ __launch_bounds__(256) void k_hdr_out(const uint2* color, float4* hdr
 template <int S, bool kRedirect, bool kAlbedo = false, bool kCopy = false>
 static void launch_s5_list(bool rcp, bool pk, dim3 g, hipStream_t s, const DenoisePostParams& Q, const uint2* in,
                            uint2* out, const uint2* alt) {
-    if (kDnSplit) {  // two threads per pixel (spatial5_tile_split)
+    if (kDnSplit && Q.listSplit) {  // two threads per pixel (spatial5_tile_split)
         const dim3 b2(512);
         if (rcp && pk) hipLaunchKernelGGL((k_spatial5_list2<S, true, kRedirect, true, kAlbedo, kCopy>), g, b2, 0, s, Q, in, out, alt);
         else if (rcp) hipLaunchKernelGGL((k_spatial5_list2<S, true, kRedirect, false, kAlbedo, kCopy>), g, b2, 0, s, Q, in, out, alt);
@@ -1719,10 +1729,10 @@ static void launch_s5_list(bool rcp, bool pk, dim3 g, hipStream_t s, const Denoi
         return;
     }
     const dim3 b(256);
-    if (rcp && pk) hipLaunchKernelGGL((k_spatial5_list<S, true, kRedirect, true>), g, b, 0, s, Q, in, out, alt);
-    else if (rcp) hipLaunchKernelGGL((k_spatial5_list<S, true, kRedirect, false>), g, b, 0, s, Q, in, out, alt);
-    else if (pk) hipLaunchKernelGGL((k_spatial5_list<S, false, kRedirect, true>), g, b, 0, s, Q, in, out, alt);
-    else hipLaunchKernelGGL((k_spatial5_list<S, false, kRedirect, false>), g, b, 0, s, Q, in, out, alt);
+    if (rcp && pk) hipLaunchKernelGGL((k_spatial5_list<S, true, kRedirect, true, kAlbedo, kCopy>), g, b, 0, s, Q, in, out, alt);
+    else if (rcp) hipLaunchKernelGGL((k_spatial5_list<S, true, kRedirect, false, kAlbedo, kCopy>), g, b, 0, s, Q, in, out, alt);
+    else if (pk) hipLaunchKernelGGL((k_spatial5_list<S, false, kRedirect, true, kAlbedo, kCopy>), g, b, 0, s, Q, in, out, alt);
+    else hipLaunchKernelGGL((k_spatial5_list<S, false, kRedirect, false, kAlbedo, kCopy>), g, b, 0, s, Q, in, out, alt);
 }
 
 // k_scale_post's footprint of 18 screen texels along an axis spans at most 17 * r + 5 render
@@ -1929,10 +1939,11 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
             DN_MARK(1, 0);
             if (useList) {  // list 0 only; TemporalFilter wrote the other tiles into the accumulation buffer
                 const dim3 b512(512);
-                if (kDnSplit && rcp7 && pk7) hipLaunchKernelGGL((k_spatial7_list2<true, true>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
-                else if (kDnSplit && rcp7) hipLaunchKernelGGL((k_spatial7_list2<true, false>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
-                else if (kDnSplit && pk7) hipLaunchKernelGGL((k_spatial7_list2<false, true>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
-                else if (kDnSplit) hipLaunchKernelGGL((k_spatial7_list2<false, false>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
+                const bool split = kDnSplit && Q.listSplit;
+                if (split && rcp7 && pk7) hipLaunchKernelGGL((k_spatial7_list2<true, true>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
+                else if (split && rcp7) hipLaunchKernelGGL((k_spatial7_list2<true, false>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
+                else if (split && pk7) hipLaunchKernelGGL((k_spatial7_list2<false, true>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
+                else if (split) hipLaunchKernelGGL((k_spatial7_list2<false, false>), gList, b512, 0, s, Q, (const uint2*)cur, dst);
                 else if (rcp7 && pk7) hipLaunchKernelGGL((k_spatial7_list<true, true>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
                 else if (rcp7) hipLaunchKernelGGL((k_spatial7_list<true, false>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
                 else if (pk7) hipLaunchKernelGGL((k_spatial7_list<false, true>), gList, b256, 0, s, Q, (const uint2*)cur, dst);
@@ -1963,9 +1974,9 @@ extern "C" hipError_t rtk_denoise_phase(DenoisePostParams* P, hipStream_t s, int
         uint2* a = cur == P->colorA ? P->colorB : cur == P->colorB ? P->colorA : spare;
         uint2* b = a == P->colorA ? P->colorB : P->colorA;
         const uint2* alt = cur;
-        // the list chain with two threads per pixel: the first pass also finishes the tiles off
-        // list 1 for the last (k_spatial5_list2 kCopy), which then runs over list 1 only
-        const bool fold = useList && kDnSplit;
+        // folded list chain ([tuning] dnFold): the first pass also finishes the tiles off list 1
+        // for the last (kCopy), which then runs over list 1 only with ApplyAlbedo in its store
+        const bool fold = useList && (P->listFold || (kDnSplit && P->listSplit));
         int c0 = 0, c1 = 0;
         tile_range(P, 1, c0, c1);
         if (tiles(3, Q, g)) {

@@ -988,6 +988,11 @@ int rt_denoise_post(rt_context* ctx, int frame_num, int with_hdr) {
     {  // multi-GPU strip-local denoise: only with a collective hook, and for the passes it covers
         uint32_t a = 0, b = p.H;
         p.stripLocal = strip_local_denoise(ctx, a, b) ? 1 : 0;
+        // the list passes at two threads per pixel ([tuning] dnSplit: 0 never, 1 synchronous frames
+        // only, 2 always): in pipelined frames their 512-thread workgroups wait for room beside the
+        // next frame's camera and shade waves (A/B in DESIGN.md §4.2)
+        p.listSplit = ctx->tune.dnSplit == 2 || (ctx->tune.dnSplit == 1 && !ctx->postStream) ? 1 : 0;
+        p.listFold = ctx->tune.dnFold ? 1 : 0;
         p.rowA = a;
         p.rowB = b;
     }

@@ -234,6 +234,8 @@ struct DenoisePostParams {
     uint32_t tileCap;           // tiles the lists can hold (16x16 tiles of the allocated render size)
     int tileParity;             // this frame's counter set (the other one is zeroed by TemporalFilter)
     int listUsed;               // out (phase 0 / 2): the chain ran over the lists; the host flips tileParity
+    int listSplit;              // the list passes at two threads per pixel (512-thread workgroups, denoise.hip)
+    int listFold;               // the last a-trous pass over list 1 only (the first finishes the other tiles)
     float rcpDepth[3];          // RN(1 / sigma_depth) of TemporalFilter, SpatialFilter7x7, the a-trous passes
     int rcpDepthOk;             // bit k: that sigma is in rt_div_rcp's range (else the taps divide)
     hipEvent_t* marks;          // optional, host side only: 2 * kDnKernels events, marks[2k] / [2k + 1]

@@ -69,6 +69,20 @@ def test_pipelined_chain_modes_match_serial(rtx, tmp_path, chain):
         assert np.array_equal(ref[k], got[k]), k
 
 
+@pytest.mark.parametrize("tuning", [{"dnFold": 1}, {"dnSplit": 2}, {"dnSplit": 2, "dnFold": 1}],
+                         ids=["fold", "split", "split-fold"])
+def test_denoise_list_variants_match_default(rtx, tmp_path, tuning):
+    """The a-trous list passes at two threads per pixel ([tuning] dnSplit, k_spatial5_list2 /
+    k_spatial7_list2) and the folded chain ([tuning] dnFold: the last pass over list 1 only, its
+    other tiles written by the first) against the default kernels: identical outputs, serial and
+    pipelined."""
+    ref, _, _ = run(rtx, tmp_path, False, False)
+    for pipelined in (False, True):
+        got, _, _ = run(rtx, tmp_path, pipelined, False, tuning=tuning)
+        for k in ref:
+            assert np.array_equal(ref[k], got[k]), (pipelined, k)
+
+
 def test_sync_on_null_stream_then_other_stream(rtx, oracle, tmp_path, default_scene):
     """rt_sync with the renderer on the null stream (set_stream(0), torch's default stream) must
     still issue the deferred denoise and wait for every renderer stream: G-buffers bound as torch

@@ -76,6 +76,14 @@ RT_DEV F3 ycocg_inv(F3 c) {
 
 RT_DEV F3 rgb_of(uint2 q) { return f3(h2f(q.x & 0xFFFFu), h2f(q.x >> 16), h2f(q.y & 0xFFFFu)); }
 RT_DEV uint32_t mask_of(uint2 q) { return q.y >> 16; }
+// rgb_of(q) * w, each product one mixed-precision fma (v_fma_mix_f32, no conversion instruction):
+// fmaf(c, w, +0) rounds the exact product once, as the multiply does, and differs from it only
+// for a -0 product (+0 then).  Only for sums that start at +0, which are never -0, so that adding
+// either zero gives the same sum.
+RT_DEV F3 rgb_mul(uint2 q, float w) {
+    return f3(__builtin_fmaf(h2f(q.x & 0xFFFFu), w, 0.0f), __builtin_fmaf(h2f(q.x >> 16), w, 0.0f),
+              __builtin_fmaf(h2f(q.y & 0xFFFFu), w, 0.0f));
+}
 RT_DEV uint2 pack_color(F3 c, uint32_t mask) {
     return make_uint2(f2h(c.x) | (f2h(c.y) << 16), f2h(c.z) | (mask << 16));
 }
@@ -1603,38 +1611,48 @@ __global__ __launch_bounds__(kScaleThreads) void k_scale_post(DenoisePostParams 
     const int x = tile_x(P) * 16 + (threadIdx.x & 15), y = tile_y(P) * 16 + (threadIdx.x >> 4);
     const BnPixel bnp = bn_pixel(P.bluenoise, x, y);
     bn_stage_sobol(P.bluenoise, sSobol, (int)threadIdx.x, kScaleThreads);
-    // render texels the 18x18 output apron reads (t1 is monotone in x and y)
-    const int ix0 = clampi(scale_t1(clampi(X0, 0, Ws - 1), Ws, W) - 1, 0, W - 1);
-    const int ix1 = clampi(scale_t1(clampi(X0 + 17, 0, Ws - 1), Ws, W) + 2, 0, W - 1);
-    const int iy0 = clampi(scale_t1(clampi(Y0, 0, Hs - 1), Hs, H) - 1, 0, H - 1);
-    const int iy1 = clampi(scale_t1(clampi(Y0 + 17, 0, Hs - 1), Hs, H) + 2, 0, H - 1);
-    const int TW = ix1 - ix0 + 1, TH = iy1 - iy0 + 1;
+    // Wave 0 evaluates the apron's 18 columns and 18 rows (lanes 0-17 x, 18-35 y; bicubic_axis:
+    // the x weights and tap columns depend on the apron column only, the y ones on the row only),
+    // and from the first taps of its end columns / rows the render texels the 18x18 apron reads (t1
+    // is monotone in x and y) — once per workgroup instead of in every wave
+    __shared__ float sW[2][18][4];
+    __shared__ int sT[2][18][4];  // tap column within the tile / tap row offset (row * TW)
+    __shared__ int sB[4];         // ix0, iy0, TW, TH
+    const int t = threadIdx.x;
+    if (t < 64) {
+        const int ax = t < 18 ? 0 : 1, k = t < 36 ? t - 18 * ax : 17;
+        const int S = ax ? Hs : Ws, R = ax ? H : W, O = ax ? Y0 : X0;
+        float w[4];
+        const int t1 = bicubic_axis(clampi(O + k, 0, S - 1), S, R, w);
+        const int ix0 = clampi(__builtin_amdgcn_readlane(t1, 0) - 1, 0, W - 1);
+        const int ix1 = clampi(__builtin_amdgcn_readlane(t1, 17) + 2, 0, W - 1);
+        const int iy0 = clampi(__builtin_amdgcn_readlane(t1, 18) - 1, 0, H - 1);
+        const int iy1 = clampi(__builtin_amdgcn_readlane(t1, 35) + 2, 0, H - 1);
+        const int TW = ix1 - ix0 + 1;
+        if (t < 36) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                sT[ax][k][i] = ax ? (clampi(t1 - 1 + i, 0, H - 1) - iy0) * TW : clampi(t1 - 1 + i, 0, W - 1) - ix0;
+                sW[ax][k][i] = w[i];
+            }
+        }
+        if (t == 0) {
+            sB[0] = ix0;
+            sB[1] = iy0;
+            sB[2] = TW;
+            sB[3] = iy1 - iy0 + 1;
+        }
+    }
+    __syncthreads();
+    const int ix0 = __builtin_amdgcn_readfirstlane(sB[0]), iy0 = __builtin_amdgcn_readfirstlane(sB[1]);
+    const int TW = __builtin_amdgcn_readfirstlane(sB[2]), TH = __builtin_amdgcn_readfirstlane(sB[3]);
     const bool staged = TW * TH <= kLds;
-    if (staged)
-        for (int i = threadIdx.x; i < TW * TH; i += kScaleThreads) sIn[i] = render[(size_t)(iy0 + i / TW) * W + ix0 + i % TW];
+    if (staged) {  // rows of 32 lanes (no division by TW)
+        for (int r = t >> 5; r < TH; r += kScaleThreads / 32)
+            for (int c = t & 31; c < TW; c += 32) sIn[r * TW + c] = render[(size_t)(iy0 + r) * W + ix0 + c];
+    }
     __syncthreads();
     if (staged) {
-        // the x weights and tap columns depend on the apron column only, the y ones on the row
-        // only: 36 axis evaluations instead of 2 per texel, same arithmetic (bicubic_axis)
-        __shared__ float sW[2][18][4];
-        __shared__ int sT[2][18][4];  // tap column within the tile / tap row offset (row * TW)
-        const int t = threadIdx.x;
-        if (t < 36) {
-            const int ax = t / 18, k = t % 18;
-            float w[4];
-            if (ax == 0) {
-                const int t1 = bicubic_axis(clampi(X0 + k, 0, Ws - 1), Ws, W, w);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) sT[0][k][i] = clampi(t1 - 1 + i, 0, W - 1) - ix0;
-            } else {
-                const int t1 = bicubic_axis(clampi(Y0 + k, 0, Hs - 1), Hs, H, w);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) sT[1][k][j] = (clampi(t1 - 1 + j, 0, H - 1) - iy0) * TW;
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) sW[ax][k][i] = w[i];
-        }
-        __syncthreads();
         for (int i = threadIdx.x; i < 18 * 18; i += kScaleThreads) {
             const int cx = i % 18, ry = i / 18;
             F3 o = f3(0.0f);
@@ -1645,7 +1663,7 @@ __global__ __launch_bounds__(kScaleThreads) void k_scale_post(DenoisePostParams 
                 for (int k = 0; k < 4; ++k) {  // the loop order of bicubic_scale_px
                     const float w = sW[0][cx][k] * sW[1][ry][j];
                     sw += w;
-                    o = o + rgb_of(sIn[sT[1][ry][j] + sT[0][cx][k]]) * w;
+                    o = o + rgb_mul(sIn[sT[1][ry][j] + sT[0][cx][k]], w);
                 }
             o = o / sw;
             sS[i] = pack_color(o, 0x3C00u);

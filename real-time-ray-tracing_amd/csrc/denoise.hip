@@ -121,7 +121,7 @@ RT_DEV F3 smooth_sum(const SmoothTaps& t, const uint2* q) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         sw += t.wt[i];
-        o = o + rgb_of(q[i]) * t.wt[i];
+        o = o + rgb_mul(q[i], t.wt[i]);
     }
     return o / sw;
 }
@@ -1394,7 +1394,7 @@ RT_DEV uint2 bicubic_scale_px(const Img& im, int W, int H, int x, int y, int Ws,
         for (int i = 0; i < 4; ++i) {
             const float w = wx[i] * wy[j];
             sw += w;
-            o = o + rgb_of(im.at(t1x - 1 + i, t1y - 1 + j)) * w;
+            o = o + rgb_mul(im.at(t1x - 1 + i, t1y - 1 + j), w);
         }
     o = o / sw;
     return pack_color(o, 0x3C00u);
@@ -1502,7 +1502,7 @@ RT_DEV F3 catmull_rom(const View2& im, F2 uv) {
         for (int i = 0; i < 4; ++i) {
             const float w = wx[i] * wy[j];
             sw += w;
-            o = o + rgb_of(im.at(t1x - 1 + i, t1y - 1 + j)) * w;
+            o = o + rgb_mul(im.at(t1x - 1 + i, t1y - 1 + j), w);
         }
     return o / sw;
 }

@@ -797,6 +797,7 @@ def main():
     on_l2 = dom in per
     peak = L2_PEAK_GBS if on_l2 else HBM_PEAK_GBS
     a = d["achieved_GBs"]
+    vi = frame_valu_issue(list(per) + list(dn), ms_per_step, pmc, matches)
     result["roofline"] = {
         "bound": "l2" if on_l2 else "hbm", "limiter": "latency",
         "kernel": dom, "kernel_ms": d["ms"], "algorithmic_bytes": d["algorithmic_bytes"],
@@ -815,7 +816,12 @@ def main():
                     "HBM; its time is the noise-gated tiles' stencil arithmetic and its waves' wait for issue slots "
                     "beside the next frame's path-trace waves (valu_busy_frac: share of wave time issuing VALU)")),
         "kernels": dict(per, **dn),
-        "valu_issue": frame_valu_issue(list(per) + list(dn), ms_per_step, pmc, matches),
+        "valu_issue": vi,
+        # what binds the whole frame, as against the named kernel's memory roofline above
+        "frame_limiter": ({"resource": "VALU issue", "frac": vi["frac"],
+                           "note": "the frame's VALU wave-instructions at 4 cycles each on 1024 SIMDs need this share "
+                                   "of ms_per_step (valu_issue); the memory rooflines of its kernels are far from peak"}
+                          if vi and vi.get("frac") is not None else None),
         "denoise_gating": dst,
         "stage": {"kernels": " -> ".join(per), "algorithmic_bytes": stage_bytes, "sum_kernel_ms": round(stage_ms, 5),
                   "achieved_GBs": round(stage_bytes / (stage_ms * 1e-3) / 1e9, 1),

@@ -49,8 +49,8 @@ typedef struct rt_context rt_context;
  * syncSpec (bool), specAfter (the kernel of this frame they follow: 1 shade), specShade (0 / 1 / 2:
  * the shade kernel never / beside the lean bounce kernels / always), specShadePerCu, specTracePerCu,
  * specChain (-1: by queue 3's length); the denoise list passes: dnSplit (0 / 1 / 2: two threads per
- * pixel never / in synchronous frames / always), dnFold (bool: the last a-trous pass over list 1 only,
- * DESIGN.md §4.2).  [debug] (fault
+ * pixel never / in synchronous frames / always; default 0), dnFold (bool, default false: the last
+ * a-trous pass over list 1 only).  [debug] (fault
  * injection, tests): bvhSkipPublish, bvhSkipPublishBuilds, bvhWaitMs.  The library reads no
  * environment variables. */
 int rt_create(int screen_width, int screen_height, const char* config_toml, rt_context** out);
